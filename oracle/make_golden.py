@@ -1,0 +1,311 @@
+"""Generate the golden fixtures under tests/golden/ from the REFERENCE itself.
+
+TEST INFRASTRUCTURE ONLY — run in the build container (it reads /root/reference,
+which does not exist on the GPU box).  The committed .npz files are data: inputs
+plus the reference's outputs; no reference source is copied into the repo.
+
+How the reference is run:
+  * GP_scripts.py lines 1-142 (myKernel, getMean, getCov, nonDivK, compute_K,
+    compute_Ks, sqExp, rbf) are exec'd unmodified from the file text.  The rest of
+    that file is Python-2-only (print statement at GP_scripts.py:173).
+  * The GP_laser.laser() posterior recipe (GP_laser.py:113-140) and the split
+    (GP_laser.py:80-96) are reproduced by calling those exec'd functions with the
+    same numpy expressions the script uses.  GP_laser.py itself cannot be imported
+    (py2 syntax, geopy/pyproj missing, interp_ALL_2016_2_7.pkl missing).
+  * krig.getGrid (krig.py:648-678) is exec'd from the file text with its two
+    py2 `print 'here x'` statements replaced by `pass` (no other change).
+  * krig.scikit_prior's model (krig.py:174-194) runs on the installed
+    scikit-learn (1.7.2; the reference pins no version).
+  * simulTracks.pkl supplies realistic drifter coordinates.  It is loaded with a
+    restricted unpickler that allows only numpy array reconstruction and the
+    laser_class.interpolated_tracks container.
+
+Usage:  python oracle/make_golden.py [--out tests/golden]
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import pickle
+import time
+
+import numpy as np
+
+REF = "/root/reference"
+
+
+def load_gp_scripts():
+    with open(os.path.join(REF, "GP_scripts.py")) as f:
+        lines = f.readlines()
+    src = "".join(lines[:142])
+    ns: dict = {}
+    exec(compile(src, "GP_scripts.py[1:142]", "exec"), ns)
+    return ns
+
+
+def load_get_grid():
+    with open(os.path.join(REF, "krig.py")) as f:
+        lines = f.readlines()
+    body = lines[647:678]  # krig.py:648-678
+    fixed = []
+    for ln in body:
+        if ln.strip().startswith("print "):
+            ind = ln[: len(ln) - len(ln.lstrip())]
+            fixed.append(ind + "pass\n")
+        else:
+            fixed.append(ln)
+    ns = {"np": np}
+    exec(compile("".join(fixed), "krig.py[648:678]", "exec"), ns)
+    return ns["getGrid"]
+
+
+class _Tracks:
+    pass
+
+
+class _RestrictedUnpickler(pickle.Unpickler):
+    def find_class(self, module, name):
+        if module == "laser_class" and name == "interpolated_tracks":
+            return _Tracks
+        if module in ("numpy.core.multiarray", "numpy._core.multiarray") and name in ("_reconstruct", "scalar"):
+            import numpy.core.multiarray as m
+            return getattr(m, name)
+        if module == "numpy" and name in ("ndarray", "dtype"):
+            return getattr(np, name)
+        raise pickle.UnpicklingError(f"blocked global {module}.{name}")
+
+
+def load_tracks():
+    with open(os.path.join(REF, "simulTracks.pkl"), "rb") as f:
+        return _RestrictedUnpickler(f, encoding="latin1").load()
+
+
+def project_km(lat, lon, lat0=28.69, lon0=-88.28):
+    """Signed local equirectangular projection (the reference's geopy/pyproj projections
+    are unavailable and simLaser's is unsigned)."""
+    R = 6371.0
+    x = R * np.cos(np.deg2rad(lat0)) * np.deg2rad(lon - lon0)
+    y = R * np.deg2rad(lat - lat0)
+    return x, y
+
+
+def synthetic_tracks(n, seed=2016, box=(60.0, 45.0), amp=1.0, L=15.0, noise_sd=0.05):
+    """SURVEY.md §8(d) synthetic inputs (also used by bench.py through gp2d.data)."""
+    rng = np.random.default_rng(seed)
+    x = rng.uniform(0, box[0], n)
+    y = rng.uniform(0, box[1], n)
+    x0, y0 = box[0] / 2, box[1] / 2
+    psi = amp * np.exp(-((x - x0) ** 2 + (y - y0) ** 2) / L ** 2)
+    u = psi * (-2 * (y - y0) / L ** 2)       # u = dψ/dy
+    v = -psi * (-2 * (x - x0) / L ** 2)      # v = -dψ/dx
+    u = u + rng.normal(0, noise_sd, n)
+    v = v + rng.normal(0, noise_sd, n)
+    return x, y, u, v
+
+
+def gen_small(gs, out):
+    """compute_K / compute_Ks / getCov / getMean on tiny problems, all three divFree kinds,
+    plus the vectorised myKernel (mixed)."""
+    rng = np.random.default_rng(7)
+    N = 16
+    x1 = rng.uniform(0, 3, N)
+    x2 = rng.uniform(0, 3, N)
+    g = np.linspace(-0.5, 3.5, 8)
+    X1s, X2s = np.meshgrid(g, g)
+    x1s, x2s = X1s.reshape(-1), X2s.reshape(-1)
+    u = rng.normal(0, 1, N)
+    v = rng.normal(0, 1, N)
+    y = np.concatenate([u, v])[:, None]
+    noise = 0.01
+    sigma = 0.7
+    d = dict(x1=x1, x2=x2, x1s=x1s, x2s=x2s, y=y[:, 0], sigma=sigma, noise=noise)
+    for kind in (0, 1, 2):
+        K = gs["compute_K"](x1, x2, sigma, kind)
+        Ks = gs["compute_Ks"](x1, x2, x1s, x2s, sigma, kind)
+        Kss = gs["compute_K"](x1s, x2s, sigma, kind)
+        Ky = K + np.identity(K.shape[0]) * noise          # GP_laser.py:114-115
+        Ki = np.linalg.inv(Ky)                           # GP_laser.py:118
+        Cov = Kss - np.dot(Ks, np.dot(Ki, Ks.T))         # GP_laser.py:129
+        M = x1s.size
+        f = gs["getMean"](Ks, Ki, y)                     # GP_laser.py:134
+        d[f"K_{kind}"] = K
+        d[f"Ks_{kind}"] = Ks
+        d[f"Kssdiag_{kind}"] = np.diag(Kss)
+        d[f"mean_{kind}"] = f
+        d[f"uvar_{kind}"] = np.diag(Cov[:M, :M])
+        d[f"vvar_{kind}"] = np.diag(Cov[M:, M:])
+        if kind != 0:   # divFree=0 broadcasts one scalar into all 4 entries: singular without noise
+            ML, _, _ = gs["getCov"](x1, x2, x1s, x2s, sigma, kind)   # noise-free getCov (GP_scripts.py:48-54)
+            d[f"getCov_diag_{kind}"] = np.diag(ML)
+    # vectorised mixed kernel (GP_scripts.py:6-42)
+    xa = np.stack([x1, x2], 1)
+    xb = np.stack([x1s, x2s], 1)
+    d["myK_mixed_aa"] = gs["myKernel"](xa, xa, 0.7, 1.1, 0.3)
+    d["myK_mixed_ab"] = gs["myKernel"](xa, xb, 0.7, 1.1, 0.3)
+    d["myK_params"] = np.array([0.7, 1.1, 0.3])
+    np.savez_compressed(os.path.join(out, "gp_scripts_small.npz"), **d)
+
+
+def gen_laser(gs, out):
+    """GP_laser.laser() posterior (GP_laser.py:80-140) with the reference's loop kernels,
+    on simulTracks coordinates: 384 drifters × 2 time steps, stride-3 split."""
+    tr = load_tracks()
+    ts = 10
+    lat = tr.lat[:384, ts:ts + 2].reshape(-1)
+    lon = tr.lon[:384, ts:ts + 2].reshape(-1)
+    xo, yo = project_km(lat, lon)
+    uo = tr.u[:384, ts:ts + 2].reshape(-1)
+    vo = tr.v[:384, ts:ts + 2].reshape(-1)
+    xo = xo - xo.min() + 2                                  # GP_laser.py:77-78
+    yo = yo - yo.min() + 2
+    n_raw = xo.size
+    samples = np.arange(0, xo.size, 3)                      # GP_laser.py:81-83 (verbatim)
+    test = set(np.arange(xo.size)) - set(samples)
+    test = np.array(list(test))
+    xt, yt, ut, vt = xo[test], yo[test], uo[test], vo[test]
+    xo, yo, uo, vo = xo[samples], yo[samples], uo[samples], vo[samples]
+    obs = np.concatenate([uo, vo])
+    obs = np.reshape(obs, [obs.size, 1])
+    dx = 1.0   # the script uses 0.5; a coarser grid keeps the O(M²) Kss loop tractable
+    x = np.arange(np.min([xo.min(), xt.min()]) - 5, np.max([xo.max(), xt.max()]) + 5, dx)
+    y = np.arange(np.min([yo.min(), yt.min()]) - 5, np.max([yo.max(), yt.max()]) + 5, dx)
+    X, Y = np.meshgrid(x, y)
+    Xs = np.reshape(X, [X.size])
+    Ys = np.reshape(Y, [Y.size])
+    l_df, l_cf, rate, noise = 5.0, 5.0, 0.5, 0.0025
+    t0 = time.time()
+    K = rate * gs["compute_K"](xo, yo, l_df, 1) + (1 - rate) * gs["compute_K"](xo, yo, l_cf, 2)
+    Ko = np.identity(np.size(K, 0)) * noise
+    K = K + Ko
+    Ki = np.linalg.inv(K)
+    Ks = rate * gs["compute_Ks"](xo, yo, Xs, Ys, l_df, 1) + (1 - rate) * gs["compute_Ks"](xo, yo, Xs, Ys, l_cf, 2)
+    Kst = rate * gs["compute_Ks"](xo, yo, xt, yt, l_df, 1) + (1 - rate) * gs["compute_Ks"](xo, yo, xt, yt, l_cf, 2)
+    Kss = rate * gs["compute_K"](Xs, Ys, l_df, 1) + (1 - rate) * gs["compute_K"](Xs, Ys, l_cf, 2)
+    Cov = Kss - np.dot(Ks, np.dot(Ki, Ks.T))
+    uvar = np.reshape(np.diag(Cov[:X.size, :X.size]), [y.size, -1])
+    vvar = np.reshape(np.diag(Cov[X.size:, X.size:]), [y.size, -1])
+    f = gs["getMean"](Ks, Ki, obs)
+    uf = np.reshape(f[:f.size // 2], [y.size, -1])
+    vf = np.reshape(f[f.size // 2:], [y.size, -1])
+    ft = gs["getMean"](Kst, Ki, obs)
+    print(f"  laser recipe N={xo.size} M={Xs.size}: {time.time() - t0:.1f}s")
+    np.savez_compressed(os.path.join(out, "laser_mixed_N256.npz"),
+                        n_raw=n_raw, samples=samples, test=test,
+                        xo=xo, yo=yo, uo=uo, vo=vo, xt=xt, yt=yt, ut=ut, vt=vt,
+                        x=x, y=y, l_df=l_df, l_cf=l_cf, rate=rate, noise=noise,
+                        uf=uf, vf=vf, uvar=uvar, vvar=vvar,
+                        uft=ft[:ft.size // 2], vft=ft[ft.size // 2:],
+                        K_rowsum=K.sum(1), K_trace=np.trace(K))
+
+
+def gen_mykernel(gs, out):
+    """Vectorised-myKernel posterior (GP_scripts.py:6-46 with the GP_laser.py:113-131 recipe),
+    N=1024 synthetic tracks, mixed α=0.5, 32×32 grid."""
+    x, y, u, v = synthetic_tracks(1024)
+    xa = np.stack([x, y], 1)
+    gx = np.linspace(-5, 65, 32)
+    gy = np.linspace(-5, 50, 32)
+    GX, GY = np.meshgrid(gx, gy)
+    xg = np.stack([GX.reshape(-1), GY.reshape(-1)], 1)
+    M = xg.shape[0]
+    l_df, l_cf, rate, noise = 5.0, 5.0, 0.5, 0.0025
+    K = gs["myKernel"](xa, xa, l_df, l_cf, rate)
+    K = K + np.identity(K.shape[0]) * noise
+    Ki = np.linalg.inv(K)
+    Ks = gs["myKernel"](xg, xa, l_df, l_cf, rate)
+    obs = np.concatenate([u, v])[:, None]
+    f = gs["getMean"](Ks, Ki, obs)
+    kssd = np.diag(gs["myKernel"](xg, xg, l_df, l_cf, rate))
+    q = np.einsum("ij,ij->i", Ks, Ks @ Ki)
+    var = kssd - q
+    rows = np.array([0, 1, 511, 1023, 1024, 2047])
+    np.savez_compressed(os.path.join(out, "mykernel_mixed_N1024.npz"),
+                        x=x, y=y, u=u, v=v, xg=xg, l_df=l_df, l_cf=l_cf, rate=rate, noise=noise,
+                        mean=f, var=var, K_rows_idx=rows, K_rows=K[rows], K_rowsum=K.sum(1),
+                        Ks_rows=Ks[[0, 5, M, M + 5]])
+    # a div-free variant at the same size (the headline kernel)
+    K = gs["myKernel"](xa, xa, l_df, l_cf, 1.0) + np.identity(2 * xa.shape[0]) * noise
+    Ki = np.linalg.inv(K)
+    Ks = gs["myKernel"](xg, xa, l_df, l_cf, 1.0)
+    f = gs["getMean"](Ks, Ki, obs)
+    var = np.diag(gs["myKernel"](xg, xg, l_df, l_cf, 1.0)) - np.einsum("ij,ij->i", Ks, Ks @ Ki)
+    np.savez_compressed(os.path.join(out, "mykernel_divfree_N1024.npz"),
+                        x=x, y=y, u=u, v=v, xg=xg, l_df=l_df, noise=noise, mean=f, var=var)
+
+
+def gen_sklearn(out):
+    """Config A: krig.scikit_prior's model (krig.py:174-194) on 3-D (T,Y,X) inputs, N=128,
+    32×32 grid at one time slice."""
+    from sklearn.gaussian_process import GaussianProcessRegressor, kernels
+    rng = np.random.default_rng(11)
+    N = 128
+    X = np.stack([rng.uniform(0, 6, N), rng.uniform(0, 20, N), rng.uniform(-5, 15, N)], 1)
+    u = np.sin(X[:, 1] / 4) * np.cos(X[:, 2] / 5) + 0.1 * X[:, 0] / 6 + rng.normal(0, 0.05, N)
+    HP = np.array([0.8, 3.0, 4.0, 5.0, 0.2, 10.0, 1.5, 2.0, 0.004])   # var1,lt,ly,lx,var2,lt,ly,lx,noise
+    k = HP[0] * kernels.RBF(length_scale=[HP[1], HP[2], HP[3]])
+    k = k + HP[4] * kernels.RBF(length_scale=[HP[5], HP[6], HP[7]])
+    k = k + kernels.WhiteKernel(noise_level=HP[-1])
+    model = GaussianProcessRegressor(kernel=k, optimizer=None)
+    model.fit(X, u[:, None])
+    yg = np.linspace(1, 15, 32)
+    xg = np.linspace(-5, 15, 32)
+    Yg, Tg, Xg = np.meshgrid(yg, np.array([3.0]), xg)
+    Xp = np.concatenate([Tg.reshape(-1, 1), Yg.reshape(-1, 1), Xg.reshape(-1, 1)], 1)
+    U, Ustd = model.predict(Xp, return_std=True)
+    np.savez_compressed(os.path.join(out, "sklearn_ard_N128.npz"), X=X, u=u, HP=HP, Xp=Xp,
+                        mean=np.asarray(U).reshape(-1), std=np.asarray(Ustd).reshape(-1))
+
+
+def gen_indices(out):
+    """Split index arrays, verbatim reference expression (GP_laser.py:81-83, krig.py:335-337)."""
+    sizes = list(range(30, 40)) + list(range(128, 140)) + [257, 1000, 1031, 3000, 12288]
+    d = {}
+    for step in (2, 3, 5):
+        for n in sizes:
+            samples = np.arange(0, n, step)
+            test = set(np.arange(n)) - set(samples)
+            test = np.array(list(test))
+            d[f"test_{step}_{n}"] = test.astype(np.int64)
+    d["sizes"] = np.array(sizes)
+    np.savez_compressed(os.path.join(out, "split_indices.npz"), **d)
+
+
+def gen_grids(out):
+    getGrid = load_get_grid()
+    rng = np.random.default_rng(3)
+    d = {}
+    cases = [
+        dict(to=rng.uniform(0, 6, 50), yo=rng.uniform(0, 20, 50), xo=rng.uniform(-5, 15, 50), dt=1.0, dx=0.7, xL=40, yL=40),
+        dict(to=rng.uniform(0, 3, 40), yo=rng.uniform(-30, 30, 40), xo=rng.uniform(0, 70, 40), dt=0.5, dx=1.3, xL=40, yL=40),
+        dict(to=np.array([12.0, 13.0]), ylim_case=True, yo=np.array([1.0, 15.0]), xo=np.array([-5.0, 15.0]), dt=1.0, dx=0.5, xL=40, yL=40),
+    ]
+    for i, c in enumerate(cases):
+        c.pop("ylim_case", None)
+        X, tg, yg, xg = getGrid(c["to"], c["yo"], c["xo"], c["dt"], c["dx"], c["xL"], c["yL"])
+        for k, v in c.items():
+            d[f"c{i}_{k}"] = np.asarray(v)
+        d[f"c{i}_X"], d[f"c{i}_tg"], d[f"c{i}_yg"], d[f"c{i}_xg"] = X, tg, yg, xg
+    d["ncases"] = np.array(len(cases))
+    np.savez_compressed(os.path.join(out, "grids.npz"), **d)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=os.path.join(os.path.dirname(__file__), "..", "tests", "golden"))
+    ap.add_argument("--only", default="")
+    a = ap.parse_args()
+    os.makedirs(a.out, exist_ok=True)
+    gs = load_gp_scripts()
+    jobs = dict(small=lambda: gen_small(gs, a.out), laser=lambda: gen_laser(gs, a.out),
+                mykernel=lambda: gen_mykernel(gs, a.out), sklearn=lambda: gen_sklearn(a.out),
+                indices=lambda: gen_indices(a.out), grids=lambda: gen_grids(a.out))
+    for name, fn in jobs.items():
+        if a.only and name not in a.only.split(","):
+            continue
+        t = time.time()
+        fn()
+        print(f"{name}: {time.time() - t:.1f}s")
+
+
+if __name__ == "__main__":
+    main()
