@@ -1,0 +1,165 @@
+// assemble.hpp — covariance assembly kernels.
+//
+// Replaces the reference's kernel builders:
+//   GP_scripts.myKernel      GP_scripts.py:6-42   (vectorised mixed df/cf kernel)
+//   GP_scripts.nonDivK       GP_scripts.py:57-69  (one 2×2 block, divFree ∈ {0,1,2})
+//   GP_scripts.compute_K/_Ks GP_scripts.py:74-123 (component-major 2×2 layout)
+//   myKernel.{myKernel,nonDivK,nonRotK}.K   myKernel.py:27-53, 159-176, 255-271
+//   sklearn RBF(ARD)+White as built in krig.scikit_prior   krig.py:174-180
+//
+// One thread evaluates one (row point i, column point j) pair and writes its
+// 2×2 block into the four component blocks; a wave covers 64 consecutive
+// column points, so every store is a coalesced 512-byte row segment.  Work is
+// exp-bound VALU; HBM traffic is the 32 B per pair written.
+#pragma once
+#include "common.hpp"
+#include "../../include/gp2d.h"
+
+namespace gp2d {
+
+struct VecParams {
+  int kind;
+  double il_df2, il_cf2;  // 1/ℓ²
+  double l_df2;           // ℓ² (scalar kind: the σ² factor of GP_scripts.py:68)
+  double ratio, cratio;   // ratio, 1 − ratio
+  int same_len;           // ℓ_df == ℓ_cf: one exp serves both parts
+};
+
+struct ArdParams {
+  int dim, nterms;
+  double var[2];
+  double ils[2][3];  // 1/ls
+};
+
+inline VecParams make_vec_params(const gp2d_kernel_t* k) {
+  VecParams p;
+  p.kind = k->kind;
+  p.il_df2 = 1.0 / (k->l_df * k->l_df);
+  p.il_cf2 = 1.0 / (k->l_cf * k->l_cf);
+  p.l_df2 = k->l_df * k->l_df;
+  p.ratio = k->ratio;
+  p.cratio = 1.0 - k->ratio;
+  p.same_len = (k->l_df == k->l_cf);
+  return p;
+}
+
+inline ArdParams make_ard_params(const gp2d_kernel_t* k) {
+  ArdParams p;
+  p.dim = k->dim;
+  p.nterms = k->nterms;
+  for (int t = 0; t < 2; ++t) {
+    p.var[t] = k->var[t];
+    for (int d = 0; d < 3; ++d) p.ils[t][d] = (k->ls[t][d] != 0.0) ? 1.0 / k->ls[t][d] : 0.0;
+  }
+  return p;
+}
+
+// 2×2 block of the SE vector kernels.
+__device__ __forceinline__ void vec_block(const VecParams& p, double d1, double d2,
+                                          double& k11, double& k12, double& k22) {
+  const double r2 = d1 * d1 + d2 * d2;
+  const double p11 = d1 * d1, p12 = d1 * d2, p22 = d2 * d2;
+  if (p.kind == GP2D_KIND_SCALAR) {
+    const double c = r2 * p.il_df2;
+    const double s = p.il_df2 * exp(-0.5 * c) * p.l_df2;  // (1/σ²)·exp(−C/2)·σ²
+    k11 = s; k12 = s; k22 = s;
+    return;
+  }
+  double f11 = 0.0, f12 = 0.0, f22 = 0.0;
+  double e_df = 0.0;
+  if (p.kind == GP2D_KIND_DIVFREE || p.kind == GP2D_KIND_MIXED) {
+    const double c = r2 * p.il_df2;
+    e_df = exp(-0.5 * c);
+    const double e = p.il_df2 * e_df;
+    const double aux = 1.0 - c;  // (p−1) − C, p = 2
+    f11 = e * (p11 * p.il_df2 + aux);
+    f12 = e * (p12 * p.il_df2);
+    f22 = e * (p22 * p.il_df2 + aux);
+    if (p.kind == GP2D_KIND_DIVFREE) { k11 = f11; k12 = f12; k22 = f22; return; }
+  }
+  const double ccf = r2 * p.il_cf2;
+  const double ecf = (p.kind == GP2D_KIND_MIXED && p.same_len) ? e_df : exp(-0.5 * ccf);
+  const double e = p.il_cf2 * ecf;
+  const double g11 = e * (1.0 - p11 * p.il_cf2);
+  const double g12 = -e * (p12 * p.il_cf2);
+  const double g22 = e * (1.0 - p22 * p.il_cf2);
+  if (p.kind == GP2D_KIND_CURLFREE) { k11 = g11; k12 = g12; k22 = g22; return; }
+  k11 = p.ratio * f11 + p.cratio * g11;
+  k12 = p.ratio * f12 + p.cratio * g12;
+  k22 = p.ratio * f22 + p.cratio * g22;
+}
+
+__device__ __forceinline__ double ard_value(const ArdParams& p, const double* a, const double* b) {
+  double k = 0.0;
+  for (int t = 0; t < p.nterms; ++t) {
+    double s = 0.0;
+    for (int d = 0; d < p.dim; ++d) {
+      const double z = (a[d] - b[d]) * p.ils[t][d];
+      s += z * z;
+    }
+    k += p.var[t] * exp(-0.5 * s);
+  }
+  return k;
+}
+
+// Block: 64 (column points) × 4 thread rows; each thread does ROWS_PER_THREAD
+// row points so that the column point's coordinates are loaded once.
+constexpr int ASM_ROWS = 16;
+
+__global__ __launch_bounds__(256) void assemble_vec_kernel(
+    const double* __restrict__ xa, int64_t na, int64_t na_pad,
+    const double* __restrict__ xb, int64_t nb, int64_t nb_pad,
+    VecParams p, double diag_add, int symmetric, double* __restrict__ out, int64_t ld) {
+  const int64_t j = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
+  const int ty = threadIdx.x >> 6;
+  const bool jv = j < nb;
+  const double b1 = jv ? xb[2 * j] : 0.0;
+  const double b2 = jv ? xb[2 * j + 1] : 0.0;
+#pragma unroll 1
+  for (int q = 0; q < ASM_ROWS / 4; ++q) {
+    const int64_t i = (int64_t)blockIdx.y * ASM_ROWS + ty + 4 * q;
+    if (i >= na_pad) break;
+    double k11, k12, k22;
+    if (jv && i < na) {
+      vec_block(p, xa[2 * i] - b1, xa[2 * i + 1] - b2, k11, k12, k22);
+      if (symmetric && i == j) { k11 += diag_add; k22 += diag_add; }
+    } else {
+      const double dd = (symmetric && i == j) ? 1.0 : 0.0;  // padded points: identity rows
+      k11 = dd; k12 = 0.0; k22 = dd;
+    }
+    double* r0 = out + i * ld;
+    double* r1 = out + (na_pad + i) * ld;
+    r0[j] = k11;
+    r0[nb_pad + j] = k12;
+    r1[j] = k12;
+    r1[nb_pad + j] = k22;
+  }
+}
+
+__global__ __launch_bounds__(256) void assemble_ard_kernel(
+    const double* __restrict__ xa, int64_t na, int64_t na_pad,
+    const double* __restrict__ xb, int64_t nb, int64_t nb_pad,
+    ArdParams p, double diag_add, int symmetric, double* __restrict__ out, int64_t ld) {
+  const int64_t j = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
+  const int ty = threadIdx.x >> 6;
+  const bool jv = j < nb;
+  double b[3] = {0.0, 0.0, 0.0};
+  for (int d = 0; d < p.dim; ++d) b[d] = jv ? xb[j * p.dim + d] : 0.0;
+#pragma unroll 1
+  for (int q = 0; q < ASM_ROWS / 4; ++q) {
+    const int64_t i = (int64_t)blockIdx.y * ASM_ROWS + ty + 4 * q;
+    if (i >= na_pad) break;
+    double k;
+    if (jv && i < na) {
+      double a[3] = {0.0, 0.0, 0.0};
+      for (int d = 0; d < p.dim; ++d) a[d] = xa[i * p.dim + d];
+      k = ard_value(p, a, b);
+      if (symmetric && i == j) k += diag_add;
+    } else {
+      k = (symmetric && i == j) ? 1.0 : 0.0;
+    }
+    out[i * ld + j] = k;
+  }
+}
+
+}  // namespace gp2d

@@ -1,0 +1,222 @@
+// gemm_f64.hpp — FP64 MFMA GEMM core (v_mfma_f64_16x16x4_f64) for gfx950.
+//
+// One 128×128 output tile per 256-thread workgroup (4 waves as 2×2, each wave a
+// 64×64 sub-tile = 4×4 MFMA tiles of 16×16, 64 fp64 accumulators per lane).
+// K advances in BK=16 slabs staged through double-buffered LDS with register
+// prefetch; one barrier per slab.  Used by every dense contraction of the path:
+//   * Cholesky panel TRSM and trailing SYRK  (NT, c_lower)     — replaces LAPACK potrf
+//     inside np.linalg.inv / GPy / sklearn (GP_laser.py:118, _gpr.py:349)
+//   * TRTRI recursive doubling                (NN, a_lower / b_lower)
+//   * predict variance V = L⁻¹·K*ᵀ with the column sum-of-squares fused in the
+//     epilogue (NN, a_lower, EPI_COLSQ) — replaces Ks·Ki·Ksᵀ (GP_laser.py:129)
+//     and solve_triangular+einsum (_gpr.py:454-475).
+//
+// MFMA f64 lane maps (verified on MI355X, tools/microbench/f64_rates.hip):
+//   A: lane l holds A[l&15][l>>4]; B: lane l holds B[l>>4][l&15];
+//   C/D: acc[r] of lane l is C[(l>>4) + 4r][l&15].
+// LDS images: A as [BM][BK+2] and Bᵀ-stored B as [BN][BK+2] (stride ≡ 2 mod 32
+// doubles: a 32-lane half reads 16 rows × 2 k-columns conflict-free); NN B as
+// [BK][BN+16] (stride ≡ 16 mod 32: 2 rows × 16 columns conflict-free).
+// Problem sizes are multiples of 128 (the engine pads), so there are no edge tiles.
+#pragma once
+#include "common.hpp"
+
+namespace gp2d {
+
+constexpr int GBM = 128, GBN = 128, GBK = 16;
+constexpr int AS = GBK + 2;
+constexpr int BS_NN = GBN + 16;
+constexpr int BS_NT = GBK + 2;
+constexpr int A_TILE = GBM * AS;                                            // 2304
+constexpr int B_TILE = (GBK * BS_NN > GBN * BS_NT) ? GBK * BS_NN : GBN * BS_NT;  // 2304
+constexpr int STAGE = A_TILE + B_TILE;
+
+enum { EPI_STORE = 0, EPI_COLSQ = 1 };
+
+struct GemmParams {
+  const double* A; int64_t lda; int64_t sA;   // M×K row-major
+  const double* B; int64_t ldb; int64_t sB;   // NN: K×N row-major; NT: N×K row-major
+  double* C; int64_t ldc; int64_t sC;         // M×N
+  int M, N, K;
+  double alpha, beta;
+  int a_lower;   // A lower-triangular: row block i0 only needs k < i0+BM
+  int b_lower;   // (NN) B lower-triangular: column block j0 only needs k >= j0
+  int c_lower;   // enumerate lower tiles of a square C; diagonal tiles store i >= j
+  int rev_rows;  // dispatch heavy (large i0) row blocks first (a_lower)
+  double* P; int64_t ldp; int64_t sP;         // EPI_COLSQ partials [M/BM][N]
+};
+
+__device__ __forceinline__ void tri_tile(int t, int& bi, int& bj) {
+  int r = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+  while ((r + 1) * (r + 2) / 2 <= t) ++r;
+  while (r * (r + 1) / 2 > t) --r;
+  bi = r;
+  bj = t - r * (r + 1) / 2;
+}
+
+template <bool BT, int EPI>
+__global__ __launch_bounds__(256, 2) void gemm_f64_kernel(GemmParams p) {
+  __shared__ double smem[2 * STAGE];
+
+  int bi, bj;
+  if (p.c_lower) {
+    tri_tile(blockIdx.x, bi, bj);
+  } else {
+    bj = blockIdx.x;
+    bi = p.rev_rows ? (int)(gridDim.y - 1 - blockIdx.y) : (int)blockIdx.y;
+  }
+  const int z = blockIdx.z;
+  const int i0 = bi * GBM, j0 = bj * GBN;
+  const double* __restrict__ A = p.A + z * p.sA;
+  const double* __restrict__ B = p.B + z * p.sB;
+
+  const int kb = p.b_lower ? j0 : 0;
+  const int ke = p.a_lower ? min(p.K, i0 + GBM) : p.K;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int lr = lane & 15, lk = lane >> 4;
+
+  d4 acc[4][4];
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = d4{0.0, 0.0, 0.0, 0.0};
+
+  // global -> register prefetch mapping
+  const int ar = tid >> 3, ac = (tid & 7) * 2;      // A / Bᵀ: 32 rows × 16 cols per pass
+  const int br = tid >> 6, bc = (tid & 63) * 2;     // NN B:   4 rows × 128 cols per pass
+  d2 ra[4], rb[4];
+
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      ra[q] = *reinterpret_cast<const d2*>(A + (int64_t)(i0 + ar + 32 * q) * p.lda + k0 + ac);
+    if (BT) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        rb[q] = *reinterpret_cast<const d2*>(B + (int64_t)(j0 + ar + 32 * q) * p.ldb + k0 + ac);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        rb[q] = *reinterpret_cast<const d2*>(B + (int64_t)(k0 + br + 4 * q) * p.ldb + j0 + bc);
+    }
+  };
+  auto swrite = [&](int buf) {
+    double* As = smem + buf * STAGE;
+    double* Bs = As + A_TILE;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) *reinterpret_cast<d2*>(As + (ar + 32 * q) * AS + ac) = ra[q];
+    if (BT) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) *reinterpret_cast<d2*>(Bs + (ar + 32 * q) * BS_NT + ac) = rb[q];
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) *reinterpret_cast<d2*>(Bs + (br + 4 * q) * BS_NN + bc) = rb[q];
+    }
+  };
+
+  if (kb < ke) {
+    gload(kb);
+    swrite(0);
+    __syncthreads();
+    int buf = 0;
+    for (int k0 = kb; k0 < ke; k0 += GBK) {
+      const bool has_next = (k0 + GBK) < ke;
+      if (has_next) gload(k0 + GBK);
+      const double* As = smem + buf * STAGE;
+      const double* Bs = As + A_TILE;
+#pragma unroll
+      for (int kk = 0; kk < GBK; kk += 4) {
+        double a[4], b[4];
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) a[mi] = As[(wr * 64 + mi * 16 + lr) * AS + kk + lk];
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+          if (BT) b[ni] = Bs[(wc * 64 + ni * 16 + lr) * BS_NT + kk + lk];
+          else    b[ni] = Bs[(kk + lk) * BS_NN + wc * 64 + ni * 16 + lr];
+        }
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
+      }
+      if (has_next) swrite(buf ^ 1);
+      __syncthreads();
+      buf ^= 1;
+    }
+  }
+
+  if (EPI == EPI_STORE) {
+    double* __restrict__ C = p.C + z * p.sC;
+    const bool diag_tile = p.c_lower && (bi == bj);
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = i0 + wr * 64 + mi * 16 + lk + 4 * r;
+          const int col = j0 + wc * 64 + ni * 16 + lr;
+          if (diag_tile && col > row) continue;
+          double* cp = C + (int64_t)row * p.ldc + col;
+          double v = p.alpha * acc[mi][ni][r];
+          if (p.beta != 0.0) v += p.beta * (*cp);
+          *cp = v;
+        }
+  } else {
+    // column sums of squares of this 128-row slab of V, combined in a fixed order:
+    // registers (rows (l>>4)+4r+16mi) -> lanes l, l^16, l^32, l^48 -> the two wave rows.
+    double* red = smem;  // [2][128]
+    double s[4];
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      double t = 0.0;
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) t += acc[mi][ni][r] * acc[mi][ni][r];
+      t += __shfl_xor(t, 16);
+      t += __shfl_xor(t, 32);
+      s[ni] = t;
+    }
+    if (lane < 16) {
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) red[wr * 128 + wc * 64 + ni * 16 + lane] = s[ni];
+    }
+    __syncthreads();
+    if (tid < 128) {
+      double* __restrict__ P = p.P + z * p.sP + (int64_t)bi * p.ldp + j0;
+      P[tid] = red[tid] + red[128 + tid];
+    }
+  }
+}
+
+// Host-side launcher.  Returns 0 / negative error.
+template <bool BT, int EPI>
+inline int launch_gemm(const GemmParams& p, int batch, hipStream_t s) {
+  if (p.M <= 0 || p.N <= 0 || batch <= 0) return 0;
+  if ((p.M % GBM) || (p.N % GBN) || (p.K % GBK)) {
+    set_error("gemm: sizes must be multiples of 128/128/16");
+    return -2;
+  }
+  dim3 grid;
+  if (p.c_lower) {
+    const int t = p.M / GBM;
+    grid = dim3(t * (t + 1) / 2, 1, batch);
+  } else {
+    grid = dim3(p.N / GBN, p.M / GBM, batch);
+  }
+  gemm_f64_kernel<BT, EPI><<<grid, 256, 0, s>>>(p);
+  return check_launch("gemm_f64_kernel");
+}
+
+inline GemmParams gemm_params() {
+  GemmParams p{};
+  p.alpha = 1.0;
+  p.beta = 0.0;
+  return p;
+}
+
+}  // namespace gp2d

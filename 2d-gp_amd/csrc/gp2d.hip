@@ -1,0 +1,315 @@
+// gp2d.hip — C ABI of the MI355X GP-kriging engine (include/gp2d.h).
+//
+// Host orchestration of the kernels in assemble.hpp / gemm_f64.hpp /
+// factor.hpp / predict.hpp.  All work is enqueued on the caller's HIP stream;
+// nothing here synchronises except gp2d_timing_read().
+#include "common.hpp"
+#include "assemble.hpp"
+#include "gemm_f64.hpp"
+#include "factor.hpp"
+#include "predict.hpp"
+#include "../../include/gp2d.h"
+
+#include <algorithm>
+#include <mutex>
+#include <string>
+#include <vector>
+
+namespace gp2d {
+
+static thread_local std::string g_err;
+void set_error(const std::string& msg) { g_err = msg; }
+
+static inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+static inline int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
+
+// ---------------------------------------------------------------- timing hooks
+struct Timing {
+  std::mutex mu;
+  bool on = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+  std::vector<double> flops;
+  std::vector<hipEvent_t> pool;
+  hipEvent_t get() {
+    if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
+    hipEvent_t e; hipEventCreate(&e); return e;
+  }
+};
+static Timing g_timing;
+
+static int validate_kernel(const gp2d_kernel_t* k) {
+  GP2D_REQUIRE(k != nullptr, "kernel descriptor is NULL");
+  if (k->family == GP2D_FAMILY_VECTOR2D) {
+    GP2D_REQUIRE(k->kind >= 0 && k->kind <= 3, "vector2d kind must be 0..3");
+    GP2D_REQUIRE(k->l_df > 0.0, "l_df must be > 0");
+    if (k->kind == GP2D_KIND_CURLFREE || k->kind == GP2D_KIND_MIXED) GP2D_REQUIRE(k->l_cf > 0.0, "l_cf must be > 0");
+  } else if (k->family == GP2D_FAMILY_ARD_RBF) {
+    GP2D_REQUIRE(k->dim >= 1 && k->dim <= 3, "ARD dim must be 1..3");
+    GP2D_REQUIRE(k->nterms >= 1 && k->nterms <= 2, "ARD nterms must be 1..2");
+    for (int t = 0; t < k->nterms; ++t)
+      for (int d = 0; d < k->dim; ++d) GP2D_REQUIRE(k->ls[t][d] > 0.0, "ARD length scales must be > 0");
+  } else {
+    set_error("unknown kernel family");
+    return -2;
+  }
+  return 0;
+}
+
+static int assemble_impl(const double* xa, int64_t na, int64_t na_pad, const double* xb, int64_t nb,
+                         int64_t nb_pad, const gp2d_kernel_t* k, double diag_add, int symmetric, double* out,
+                         int64_t ld, hipStream_t s) {
+  GP2D_CHECK(validate_kernel(k));
+  GP2D_REQUIRE(na_pad % PT_TILE == 0 && nb_pad % PT_TILE == 0, "padded point counts must be multiples of 64");
+  GP2D_REQUIRE(na <= na_pad && nb <= nb_pad && na >= 0 && nb >= 0, "point counts exceed padded counts");
+  if (na_pad == 0 || nb_pad == 0) return 0;
+  const int bd = (k->family == GP2D_FAMILY_VECTOR2D) ? 2 : 1;
+  GP2D_REQUIRE(ld >= bd * nb_pad, "ld too small");
+  dim3 grid(nb_pad / 64, (na_pad + ASM_ROWS - 1) / ASM_ROWS);
+  if (bd == 2) {
+    assemble_vec_kernel<<<grid, 256, 0, s>>>(xa, na, na_pad, xb, nb, nb_pad, make_vec_params(k), diag_add,
+                                             symmetric, out, ld);
+  } else {
+    assemble_ard_kernel<<<grid, 256, 0, s>>>(xa, na, na_pad, xb, nb, nb_pad, make_ard_params(k), diag_add,
+                                             symmetric, out, ld);
+  }
+  return check_launch("assemble");
+}
+
+}  // namespace gp2d
+
+using namespace gp2d;
+
+extern "C" {
+
+int gp2d_abi_version(void) { return GP2D_ABI_VERSION; }
+int64_t gp2d_padded_points(int64_t n) { return round_up(n < 1 ? 1 : n, PT_TILE); }
+int gp2d_block_dim(const gp2d_kernel_t* k) { return (k && k->family == GP2D_FAMILY_ARD_RBF) ? 1 : 2; }
+
+double gp2d_kernel_diag(const gp2d_kernel_t* k) {
+  if (!k) return 0.0;
+  if (k->family == GP2D_FAMILY_ARD_RBF) {
+    double s = 0.0;
+    for (int t = 0; t < k->nterms; ++t) s += k->var[t];
+    return s;
+  }
+  switch (k->kind) {
+    case GP2D_KIND_SCALAR: return (1.0 / k->l_df) * (1.0 / k->l_df) * (k->l_df * k->l_df);
+    case GP2D_KIND_DIVFREE: return 1.0 / (k->l_df * k->l_df);
+    case GP2D_KIND_CURLFREE: return 1.0 / (k->l_cf * k->l_cf);
+    default: return k->ratio * (1.0 / (k->l_df * k->l_df)) + (1.0 - k->ratio) * (1.0 / (k->l_cf * k->l_cf));
+  }
+}
+
+const char* gp2d_last_error(void) { return g_err.c_str(); }
+
+int gp2d_assemble(const double* xa, int64_t na, int64_t na_pad, const double* xb, int64_t nb, int64_t nb_pad,
+                  const gp2d_kernel_t* k, double diag_add, int symmetric, double* out, int64_t ld, void* stream) {
+  return assemble_impl(xa, na, na_pad, xb, nb, nb_pad, k, diag_add, symmetric, out, ld, S(stream));
+}
+
+// ------------------------------------------------------------------------ POTRF
+size_t gp2d_potrf_workspace(int64_t) { return 0; }
+
+int gp2d_potrf(double* A, int64_t n, int64_t lda, double* dinv, int* info_dev, void*, size_t, void* stream) {
+  GP2D_REQUIRE(n % NB == 0 && n > 0, "potrf: n must be a positive multiple of 128");
+  GP2D_REQUIRE(lda >= n && lda % 2 == 0, "potrf: lda must be >= n and even");
+  hipStream_t s = S(stream);
+  const int nb = (int)(n / NB);
+  for (int k = 0; k < nb; ++k) {
+    const int k0 = k * NB;
+    potrf_diag_kernel<<<1, 256, 0, s>>>(A, lda, k0, dinv, info_dev);
+    GP2D_CHECK(check_launch("potrf_diag_kernel"));
+    if (k == nb - 1) break;
+    const int rows = (int)(n - k0 - NB);
+    // in-place panel TRSM  L21 = A21 · inv(L11)ᵀ   (needs inv(L11): from dinv or recomputed)
+    const double* inv_kk = dinv ? dinv + (int64_t)k * NB * NB : nullptr;
+    GP2D_REQUIRE(inv_kk != nullptr, "potrf: dinv buffer is required");
+    GemmParams p = gemm_params();
+    p.A = A + (int64_t)(k0 + NB) * lda + k0; p.lda = lda;
+    p.B = inv_kk; p.ldb = NB;
+    p.C = A + (int64_t)(k0 + NB) * lda + k0; p.ldc = lda;
+    p.M = rows; p.N = NB; p.K = NB;
+    GP2D_CHECK((launch_gemm<true, EPI_STORE>(p, 1, s)));
+    // trailing SYRK  A22 −= L21 L21ᵀ  (lower tiles)
+    GemmParams q = gemm_params();
+    q.A = A + (int64_t)(k0 + NB) * lda + k0; q.lda = lda;
+    q.B = q.A; q.ldb = lda;
+    q.C = A + (int64_t)(k0 + NB) * lda + (k0 + NB); q.ldc = lda;
+    q.M = rows; q.N = rows; q.K = NB;
+    q.alpha = -1.0; q.beta = 1.0; q.c_lower = 1;
+    GP2D_CHECK((launch_gemm<true, EPI_STORE>(q, 1, s)));
+  }
+  dim3 zg((unsigned)((n / 2 + 255) / 256), (unsigned)n);
+  zero_upper_kernel<<<zg, 256, 0, s>>>(A, n, lda);
+  return check_launch("zero_upper_kernel");
+}
+
+// ------------------------------------------------------------------------ TRTRI
+size_t gp2d_trtri_workspace(int64_t n) {
+  // T buffers of the widest level: pairs × (g·NB)² doubles  ≤ n²/4 (+ dinv if not supplied)
+  const int64_t nb = n / NB;
+  size_t t = (size_t)(n / 2 + NB) * (size_t)(n / 2 + NB) * sizeof(double);
+  return t + (size_t)nb * NB * NB * sizeof(double);
+}
+
+int gp2d_trtri(double* A, int64_t n, int64_t lda, const double* dinv, void* work, size_t work_bytes, void* stream) {
+  GP2D_REQUIRE(n % NB == 0 && n > 0, "trtri: n must be a positive multiple of 128");
+  GP2D_REQUIRE(work != nullptr && work_bytes >= gp2d_trtri_workspace(n), "trtri: workspace too small");
+  hipStream_t s = S(stream);
+  const int nb = (int)(n / NB);
+  double* T = reinterpret_cast<double*>(work);
+  double* dwork = T + (size_t)(n / 2 + NB) * (size_t)(n / 2 + NB);
+  if (!dinv) {
+    trti2_diag_kernel<<<nb, 256, 0, s>>>(A, lda, dwork);
+    GP2D_CHECK(check_launch("trti2_diag_kernel"));
+    dinv = dwork;
+  }
+  put_diag_blocks_kernel<<<dim3(NB * NB / 256, nb), 256, 0, s>>>(A, lda, dinv);
+  GP2D_CHECK(check_launch("put_diag_blocks_kernel"));
+  for (int g = 1; g < nb; g *= 2) {
+    // pairs (left = [s·2g, s·2g+g), right = [s·2g+g, min(s·2g+2g, nb))) in 128-blocks
+    const int full = nb / (2 * g);                 // pairs whose right part has g blocks
+    const int rem = nb - full * 2 * g;             // trailing blocks
+    struct Pair { int Ls, Rs, Rn, count; };
+    std::vector<Pair> launches;
+    if (full > 0) launches.push_back({0, g, g, full});
+    if (rem > g) launches.push_back({full * 2 * g, full * 2 * g + g, rem - g, 1});
+    for (const Pair& pr : launches) {
+      const int64_t Lo = (int64_t)pr.Ls * NB, Ro = (int64_t)pr.Rs * NB;
+      const int bw = g * NB, rh = pr.Rn * NB;
+      const int64_t stride = (int64_t)2 * g * NB * (lda + 1);  // next pair's diagonal offset
+      // T = C · WA      C = A[R, L] (rh × bw), WA = A[L, L] (bw × bw lower)
+      GemmParams p = gemm_params();
+      p.A = A + Ro * lda + Lo; p.lda = lda; p.sA = stride;
+      p.B = A + Lo * lda + Lo; p.ldb = lda; p.sB = stride;
+      p.C = T; p.ldc = bw; p.sC = (int64_t)rh * bw;
+      p.M = rh; p.N = bw; p.K = bw; p.b_lower = 1;
+      GP2D_CHECK((launch_gemm<false, EPI_STORE>(p, pr.count, s)));
+      // A[R, L] = −WD · T     WD = A[R, R] (rh × rh lower)
+      GemmParams q = gemm_params();
+      q.A = A + Ro * lda + Ro; q.lda = lda; q.sA = stride;
+      q.B = T; q.ldb = bw; q.sB = (int64_t)rh * bw;
+      q.C = A + Ro * lda + Lo; q.ldc = lda; q.sC = stride;
+      q.M = rh; q.N = bw; q.K = rh; q.a_lower = 1; q.alpha = -1.0;
+      GP2D_CHECK((launch_gemm<false, EPI_STORE>(q, pr.count, s)));
+    }
+  }
+  return 0;
+}
+
+// ------------------------------------------------------------------------ POTRS
+size_t gp2d_potrs_workspace(int64_t n) { return (size_t)n * sizeof(double) * (1 + (size_t)(n / NB + 1)); }
+
+int gp2d_potrs_inv(const double* W, int64_t n, int64_t ldw, const double* y, double* alpha, void* work,
+                   size_t work_bytes, void* stream) {
+  GP2D_REQUIRE(n % NB == 0 && n > 0, "potrs: n must be a positive multiple of 128");
+  GP2D_REQUIRE(work != nullptr && work_bytes >= gp2d_potrs_workspace(n), "potrs: workspace too small");
+  hipStream_t s = S(stream);
+  double* z = reinterpret_cast<double*>(work);
+  double* part = z + n;
+  trmv_n_lower_kernel<<<(unsigned)((n + 3) / 4), 256, 0, s>>>(W, n, ldw, y, z);
+  GP2D_CHECK(check_launch("trmv_n_lower_kernel"));
+  const int64_t nseg = n / NB;
+  trmv_t_lower_part_kernel<<<dim3((unsigned)((n + 255) / 256), (unsigned)nseg), 256, 0, s>>>(W, n, ldw, z, part);
+  GP2D_CHECK(check_launch("trmv_t_lower_part_kernel"));
+  sum_segments_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(part, nseg, n, alpha);
+  return check_launch("sum_segments_kernel");
+}
+
+// ---------------------------------------------------------------------- PREDICT
+size_t gp2d_predict_workspace(int64_t n, int64_t chunk, int bd) {
+  const int64_t cp = round_up(chunk < 1 ? 1 : chunk, PT_TILE);
+  const int64_t ncols = bd * cp;
+  const int64_t ncols_t = round_up(ncols, GBN);
+  return sizeof(double) * ((size_t)n * ncols_t + 2 * (size_t)(n / MEAN_SEG + 1) * ncols_t);
+}
+
+int gp2d_predict(const double* W, int64_t n, int64_t ldw, const double* alpha, const double* xtr, int64_t ntr,
+                 int64_t ntr_pad, const double* xg, int64_t m, const gp2d_kernel_t* k, int var_mode, double noise,
+                 int compute_var, double* mean, double* var, int64_t chunk, void* work, size_t work_bytes,
+                 void* stream) {
+  GP2D_CHECK(validate_kernel(k));
+  const int bd = gp2d_block_dim(k);
+  GP2D_REQUIRE(n == bd * ntr_pad, "predict: n must equal block_dim × ntr_pad");
+  GP2D_REQUIRE(n % NB == 0, "predict: n must be a multiple of 128");
+  GP2D_REQUIRE(chunk > 0 && chunk % PT_TILE == 0, "predict: chunk must be a positive multiple of 64");
+  GP2D_REQUIRE(bd * chunk % GBN == 0, "predict: block_dim × chunk must be a multiple of 128");
+  GP2D_REQUIRE(work != nullptr && work_bytes >= gp2d_predict_workspace(n, chunk, bd), "predict: workspace too small");
+  GP2D_REQUIRE(var_mode >= 0 && var_mode <= 2, "predict: bad var_mode");
+  if (m <= 0) return 0;
+  hipStream_t s = S(stream);
+  const int64_t ncols_max = bd * chunk;
+  double* Bm = reinterpret_cast<double*>(work);
+  double* pm = Bm + (size_t)n * ncols_max;
+  double* P = pm + (size_t)(n / MEAN_SEG + 1) * ncols_max;
+  const double kss = gp2d_kernel_diag(k);
+  const double add = (var_mode == GP2D_VAR_LATENT) ? 0.0 : noise;
+  const int clip = (var_mode == GP2D_VAR_CLIPPED);
+  const int dim = (k->family == GP2D_FAMILY_VECTOR2D) ? 2 : k->dim;
+
+  for (int64_t c0 = 0; c0 < m; c0 += chunk) {
+    const int64_t cv = std::min<int64_t>(chunk, m - c0);
+    const int64_t cp = round_up(cv, (bd == 2) ? PT_TILE : GBN);
+    const int64_t ncols = bd * cp;
+    // K*ᵀ chunk: rows = training components, cols = grid components
+    GP2D_CHECK(assemble_impl(xtr, ntr, ntr_pad, xg + c0 * dim, cv, cp, k, 0.0, 0, Bm, ncols, s));
+    const int64_t nmseg = n / MEAN_SEG;
+    mean_part_kernel<<<dim3((unsigned)((ncols + 255) / 256), (unsigned)nmseg), 256, 0, s>>>(Bm, ncols, ncols, alpha, pm);
+    GP2D_CHECK(check_launch("mean_part_kernel"));
+    const int64_t npseg = n / GBM;
+    if (compute_var) {
+      GemmParams p = gemm_params();
+      p.A = W; p.lda = ldw;
+      p.B = Bm; p.ldb = ncols;
+      p.M = (int)n; p.N = (int)ncols; p.K = (int)n;
+      p.a_lower = 1; p.rev_rows = 1;
+      p.P = P; p.ldp = ncols;
+      hipEvent_t e0 = nullptr, e1 = nullptr;
+      {
+        std::lock_guard<std::mutex> lk(g_timing.mu);
+        if (g_timing.on) { e0 = g_timing.get(); e1 = g_timing.get(); hipEventRecord(e0, s); }
+      }
+      GP2D_CHECK((launch_gemm<false, EPI_COLSQ>(p, 1, s)));
+      if (e0) {
+        std::lock_guard<std::mutex> lk(g_timing.mu);
+        hipEventRecord(e1, s);
+        g_timing.ev.push_back({e0, e1});
+        const double nv = (double)bd * (double)ntr;  // algorithmic order (valid points)
+        g_timing.flops.push_back((double)bd * (double)cv * nv * nv);  // 2·(2N)² per point (vector2d)
+      }
+    }
+    predict_finalize_kernel<<<(unsigned)((ncols + 255) / 256), 256, 0, s>>>(
+        pm, nmseg, P, npseg, ncols, cp, cv, c0, m, kss, add, clip, compute_var, mean, var);
+    GP2D_CHECK(check_launch("predict_finalize_kernel"));
+  }
+  return 0;
+}
+
+// ------------------------------------------------------------------ instrumentation
+void gp2d_timing_enable(int on) {
+  std::lock_guard<std::mutex> lk(g_timing.mu);
+  g_timing.on = (on != 0);
+}
+
+int gp2d_timing_read(double* total_ms, int64_t* launches, double* flops) {
+  std::lock_guard<std::mutex> lk(g_timing.mu);
+  double ms = 0.0, fl = 0.0;
+  for (size_t i = 0; i < g_timing.ev.size(); ++i) {
+    auto& pr = g_timing.ev[i];
+    if (hipEventSynchronize(pr.second) != hipSuccess) { set_error("timing: event sync failed"); return -1; }
+    float t = 0.f;
+    hipEventElapsedTime(&t, pr.first, pr.second);
+    ms += t;
+    fl += g_timing.flops[i];
+    g_timing.pool.push_back(pr.first);
+    g_timing.pool.push_back(pr.second);
+  }
+  if (total_ms) *total_ms = ms;
+  if (launches) *launches = (int64_t)g_timing.ev.size();
+  if (flops) *flops = fl;
+  g_timing.ev.clear();
+  g_timing.flops.clear();
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,139 @@
+"""ctypes binding of libgp2d.so (include/gp2d.h).
+
+The HIP engine is the only compute path: if the shared library is missing or
+fails to load, every compute entry point raises ``NativeLibraryError``; there is
+no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("GP2D_LIB", os.path.join(_HERE, "libgp2d.so"))
+
+FAMILY_VECTOR2D, FAMILY_ARD_RBF = 0, 1
+KIND_SCALAR, KIND_DIVFREE, KIND_CURLFREE, KIND_MIXED = 0, 1, 2, 3
+VAR_LATENT, VAR_NOISY, VAR_CLIPPED = 0, 1, 2
+
+# every symbol declared in include/gp2d.h
+EXPORTS = (
+    "gp2d_abi_version", "gp2d_padded_points", "gp2d_block_dim", "gp2d_kernel_diag",
+    "gp2d_assemble", "gp2d_potrf_workspace", "gp2d_potrf", "gp2d_trtri_workspace", "gp2d_trtri",
+    "gp2d_potrs_workspace", "gp2d_potrs_inv", "gp2d_predict_workspace", "gp2d_predict",
+    "gp2d_timing_enable", "gp2d_timing_read", "gp2d_last_error",
+)
+
+
+class NativeLibraryError(RuntimeError):
+    pass
+
+
+class GP2DError(RuntimeError):
+    pass
+
+
+class KernelDesc(ctypes.Structure):
+    _fields_ = [
+        ("family", ctypes.c_int32),
+        ("kind", ctypes.c_int32),
+        ("l_df", ctypes.c_double),
+        ("l_cf", ctypes.c_double),
+        ("ratio", ctypes.c_double),
+        ("dim", ctypes.c_int32),
+        ("nterms", ctypes.c_int32),
+        ("var", ctypes.c_double * 2),
+        ("ls", (ctypes.c_double * 3) * 2),
+    ]
+
+
+_lib = None
+_lock = threading.Lock()
+
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_D = ctypes.c_double
+_I = ctypes.c_int
+_SZ = ctypes.c_size_t
+_KP = ctypes.POINTER(KernelDesc)
+
+_SIGS = {
+    "gp2d_abi_version": (_I, []),
+    "gp2d_padded_points": (_I64, [_I64]),
+    "gp2d_block_dim": (_I, [_KP]),
+    "gp2d_kernel_diag": (_D, [_KP]),
+    "gp2d_assemble": (_I, [_P, _I64, _I64, _P, _I64, _I64, _KP, _D, _I, _P, _I64, _P]),
+    "gp2d_potrf_workspace": (_SZ, [_I64]),
+    "gp2d_potrf": (_I, [_P, _I64, _I64, _P, _P, _P, _SZ, _P]),
+    "gp2d_trtri_workspace": (_SZ, [_I64]),
+    "gp2d_trtri": (_I, [_P, _I64, _I64, _P, _P, _SZ, _P]),
+    "gp2d_potrs_workspace": (_SZ, [_I64]),
+    "gp2d_potrs_inv": (_I, [_P, _I64, _I64, _P, _P, _P, _SZ, _P]),
+    "gp2d_predict_workspace": (_SZ, [_I64, _I64, _I]),
+    "gp2d_predict": (_I, [_P, _I64, _I64, _P, _P, _I64, _I64, _P, _I64, _KP, _I, _D, _I, _P, _P, _I64, _P, _SZ, _P]),
+    "gp2d_timing_enable": (None, [_I]),
+    "gp2d_timing_read": (_I, [ctypes.POINTER(_D), ctypes.POINTER(_I64), ctypes.POINTER(_D)]),
+    "gp2d_last_error": (ctypes.c_char_p, []),
+}
+
+
+def lib():
+    """Load libgp2d.so once; raise NativeLibraryError (never fall back) on failure."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise NativeLibraryError(
+                f"gp2d HIP engine not built: {LIB_PATH} is missing (run `python __graft_entry__.py build`)")
+        try:
+            L = ctypes.CDLL(LIB_PATH)
+        except OSError as e:  # pragma: no cover - depends on the ROCm install
+            raise NativeLibraryError(f"cannot load {LIB_PATH}: {e}") from e
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        if L.gp2d_abi_version() != 1:
+            raise NativeLibraryError("libgp2d.so ABI version mismatch")
+        _lib = L
+        return _lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = lib().gp2d_last_error().decode(errors="replace")
+        raise GP2DError(f"{what} failed (rc={rc}): {msg}")
+
+
+def vector_kernel_desc(kind: int, l_df: float, l_cf: float = 1.0, ratio: float = 1.0) -> KernelDesc:
+    k = KernelDesc()
+    k.family = FAMILY_VECTOR2D
+    k.kind = int(kind)
+    k.l_df = float(l_df)
+    k.l_cf = float(l_cf)
+    k.ratio = float(ratio)
+    return k
+
+
+def ard_kernel_desc(variances, lengthscales) -> KernelDesc:
+    k = KernelDesc()
+    k.family = FAMILY_ARD_RBF
+    k.nterms = len(variances)
+    if not 1 <= k.nterms <= 2:
+        raise ValueError("ARD family supports 1 or 2 RBF terms")
+    dim = len(lengthscales[0])
+    if not 1 <= dim <= 3:
+        raise ValueError("ARD family supports 1..3 input dimensions")
+    k.dim = dim
+    for t in range(k.nterms):
+        k.var[t] = float(variances[t])
+        ls = list(lengthscales[t])
+        if len(ls) != dim:
+            raise ValueError("all RBF terms must have the same input dimension")
+        for d in range(dim):
+            k.ls[t][d] = float(ls[d])
+    return k

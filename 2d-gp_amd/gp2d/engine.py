@@ -1,0 +1,237 @@
+"""Device-resident GP engine: fit (assemble → POTRF → TRTRI → α) and predict.
+
+Host orchestration over the C ABI of libgp2d.so.  torch-ROCm tensors are used
+only as device-memory containers and for the current HIP stream; every FLOP runs
+in the hand-written HIP kernels.
+
+Reference call sites replaced:
+  * GP_laser.laser  GP_laser.py:113-140  (K, +noise·I, inv, Ks, mean, var)
+  * GPy GPRegression fit / model.predict  krig.py:411, :543-544
+  * sklearn GaussianProcessRegressor fit / predict(return_std)  krig.py:182-194
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from . import _native as N
+
+NB = 128
+
+
+def _stream_handle(device) -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _ptr(t: torch.Tensor) -> ctypes.c_void_p:
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _require_device(device=None) -> torch.device:
+    if not torch.cuda.is_available():
+        raise N.NativeLibraryError("gp2d needs a HIP device (torch.cuda.is_available() is False); "
+                                   "there is no CPU fallback")
+    N.lib()
+    return torch.device(device if device is not None else "cuda")
+
+
+def _as_points(x, dim: int, device) -> torch.Tensor:
+    if isinstance(x, torch.Tensor):
+        t = x.to(device=device, dtype=torch.float64)
+    else:
+        t = torch.as_tensor(np.ascontiguousarray(np.asarray(x, dtype=np.float64)), device=device)
+    return t.reshape(-1, dim).contiguous()
+
+
+@dataclass
+class KernelSpec:
+    """Hyperparameters of the covariance function.
+
+    family 'vector2d' (the reference's div-free / curl-free SE kernels):
+        kind 'df' | 'cf' | 'mixed' | 'scalar' (divFree 1 | 2 | mixed | 0),
+        l_df, l_cf, ratio  (myKernel.py:13-22; GP_laser.py:16 `l_df, l_cf, rate`)
+    family 'ard' (the sklearn model of krig.scikit_prior, krig.py:174-180):
+        variances (1-2 terms), lengthscales (per term, 1-3 dims)
+    """
+    family: str = "vector2d"
+    kind: str = "df"
+    l_df: float = 5.0
+    l_cf: float = 5.0
+    ratio: float = 1.0
+    variances: tuple = ()
+    lengthscales: tuple = ()
+
+    _KINDS = {"scalar": N.KIND_SCALAR, "df": N.KIND_DIVFREE, "cf": N.KIND_CURLFREE, "mixed": N.KIND_MIXED,
+              0: N.KIND_SCALAR, 1: N.KIND_DIVFREE, 2: N.KIND_CURLFREE, 3: N.KIND_MIXED}
+
+    def desc(self) -> N.KernelDesc:
+        if self.family == "vector2d":
+            return N.vector_kernel_desc(self._KINDS[self.kind], self.l_df, self.l_cf, self.ratio)
+        if self.family == "ard":
+            return N.ard_kernel_desc(self.variances, self.lengthscales)
+        raise ValueError(f"unknown kernel family {self.family!r}")
+
+    @property
+    def block_dim(self) -> int:
+        return 2 if self.family == "vector2d" else 1
+
+    @property
+    def input_dim(self) -> int:
+        return 2 if self.family == "vector2d" else len(self.lengthscales[0])
+
+    def kdiag(self) -> float:
+        return float(N.lib().gp2d_kernel_diag(ctypes.byref(self.desc())))
+
+
+def padded_points(n: int) -> int:
+    return int(N.lib().gp2d_padded_points(int(n)))
+
+
+def assemble(kernel: KernelSpec, xa, xb=None, diag_add: float = 0.0, device=None) -> torch.Tensor:
+    """Covariance matrix K(xa, xb) on the device, exactly as the reference lays it out
+    ((bd·Na) × (bd·Nb) component-major; no padding in the returned tensor)."""
+    dev = _require_device(device)
+    d = kernel.input_dim
+    bd = kernel.block_dim
+    A = _as_points(xa, d, dev)
+    sym = xb is None
+    B = A if sym else _as_points(xb, d, dev)
+    na, nb = A.shape[0], B.shape[0]
+    nap, nbp = padded_points(na), padded_points(nb)
+    out = torch.empty((bd * nap, bd * nbp), dtype=torch.float64, device=dev)
+    desc = kernel.desc()
+    N.check(N.lib().gp2d_assemble(_ptr(A), na, nap, _ptr(B), nb, nbp, ctypes.byref(desc), float(diag_add),
+                                  int(sym), _ptr(out), out.shape[1], _stream_handle(dev)), "gp2d_assemble")
+    if bd == 1:
+        return out[:na, :nb]
+    idx_r = torch.cat([torch.arange(na, device=dev), nap + torch.arange(na, device=dev)])
+    idx_c = torch.cat([torch.arange(nb, device=dev), nbp + torch.arange(nb, device=dev)])
+    return out.index_select(0, idx_r).index_select(1, idx_c)
+
+
+@dataclass
+class GPFit:
+    """A fitted GP resident in HBM: W = L⁻¹ (n×n), α = K_y⁻¹y, training points."""
+    kernel: KernelSpec
+    noise: float
+    x: torch.Tensor          # (N, dim) device
+    n_train: int
+    n_pad: int               # padded point count
+    W: torch.Tensor          # (n, n) lower-triangular inverse Cholesky factor
+    alpha: torch.Tensor      # (n,)
+    device: torch.device
+    info: int = 0
+    extra: dict = field(default_factory=dict)
+
+    @property
+    def n(self) -> int:
+        return self.W.shape[0]
+
+
+def _pad_obs(y, n_train: int, n_pad: int, bd: int, device) -> torch.Tensor:
+    if isinstance(y, torch.Tensor):
+        yt = y.to(device=device, dtype=torch.float64).reshape(-1)
+    else:
+        yt = torch.as_tensor(np.asarray(y, dtype=np.float64).reshape(-1), device=device)
+    if yt.numel() != bd * n_train:
+        raise ValueError(f"observation vector has {yt.numel()} entries, expected {bd * n_train}")
+    out = torch.zeros(bd * n_pad, dtype=torch.float64, device=device)
+    for c in range(bd):
+        out[c * n_pad:c * n_pad + n_train] = yt[c * n_train:(c + 1) * n_train]
+    return out
+
+
+def fit(kernel: KernelSpec, x, y, noise: float, jitter: float = 0.0, device=None) -> GPFit:
+    """K_y = K(x,x) + (noise+jitter)·I → L = chol(K_y) → W = L⁻¹ → α = Wᵀ W y.
+
+    Raises numpy.linalg.LinAlgError if K_y is not positive definite (the
+    reference's np.linalg.inv / GPy jitchol / sklearn error paths).
+    """
+    dev = _require_device(device)
+    L = N.lib()
+    d, bd = kernel.input_dim, kernel.block_dim
+    X = _as_points(x, d, dev)
+    ntr = X.shape[0]
+    if ntr < 1:
+        raise ValueError("need at least one training point")
+    npad = padded_points(ntr)
+    n = bd * npad
+    if n % NB:  # scalar (ARD) family: the matrix order itself must be a multiple of 128
+        npad = (npad + NB - 1) // NB * NB
+        n = bd * npad
+    s = _stream_handle(dev)
+    desc = kernel.desc()
+    A = torch.empty((n, n), dtype=torch.float64, device=dev)
+    N.check(L.gp2d_assemble(_ptr(X), ntr, npad, _ptr(X), ntr, npad, ctypes.byref(desc), float(noise + jitter), 1,
+                            _ptr(A), n, s), "gp2d_assemble")
+    dinv = torch.empty((n // NB, NB, NB), dtype=torch.float64, device=dev)
+    info = torch.zeros(1, dtype=torch.int32, device=dev)
+    N.check(L.gp2d_potrf(_ptr(A), n, n, _ptr(dinv), _ptr(info), None, 0, s), "gp2d_potrf")
+    inf = int(info.item())
+    if inf != 0:
+        raise np.linalg.LinAlgError(
+            f"K_y is not positive definite (leading minor of order {inf}); "
+            "increase the noise / jitter (cf. sklearn _gpr.py:350-358)")
+    wbytes = int(L.gp2d_trtri_workspace(n))
+    work = torch.empty(wbytes // 8 + 1, dtype=torch.float64, device=dev)
+    N.check(L.gp2d_trtri(_ptr(A), n, n, _ptr(dinv), _ptr(work), wbytes, s), "gp2d_trtri")
+    del work, dinv
+    Y = _pad_obs(y, ntr, npad, bd, dev)
+    alpha = torch.empty(n, dtype=torch.float64, device=dev)
+    pbytes = int(L.gp2d_potrs_workspace(n))
+    pwork = torch.empty(pbytes // 8 + 1, dtype=torch.float64, device=dev)
+    N.check(L.gp2d_potrs_inv(_ptr(A), n, n, _ptr(Y), _ptr(alpha), _ptr(pwork), pbytes, s), "gp2d_potrs_inv")
+    return GPFit(kernel=kernel, noise=float(noise), x=X, n_train=ntr, n_pad=npad, W=A, alpha=alpha, device=dev)
+
+
+_VAR_MODES = {"latent": N.VAR_LATENT, "gpy": N.VAR_NOISY, "noisy": N.VAR_NOISY, "sklearn": N.VAR_CLIPPED,
+              "clipped": N.VAR_CLIPPED}
+
+
+class Predictor:
+    """Reusable predict workspace for one GPFit (chunked over the grid)."""
+
+    def __init__(self, gp: GPFit, chunk: int = 8192):
+        self.gp = gp
+        bd = gp.kernel.block_dim
+        unit = 64 if bd == 2 else 128
+        self.chunk = max(unit, (int(chunk) + unit - 1) // unit * unit)
+        self.wbytes = int(N.lib().gp2d_predict_workspace(gp.n, self.chunk, bd))
+        self.work = torch.empty(self.wbytes // 8 + 1, dtype=torch.float64, device=gp.device)
+
+    def __call__(self, xg, var_mode: str = "latent", compute_var: bool = True, out=None):
+        gp = self.gp
+        L = N.lib()
+        d, bd = gp.kernel.input_dim, gp.kernel.block_dim
+        G = _as_points(xg, d, gp.device)
+        m = G.shape[0]
+        if out is None:
+            mean = torch.empty(bd * m, dtype=torch.float64, device=gp.device)
+            var = torch.empty(bd * m, dtype=torch.float64, device=gp.device)
+        else:
+            mean, var = out
+        desc = gp.kernel.desc()
+        N.check(L.gp2d_predict(_ptr(gp.W), gp.n, gp.n, _ptr(gp.alpha), _ptr(gp.x), gp.n_train, gp.n_pad,
+                               _ptr(G), m, ctypes.byref(desc), _VAR_MODES[var_mode], float(gp.noise),
+                               int(bool(compute_var)), _ptr(mean), _ptr(var), self.chunk, _ptr(self.work),
+                               self.wbytes, _stream_handle(gp.device)), "gp2d_predict")
+        return mean, (var if compute_var else None)
+
+
+def predict(gp: GPFit, xg, var_mode: str = "latent", compute_var: bool = True, chunk: int = 8192):
+    return Predictor(gp, chunk)(xg, var_mode=var_mode, compute_var=compute_var)
+
+
+def timing_enable(on: bool = True):
+    N.lib().gp2d_timing_enable(int(bool(on)))
+
+
+def timing_read():
+    ms = ctypes.c_double()
+    cnt = ctypes.c_int64()
+    fl = ctypes.c_double()
+    N.check(N.lib().gp2d_timing_read(ctypes.byref(ms), ctypes.byref(cnt), ctypes.byref(fl)), "gp2d_timing_read")
+    return ms.value, cnt.value, fl.value

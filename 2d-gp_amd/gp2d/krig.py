@@ -1,0 +1,467 @@
+"""The reference's ``krig`` module surface, backed by the MI355X engine.
+
+Reference: krig.py (module functions), runKrig.py / runPredict.py (drivers),
+GP_laser.py:16-142 (the explicit-numpy posterior).  ``Krig`` is the stateful
+fit/predict object the north_star names (`krig.Krig`); the module functions
+keep the reference's names, argument meaning and error behaviour.
+
+Differences forced by the environment (documented in DESIGN.md):
+  * data files (Filtered_2016_2_7.pkl, .mat outputs, GPy pickles) do not exist:
+    functions take a track container (``Tracks``) or ``.npz`` paths; model files
+    are ``.npz`` (inputs + hyperparameters, optionally the factor);
+  * pyproj / NAD83 is absent: ``project`` is a signed local equirectangular
+    projection in km about (lat0, lon0);
+  * NetCDF output is SURVEY.md §8f item 3 (next): outputs are ``.npz``;
+  * hyperparameter optimisation (GPy optimize_restarts) is §8f item 1 (next):
+    ``runRestarts`` raises NotImplementedError;
+  * kernelType 2/3/4 use the 2-D spatial div-free / curl-free / mixed kernels on
+    the (Y, X) columns — the reference's spatio-temporal myKernel2 is missing from
+    the reference itself (krig.py:9).
+"""
+from __future__ import annotations
+
+import os
+import time
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import data as D
+from . import engine as E
+
+lat0 = 28.8
+lon0 = -88.6
+
+KERNEL_NAMES = {"df": "df", "divfree": "df", "div-free": "df", 1: "df",
+                "cf": "cf", "curlfree": "cf", "curl-free": "cf", 2: "cf",
+                "mixed": "mixed", "combined": "mixed", 3: "mixed",
+                "scalar": "scalar", "isotropic": "scalar", 0: "scalar"}
+
+
+def project(lon, lat, lon_0: float = lon0, lat_0: float = lat0):
+    """Signed local equirectangular projection to km (stands in for the NAD83
+    projection of krig.py:19-20,291-298, which needs pyproj)."""
+    R = 6371.0
+    x = R * np.cos(np.deg2rad(lat_0)) * np.deg2rad(np.asarray(lon, dtype=np.float64) - lon_0)
+    y = R * np.deg2rad(np.asarray(lat, dtype=np.float64) - lat_0)
+    return x, y
+
+
+def _to_numpy(t):
+    return t.detach().cpu().numpy() if isinstance(t, torch.Tensor) else np.asarray(t)
+
+
+# =============================================================================== Krig
+class Krig:
+    """Stateful GP kriging object: ``Krig(...).fit(X, obs).predict(Xg)``.
+
+    kernel: 'df' (divergence-free, GP_scripts divFree=1), 'cf' (curl-free, 2),
+    'mixed' (ratio·df + (1−ratio)·cf, GP_laser.py:113), 'scalar' (divFree=0),
+    a ``kern.myKernel``/``nonDivK``/``nonRotK`` instance, or an ``engine.KernelSpec``
+    (incl. family='ard' for the sklearn model of krig.scikit_prior).
+    var_mode: 'latent' (GP_laser.py:128-131), 'gpy' (+noise, GPy model.predict),
+    'sklearn' (+noise, clipped at 0, _gpr.py:473-485).
+    """
+
+    def __init__(self, kernel="df", l_df: float = 5.0, l_cf: float = 5.0, ratio: float = None,
+                 noise: float = 0.0025, jitter: float = 0.0, var_mode: str = "latent", device=None,
+                 chunk: int = 8192):
+        self.spec = self._make_spec(kernel, l_df, l_cf, ratio)
+        self.noise = float(noise)
+        self.jitter = float(jitter)
+        self.var_mode = var_mode
+        self.device = device
+        self.chunk = int(chunk)
+        self.gp = None
+        self._pred = None
+        self._X = None
+        self._y = None
+
+    @staticmethod
+    def _make_spec(kernel, l_df, l_cf, ratio):
+        if isinstance(kernel, E.KernelSpec):
+            return kernel
+        if hasattr(kernel, "_spec"):
+            return kernel._spec()
+        kind = KERNEL_NAMES[kernel.lower() if isinstance(kernel, str) else kernel]
+        if ratio is None:
+            ratio = 0.5 if kind == "mixed" else (0.0 if kind == "cf" else 1.0)
+        return E.KernelSpec(kind=kind, l_df=float(l_df), l_cf=float(l_cf), ratio=float(ratio))
+
+    # ------------------------------------------------------------------ fit
+    def fit(self, X, obs):
+        """X: (N, dim) inputs; obs: (2N,) = [u; v] (or (N, 2) columns u, v) for the
+        vector kernels, (N,) for the scalar ARD family."""
+        X = np.asarray(X, dtype=np.float64) if not isinstance(X, torch.Tensor) else X
+        bd = self.spec.block_dim
+        y = obs if isinstance(obs, torch.Tensor) else np.asarray(obs, dtype=np.float64)
+        if bd == 2 and not isinstance(y, torch.Tensor) and y.ndim == 2 and y.shape[1] == 2:
+            y = np.concatenate([y[:, 0], y[:, 1]])
+        self.gp = E.fit(self.spec, X, y, self.noise, jitter=self.jitter, device=self.device)
+        self._pred = E.Predictor(self.gp, self.chunk)
+        self._X, self._y = X, y
+        return self
+
+    def _check(self):
+        if self.gp is None:
+            raise RuntimeError("Krig.fit must be called before predict")
+
+    # ------------------------------------------------------------------ predict
+    def predict_device(self, Xg, var_mode=None, compute_var=True):
+        """Posterior mean and variance as device tensors ([u..., v...] for vector kernels)."""
+        self._check()
+        return self._pred(Xg, var_mode=var_mode or self.var_mode, compute_var=compute_var)
+
+    def predict(self, Xg, var_mode=None, compute_var=True):
+        """(mean, var) numpy arrays of shape (bd·M, 1), as GPy's model.predict returns
+        (krig.py:543-544; f[:M] = u, f[M:] = v, GP_plots.py:768-771)."""
+        mu, var = self.predict_device(Xg, var_mode=var_mode, compute_var=compute_var)
+        mu = _to_numpy(mu)[:, None]
+        return mu, (_to_numpy(var)[:, None] if compute_var else None)
+
+    def predict_grid(self, x, y, var_mode=None):
+        """GP_laser.py:107-136 on the grid meshgrid(x, y): returns uf, vf, uvar, vvar,
+        each reshaped to [y.size, x.size]."""
+        X, Y = np.meshgrid(x, y)
+        pts = np.stack([X.reshape(-1), Y.reshape(-1)], 1)
+        mu, var = self.predict_device(pts, var_mode=var_mode)
+        mu, var = _to_numpy(mu), _to_numpy(var)
+        M = pts.shape[0]
+        shp = [np.size(y), -1]
+        return (mu[:M].reshape(shp), mu[M:].reshape(shp), var[:M].reshape(shp), var[M:].reshape(shp))
+
+    # ------------------------------------------------------------------ state
+    @property
+    def param_array(self):
+        s = self.spec
+        if s.family == "ard":
+            hp = []
+            for v, ls in zip(s.variances, s.lengthscales):
+                hp += [v, *ls]
+            return np.array(hp + [self.noise])
+        return np.array([s.l_df, s.l_cf, s.ratio, self.noise])
+
+    def save(self, path: str, with_factor: bool = False):
+        """Checkpoint: inputs, observations, hyperparameters (and optionally W = L⁻¹, α),
+        the analogue of model.pickle (krig.py:412)."""
+        self._check()
+        s = self.spec
+        d = dict(X=_to_numpy(self._X), y=_to_numpy(self._y), family=s.family, kind=str(s.kind), l_df=s.l_df,
+                 l_cf=s.l_cf, ratio=s.ratio, variances=np.asarray(s.variances, dtype=np.float64),
+                 lengthscales=np.asarray(s.lengthscales, dtype=np.float64), noise=self.noise, jitter=self.jitter,
+                 var_mode=self.var_mode)
+        if with_factor:
+            d["W"] = _to_numpy(self.gp.W)
+            d["alpha"] = _to_numpy(self.gp.alpha)
+        np.savez(path, **d)
+
+    @classmethod
+    def load(cls, path: str, device=None, refit: bool = True):
+        z = np.load(path, allow_pickle=False)
+        fam = str(z["family"])
+        if fam == "ard":
+            spec = E.KernelSpec(family="ard", variances=tuple(z["variances"].tolist()),
+                                lengthscales=tuple(tuple(r) for r in z["lengthscales"].tolist()))
+        else:
+            spec = E.KernelSpec(kind=str(z["kind"]), l_df=float(z["l_df"]), l_cf=float(z["l_cf"]),
+                                ratio=float(z["ratio"]))
+        k = cls(spec, noise=float(z["noise"]), jitter=float(z["jitter"]), var_mode=str(z["var_mode"]),
+                device=device)
+        if refit:
+            k.fit(z["X"], z["y"])
+        return k
+
+
+# ===================================================================== module functions
+def rmse(ys, y):
+    """krig.rmse (krig.py:641-645)."""
+    error = np.reshape(np.asarray(ys) - np.asarray(y), [-1])
+    return np.sqrt(np.mean(np.square(error)))
+
+
+def getGrid(to, yo, xo, dt=0.5, dx=0.5, xL=40, yL=40):
+    """krig.getGrid (krig.py:648-678) — bit-exact (tests/golden/grids.npz)."""
+    return D.get_grid(to, yo, xo, dt, dx, xL, yL)
+
+
+def boundData(var, varlim, lat, lon, v, u):
+    """krig.boundData (krig.py:79-86)."""
+    return D.bound_data(var, varlim, lat, lon, v, u)
+
+
+@dataclass
+class Tracks:
+    """Drifter track container (the fields of laser_class.interpolated_tracks used by
+    krig.getData, krig.py:42-77): time (T,), lat/lon/u/v (T, D)."""
+    time: np.ndarray
+    lat: np.ndarray
+    lon: np.ndarray
+    u: np.ndarray
+    v: np.ndarray
+
+    @classmethod
+    def load(cls, path: str) -> "Tracks":
+        z = np.load(path, allow_pickle=False)
+        return cls(z["time"], z["lat"], z["lon"], z["u"], z["v"])
+
+    @classmethod
+    def synthetic(cls, n_time: int = 96, n_drifters: int = 64, seed: int = 2016) -> "Tracks":
+        """Drifters advected through the div-free Gaussian eddy of data.synthetic_tracks."""
+        rng = np.random.default_rng(seed)
+        x = rng.uniform(0, 60, n_drifters)
+        y = rng.uniform(0, 45, n_drifters)
+        dt_h = 0.25
+        X = np.empty((n_time, n_drifters))
+        Y = np.empty((n_time, n_drifters))
+        U = np.empty((n_time, n_drifters))
+        V = np.empty((n_time, n_drifters))
+        for t in range(n_time):
+            psi = np.exp(-((x - 30) ** 2 + (y - 22.5) ** 2) / 15.0 ** 2)
+            u = psi * (-2 * (y - 22.5) / 15.0 ** 2) + rng.normal(0, 0.02, n_drifters)
+            v = -psi * (-2 * (x - 30) / 15.0 ** 2) + rng.normal(0, 0.02, n_drifters)
+            X[t], Y[t], U[t], V[t] = x, y, u, v
+            x = x + u * 3.6 * dt_h
+            y = y + v * 3.6 * dt_h
+        R = 6371.0
+        lat = lat0 + np.rad2deg(Y / R)
+        lon = lon0 + np.rad2deg(X / (R * np.cos(np.deg2rad(lat0))))
+        return cls(np.arange(n_time) * dt_h * 3600.0, lat, lon, U, V)
+
+
+def getData(st, et, tracks: Tracks):
+    """krig.getData (krig.py:42-77) on a track container: time in hours from the first
+    sample, columns ordered by decreasing number of valid points."""
+    time_h = (tracks.time[st:et] - tracks.time[0]) / 3600.0
+    latt = tracks.lat[st:et, :]
+    lont = tracks.lon[st:et, :]
+    uob = tracks.u[st:et, :]
+    vob = tracks.v[st:et, :]
+    valid = np.array([np.size(np.where((~np.isnan(lont[:, i])) & (~np.isnan(latt[:, i])))[0])
+                      for i in range(latt.shape[1])])
+    order = np.squeeze(valid.argsort(axis=0))[::-1]
+    return time_h, latt[:, order], lont[:, order], vob[:, order], uob[:, order], valid[order]
+
+
+def _prepare(tracks, st, et, lalim, lolim, sample_step, skip):
+    """Data selection of krig.kriging (krig.py:274-381): bounds, projection, split,
+    NaN filter, T,Y,X stacking.  Returns dict of observation / test arrays."""
+    time_h, latt, lont, vob, uob, _ = getData(st, et, tracks)
+    if lolim[1] > lolim[0]:
+        latt, lont, vob, uob = boundData(lont, lolim, latt, lont, vob, uob)
+    if lalim[1] > lalim[0]:
+        latt, lont, vob, uob = boundData(latt, lalim, latt, lont, vob, uob)
+    xob, yob = project(lont, latt)
+    tob = np.repeat(time_h[:, None], latt.shape[1], axis=1)
+    yob[np.where(np.isnan(lont))] = np.nan
+    xob[np.where(np.isnan(lont))] = np.nan
+    if (sample_step < 0) or (skip > 1):
+        samples, testt, testd = D.drifter_split(tob.shape[0], tob.shape[1], sample_step, skip)
+
+        def pick(a):
+            return np.reshape(a[samples, ::skip], [-1, 1]), np.reshape(a[testt[:, None], testd], [-1, 1])
+    else:
+        samples, test = D.split_indices(xob.size, sample_step)
+
+        def pick(a):
+            return np.reshape(a, [-1])[samples, None], np.reshape(a, [-1])[test, None]
+    (to, tt), (yo, yt), (xo, xt) = pick(tob), pick(yob), pick(xob)
+    (lat_o, lat_t), (lon_o, lon_t) = pick(latt), pick(lont)
+    (uo, ut), (vo, vt) = pick(uob), pick(vob)
+    vo_mask = np.where((~np.isnan(xo)) & (~np.isnan(yo)))
+    vt_mask = np.where((~np.isnan(xt)) & (~np.isnan(yt)))
+    o = [a[vo_mask][:, None] for a in (to, yo, xo, lat_o, lon_o, uo, vo)]
+    t = [a[vt_mask][:, None] for a in (tt, yt, xt, lat_t, lon_t, ut, vt)]
+    return dict(X=np.concatenate([o[0], o[1], o[2]], 1), LL_o=np.concatenate([o[0], o[3], o[4]], 1),
+                uo=o[5], vo=o[6], Xt=np.concatenate([t[0], t[1], t[2]], 1),
+                LL_t=np.concatenate([t[0], t[3], t[4]], 1), ut=t[5], vt=t[6])
+
+
+def kriging(st, et, lalim=(0, 0), lolim=(0, 0), sample_step=5, skip=5, nKernels=1, output="rbfModel",
+            pkg="gp2d", kernelType=1, laser=1, tracks: Tracks = None, hyper: dict = None, device=None):
+    """krig.kriging (krig.py:259-418): build the GP model(s) for a drifter data window.
+
+    kernelType 1: scalar ARD RBF on (T, Y, X), one model per component (v, u);
+    2 / 3 / 4: div-free / curl-free / mixed vector kernel on (Y, X) with obs = [v; u]
+    (krig.py:392-404).  nKernels > 1 sums nKernels identical ARD terms (krig.py:405-407;
+    ≤ 2 supported).  Hyperparameters come from `hyper` (no optimisation here).
+    Writes output+'.npz' (the .mat of krig.py:417) and the model files; returns the models.
+    """
+    if tracks is None:
+        raise ValueError("tracks= is required (the reference's Filtered_2016_2_7.pkl is not available)")
+    t0 = time.time()
+    h = dict(l_df=5.0, l_cf=5.0, ratio=None, noise=0.0025, variance=1.0, lengthscale=(1.0, 1.0, 1.0))
+    h.update(hyper or {})
+    d = _prepare(tracks, st, et, lalim, lolim, sample_step, skip)
+    X, Xt = d["X"], d["Xt"]
+    models = {}
+    if kernelType == 1:
+        nk = min(int(nKernels), 2)
+        spec = E.KernelSpec(family="ard", variances=tuple([h["variance"]] * nk),
+                            lengthscales=tuple([tuple(h["lengthscale"])] * nk))
+        for name, obs in (("v", d["vo"]), ("u", d["uo"])):
+            k = Krig(spec, noise=h["noise"], var_mode="gpy", device=device).fit(X, obs[:, 0])
+            k.save(output + f"_{name}.npz")
+            models[name] = k
+        obs_all = np.concatenate([d["vo"], d["uo"]], 1)
+        obst = np.concatenate([d["vt"], d["ut"]], 1)
+    else:
+        kind = {2: "df", 3: "cf", 4: "mixed"}[int(kernelType)]
+        obs_all = np.concatenate([d["vo"], d["uo"]], 0)
+        obst = np.concatenate([d["vt"], d["ut"]], 0)
+        k = Krig(kind, l_df=h["l_df"], l_cf=h["l_cf"], ratio=h["ratio"], noise=h["noise"], var_mode="gpy",
+                 device=device).fit(X[:, 1:3], obs_all[:, 0])
+        tag = {2: "_divFree", 3: "_curlFree", 4: "_combined"}[int(kernelType)]
+        k.save(output + tag + ".npz")
+        models[tag] = k
+    np.savez(output + ".npz", Xo=X, obs=obs_all, Xt=Xt, LL_o=d["LL_o"], LL_t=d["LL_t"], test_points=obst,
+             kernelType=kernelType)
+    print("End of script, time : " + str(time.time() - t0))
+    return models
+
+
+def runRestarts(fname, nres=10, nKernels=2):
+    """krig.runRestarts (krig.py:430-468): GPy optimize_restarts of the hyperparameters."""
+    raise NotImplementedError("hyperparameter optimisation is SURVEY.md §8f item 1 (next round)")
+
+
+def predict(filename, tlim=(0, 0), ylim=(0, 0), xlim=(0, 0), dt=0.5, dx=0.5, xL=40, yL=40, Simul=0,
+            device=None):
+    """krig.predict (krig.py:471-574): grid posterior per time slice for the u and v
+    models saved by kriging(); writes filename+'_pred.npz' and returns
+    (Xp, V, U, VVar, UVar) reshaped [tp, yp, xp]."""
+    t0 = time.time()
+    f = np.load(filename + ".npz", allow_pickle=False)
+    kt = int(f["kernelType"]) if "kernelType" in f.files else 1
+    if (ylim[0] == ylim[1]) and (xlim[0] == xlim[1]):
+        Xo = f["Xo"]
+        Xp, tp, yp, xp = getGrid(Xo[:, 0], Xo[:, 1], Xo[:, 2])
+    else:
+        Xp, tp, yp, xp = getGrid(tlim, ylim, xlim, dt, dx, xL, yL)
+    inc = yp.size * xp.size
+    V, U, VV, UV = [], [], [], []
+    if kt == 1:
+        mv = Krig.load(filename + "_v.npz", device=device)
+        mu_ = Krig.load(filename + "_u.npz", device=device)
+    else:
+        tag = {2: "_divFree", 3: "_curlFree", 4: "_combined"}[kt]
+        mvec = Krig.load(filename + tag + ".npz", device=device)
+    for i in range(tp.size):                         # krig.py:541-557
+        Xp2 = Xp[i * inc:(i + 1) * inc, :]
+        if kt == 1:
+            v2, vv2 = mv.predict(Xp2)
+            u2, uv2 = mu_.predict(Xp2)
+        else:
+            f2, fv2 = mvec.predict(Xp2[:, 1:3])
+            v2, u2 = f2[:inc], f2[inc:]
+            vv2, uv2 = fv2[:inc], fv2[inc:]
+        V.append(v2)
+        U.append(u2)
+        VV.append(vv2)
+        UV.append(uv2)
+    shp = [tp.size, yp.size, xp.size]
+    V, U, VV, UV = (np.reshape(np.concatenate(a, 0), shp) for a in (V, U, VV, UV))
+    np.savez(filename + "_pred.npz", time=tp, y=yp, x=xp, v=V, u=U, vvar=VV, uvar=UV)
+    print("End of script, time : " + str(time.time() - t0))
+    return Xp, V, U, VV, UV
+
+
+def predictTest(filename, device=None):
+    """krig.predictTest (krig.py:578-616): predict at the held-out test points in 10
+    chunks (step = Nt // 10, the py2 integer division of krig.py:593)."""
+    f = np.load(filename + ".npz", allow_pickle=False)
+    Xt = f["Xt"]
+    obst = f["test_points"]
+    kt = int(f["kernelType"]) if "kernelType" in f.files else 1
+    Nt = Xt.shape[0]
+    step = max(Nt // 10, 1)
+    if kt == 1:
+        mv = Krig.load(filename + "_v.npz", device=device)
+        mu_ = Krig.load(filename + "_u.npz", device=device)
+    else:
+        tag = {2: "_divFree", 3: "_curlFree", 4: "_combined"}[kt]
+        mvec = Krig.load(filename + tag + ".npz", device=device)
+    V, U, VV, UV = [], [], [], []
+    for i in range(0, Nt, step):
+        Xt2 = Xt[i:i + step, :] if i + step < Nt else Xt[i:, :]
+        if kt == 1:
+            v2, vv2 = mv.predict(Xt2)
+            u2, uv2 = mu_.predict(Xt2)
+        else:
+            m = Xt2.shape[0]
+            f2, fv2 = mvec.predict(Xt2[:, 1:3])
+            v2, u2, vv2, uv2 = f2[:m], f2[m:], fv2[:m], fv2[m:]
+        V.append(v2)
+        U.append(u2)
+        VV.append(vv2)
+        UV.append(uv2)
+    V, U, VV, UV = (np.concatenate(a, 0) for a in (V, U, VV, UV))
+    np.savez(filename + "_test.npz", Xt=Xt, Vp=V, VpVar=VV, Up=U, UpVar=UV, test_points=obst)
+    return V, U, VV, UV
+
+
+def scikit_prior(filename0, varname="v", dt=0, tlim=6, radar="", xlim=(0, 0), ylim=(0, 0), dx=0, ind=0, xrange=3,
+                 HP=None, device=None):
+    """krig.scikit_prior (krig.py:88-207): fixed-hyperparameter scalar GP
+    HP0·RBF([lt,ly,lx]) (+ HP4·RBF) + White(noise) on the windowed observations,
+    predicted on the getGrid window at time dt.  Model inputs come from
+    filename0+'.npz' (written by kriging); HP = [var1, lt, ly, lx, (var2, lt, ly, lx,) noise]
+    (the GPy param_array the reference loads at krig.py:159-161).
+    Returns (U, Ustd²) reshaped [1, yg, xg] and writes the .npz output."""
+    if radar:
+        raise NotImplementedError("radar grids need NetCDF input (SURVEY.md §8f item 3)")
+    fm = np.load(filename0 + ".npz", allow_pickle=False)
+    if HP is None:
+        raise ValueError("HP (hyperparameters) is required: the reference reads them from a GPy pickle")
+    HP = np.asarray(HP, dtype=np.float64)
+    if not ((xlim[1] > xlim[0]) and (ylim[1] > ylim[0])):
+        raise ValueError("scikit_prior needs an explicit xlim/ylim window (pre-existing NetCDF grids are next)")
+    X, tcenter, yg, xg = getGrid([dt, dt + 1], ylim, xlim, 1, dx)   # krig.py:121
+    to, tt = fm["Xo"][:, 0], fm["Xt"][:, 0]
+    xo, xt = fm["Xo"][:, 2], fm["Xt"][:, 2]
+    ito = np.where((to >= tcenter - tlim) & (to <= tcenter + tlim) & (xo >= xlim[0] - xrange) & (xo <= xlim[1] + xrange))
+    itt = np.where((tt >= tcenter - tlim) & (tt <= tcenter + tlim) & (xt >= xlim[0] - xrange) & (xt <= xlim[1] + xrange))
+    Xo = fm["Xo"][ito, :].squeeze(0)
+    Xt = fm["Xt"][itt, :].squeeze(0)
+    XT = np.concatenate([Xo, Xt], axis=0)
+    obs = fm["obs"][ito, :].squeeze(0)
+    obst = fm["test_points"][itt, :].squeeze(0)
+    col = 1 if varname == "u" else 0
+    u = np.concatenate([obs[:, col], obst[:, col]])
+    N = HP.size - 1
+    variances = [HP[0]]
+    lengths = [tuple(HP[1:4])]
+    if N > 5:
+        variances.append(HP[4])
+        lengths.append(tuple(HP[5:8]))
+    spec = E.KernelSpec(family="ard", variances=tuple(variances), lengthscales=tuple(lengths))
+    # sklearn: WhiteKernel adds noise to K_y and to the predictive diagonal; fit adds alpha=1e-10
+    k = Krig(spec, noise=HP[-1], jitter=1e-10, var_mode="sklearn", device=device).fit(XT, u)
+    Um, Uvar = k.predict(X)
+    U = np.reshape(Um, [tcenter.size, yg.size, xg.size])
+    Ustd2 = np.reshape(Uvar, [tcenter.size, yg.size, xg.size])
+    out = filename0 + "_cyc_" + str(np.round(tcenter[0], decimals=2)) + "h_scikit_" + str(ind) + ".npz"
+    np.savez(out, time=tcenter, y=yg, x=xg, **{varname: U, varname + "var": Ustd2, "hyperparam_" + varname: HP})
+    return U, Ustd2
+
+
+def laser(xo, yo, uo, vo, l_df=5, l_cf=5, rate=0.5, noise=0.0025, nsamples=1, dx=0.5, device=None):
+    """GP_laser.laser (GP_laser.py:16-142) from projected observations (the pickle /
+    pyproj loading of GP_laser.py:26-78 is data plumbing outside the hot path):
+    stride-3 split, grid over obs ∪ test ± 5 km, mixed kernel rate·K_df + (1−rate)·K_cf
+    + noise·I, posterior mean / variance on the grid and mean at the test points.
+    Returns (x, y, uf, vf, xo, yo, uo, vo, uvar, vvar, xt, yt, ut, vt, uft, vft)."""
+    xo, yo, uo, vo = (np.asarray(a, dtype=np.float64).reshape(-1) for a in (xo, yo, uo, vo))
+    if nsamples > 0:
+        samples, test = D.split_indices(xo.size, 3)
+        xt, yt, ut, vt = xo[test], yo[test], uo[test], vo[test]
+        xo, yo, uo, vo = xo[samples], yo[samples], uo[samples], vo[samples]
+    else:
+        xt = yt = ut = vt = np.array([0.0])
+    x, y, Xs, Ys = D.laser_grid(xo, yo, xt, yt, dx=dx)
+    k = Krig("mixed", l_df=l_df, l_cf=l_cf, ratio=rate, noise=noise, device=device)
+    k.fit(np.stack([xo, yo], 1), np.concatenate([uo, vo]))
+    uf, vf, uvar, vvar = k.predict_grid(x, y)
+    ft, _ = k.predict(np.stack([xt, yt], 1), compute_var=False)
+    ft = ft[:, 0]
+    return x, y, uf, vf, xo, yo, uo, vo, uvar, vvar, xt, yt, ut, vt, ft[:ft.size // 2], ft[ft.size // 2:]

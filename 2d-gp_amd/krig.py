@@ -1,0 +1,5 @@
+"""`import krig` compatibility module: the reference's krig surface (krig.py) backed
+by the MI355X engine.  See gp2d/krig.py."""
+from gp2d.krig import (Krig, Tracks, boundData, getData, getGrid, kriging, laser, predict,  # noqa: F401
+                       predictTest, project, rmse, runRestarts, scikit_prior)
+from gp2d.kern import myKernel, nonDivK, nonRotK  # noqa: F401

@@ -1,0 +1,137 @@
+/*
+ * gp2d.h — C ABI of libgp2d.so, the MI355X (gfx950) GP-kriging engine.
+ *
+ * Drop-in boundary for rafaelcgon/2D-GP's hot path.  Every
+ * entry point below replaces one numpy/GPy/sklearn call of the reference;
+ * the replaced call site is cited per function.  All array pointers are
+ * caller-owned DEVICE buffers (e.g. torch-ROCm tensors' data_ptr()), fp64,
+ * row-major.  `stream` is a hipStream_t passed as void* (NULL = default).
+ * No function allocates device memory: callers size workspaces with the
+ * *_workspace() queries.
+ *
+ * Return value: 0 on success; < 0 on an argument or HIP launch error
+ * (gp2d_last_error() gives the message).  Numerical failure of the Cholesky
+ * factorisation is reported LAPACK-style through *info_dev (device int):
+ * 0 = success, k > 0 = the leading minor of order k is not positive definite.
+ *
+ * Layouts:
+ *   points          (N, dim) row-major; dim = 2 for the vector kernels (x1, x2),
+ *                   dim = 1..3 for the scalar ARD family (T, Y, X order);
+ *   vector kernels  component-major 2Np × 2Np: [[K_uu, K_uv], [K_vu, K_vv]]
+ *                   (GP_scripts.py:89-95), Np = gp2d_padded_points(N);
+ *   observations    y = [u_1..u_N, 0.., v_1..v_N, 0..] (2Np; GP_laser.py:98-99);
+ *   predictions     mean/var = [u_1..u_M, v_1..v_M] (GP_laser.py:134-136).
+ * Padded training points carry identity rows in K_y and zero cross-covariance,
+ * so they change nothing.
+ */
+#ifndef GP2D_H
+#define GP2D_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GP2D_ABI_VERSION 1
+
+/* kernel families */
+#define GP2D_FAMILY_VECTOR2D 0   /* 2×2 matrix-valued SE kernels on (x1, x2)          */
+#define GP2D_FAMILY_ARD_RBF  1   /* scalar Σ var·exp(−½Σ_d (Δ_d/ls_d)²) (krig.py:174-180) */
+
+/* vector2d kinds — the reference's divFree flag (GP_scripts.py:57-69) */
+#define GP2D_KIND_SCALAR   0     /* divFree=0: scalar SE broadcast into the 2×2 block  */
+#define GP2D_KIND_DIVFREE  1     /* divFree=1 (nonDivK, myKernel.py:159-176)           */
+#define GP2D_KIND_CURLFREE 2     /* divFree=2 (nonRotK, myKernel.py:255-271)           */
+#define GP2D_KIND_MIXED    3     /* ratio·K_df + (1−ratio)·K_cf (myKernel.py:27-53)    */
+
+/* predictive-variance conventions */
+#define GP2D_VAR_LATENT  0       /* Kss − k*ᵀK_y⁻¹k* (GP_laser.py:128-131)             */
+#define GP2D_VAR_NOISY   1       /* + likelihood noise (GPy model.predict)             */
+#define GP2D_VAR_CLIPPED 2       /* + noise, negatives clipped to 0 (sklearn _gpr.py:473-485) */
+
+typedef struct gp2d_kernel {
+    int32_t family;      /* GP2D_FAMILY_*                                              */
+    int32_t kind;        /* GP2D_KIND_* (vector2d)                                     */
+    double  l_df;        /* div-free length scale (σ for KIND_SCALAR)                  */
+    double  l_cf;        /* curl-free length scale                                     */
+    double  ratio;       /* weight of the div-free part (myKernel `ratio`, GP_laser `rate`) */
+    int32_t dim;         /* ARD: input dimension, 1..3                                 */
+    int32_t nterms;      /* ARD: number of RBF terms, 1..2                             */
+    double  var[2];      /* ARD: term variances                                        */
+    double  ls[2][3];    /* ARD: term length scales per dimension                      */
+} gp2d_kernel_t;
+
+/* ---- sizes ------------------------------------------------------------------- */
+int     gp2d_abi_version(void);
+int64_t gp2d_padded_points(int64_t n);                 /* round up to the 64-point tile */
+int     gp2d_block_dim(const gp2d_kernel_t* k);        /* 2 for vector2d, 1 for ARD      */
+double  gp2d_kernel_diag(const gp2d_kernel_t* k);      /* k(x,x) per component: myKernel.Kdiag, myKernel.py:55-57 */
+
+/* ---- covariance assembly -----------------------------------------------------
+ * Replaces GP_scripts.myKernel (GP_scripts.py:6-42), compute_K / compute_Ks
+ * (GP_scripts.py:74-123) and the GPy Kern.K methods (myKernel.py:27-53,
+ * 159-176, 255-271).  out is (bd·nb_pad) × (bd·... ) with leading dim ld:
+ * rows index xa's components, columns xb's.  diag_add (noise + jitter) is added
+ * on the diagonal when xa == xb (GP_laser.py:114-115); padded rows/columns are
+ * identity (when diag_add is used) or zero.                                     */
+int gp2d_assemble(const double* xa, int64_t na, int64_t na_pad,
+                  const double* xb, int64_t nb, int64_t nb_pad,
+                  const gp2d_kernel_t* k, double diag_add, int symmetric,
+                  double* out, int64_t ld, void* stream);
+
+/* ---- fit ---------------------------------------------------------------------
+ * gp2d_potrf: in-place lower Cholesky of the n×n SPD matrix A (n a multiple of
+ * 128).  Replaces np.linalg.inv(K) (GP_laser.py:118, GP_scripts.py:50) and the
+ * Cholesky inside GPy / sklearn (_gpr.py:349).  On return the strict upper
+ * triangle is zero.  If dinv != NULL it receives the (n/128) inverted 128×128
+ * diagonal blocks (input to gp2d_trtri).  *info_dev as LAPACK potrf.            */
+size_t gp2d_potrf_workspace(int64_t n);
+int gp2d_potrf(double* A, int64_t n, int64_t lda, double* dinv, int* info_dev,
+               void* work, size_t work_bytes, void* stream);
+
+/* gp2d_trtri: in-place inverse of the lower-triangular L (L → W = L⁻¹), using the
+ * diagonal-block inverses from gp2d_potrf (dinv) or computing them if NULL.     */
+size_t gp2d_trtri_workspace(int64_t n);
+int gp2d_trtri(double* A, int64_t n, int64_t lda, const double* dinv,
+               void* work, size_t work_bytes, void* stream);
+
+/* gp2d_potrs_inv: alpha = Wᵀ (W y) = K_y⁻¹ y given W = L⁻¹.  Replaces
+ * np.dot(Ki, y) (GP_scripts.py:45) / cho_solve (_gpr.py:360).                    */
+size_t gp2d_potrs_workspace(int64_t n);
+int gp2d_potrs_inv(const double* W, int64_t n, int64_t ldw, const double* y, double* alpha,
+                   void* work, size_t work_bytes, void* stream);
+
+/* ---- predict ------------------------------------------------------------------
+ * Posterior mean and variance at m points.  Replaces compute_Ks + getMean +
+ * the Kss − Ks·Ki·Ksᵀ diagonal (GP_laser.py:122-136), GPy model.predict
+ * (krig.py:543-544) and sklearn predict(return_std=True) (_gpr.py:436-490).
+ * W: n×n inverse Cholesky factor, n = bd·ntr_pad; alpha: n; xtr (ntr, dim);
+ * xg (m, dim).  mean, var: bd·m outputs ([u..., v...] for vector2d).
+ * var_mode: GP2D_VAR_*; noise is added for NOISY/CLIPPED.  The grid is
+ * processed in chunks of `chunk` points (multiple of 64); the workspace
+ * depends on (n, chunk).  Deterministic: no atomics, fixed reduction order, so
+ * results do not depend on how the grid is sharded across GPUs.                  */
+size_t gp2d_predict_workspace(int64_t n, int64_t chunk, int bd);
+int gp2d_predict(const double* W, int64_t n, int64_t ldw, const double* alpha,
+                 const double* xtr, int64_t ntr, int64_t ntr_pad,
+                 const double* xg, int64_t m, const gp2d_kernel_t* k,
+                 int var_mode, double noise, int compute_var,
+                 double* mean, double* var, int64_t chunk,
+                 void* work, size_t work_bytes, void* stream);
+
+/* ---- instrumentation ------------------------------------------------------------
+ * When enabled, every launch of the predict variance kernel (the dominant
+ * kernel) is bracketed by hipEvents on its stream; gp2d_timing_read()
+ * synchronises those events and returns the summed milliseconds, the launch
+ * count and the summed algorithmic flop count, then resets the counters.        */
+void gp2d_timing_enable(int on);
+int  gp2d_timing_read(double* total_ms, int64_t* launches, double* flops);
+
+const char* gp2d_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GP2D_H */

@@ -66,7 +66,8 @@ def vector_kernel(xa, xb, kind=KIND_DIVFREE, l_df=1.0, l_cf=1.0, ratio=1.0):
     compute_K/compute_Ks with divFree=0 (GP_scripts.py:74-123), which broadcasts
     the scalar SE value into all four entries of each 2×2 block.
     For kind=mixed the result is ratio·K_df(l_df) + (1−ratio)·K_cf(l_cf)
-    (GP_scripts.py:42; GP_laser.py:113,122).  For kind=scalar `l_df` is σ.
+    (GP_scripts.py:42; GP_laser.py:113,122).  kind=df uses l_df, kind=cf uses
+    l_cf, kind=scalar uses l_df as σ.
     """
     kind = kind_code(kind)
     xa = np.asarray(xa, dtype=np.float64).reshape(-1, 2)
@@ -80,7 +81,8 @@ def vector_kernel(xa, xb, kind=KIND_DIVFREE, l_df=1.0, l_cf=1.0, ratio=1.0):
         k12 = ratio * a12 + (1 - ratio) * b12
         k22 = ratio * a22 + (1 - ratio) * b22
     else:
-        k11, k12, k22 = _block_terms(d1, d2, l_df, kind)
+        length = l_cf if kind == KIND_CURLFREE else l_df
+        k11, k12, k22 = _block_terms(d1, d2, length, kind)
     return np.block([[k11, k12], [k12, k22]])
 
 
@@ -92,6 +94,8 @@ def kernel_diag(kind=KIND_DIVFREE, l_df=1.0, l_cf=1.0, ratio=1.0):
         return ratio * (1.0 / l_df ** 2) + (1 - ratio) * (1.0 / l_cf ** 2)
     if kind == KIND_SCALAR:
         return np.square(1.0 / l_df) * np.square(l_df)
+    if kind == KIND_CURLFREE:
+        return 1.0 / l_cf ** 2
     return 1.0 / l_df ** 2
 
 

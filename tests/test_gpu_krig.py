@@ -1,0 +1,121 @@
+"""The reference-compatible surface (krig / kern) on the GPU vs golden vectors and the oracle."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("no HIP device", allow_module_level=True)
+
+import krig  # noqa: E402
+from gp2d import engine as E  # noqa: E402
+from gp2d import kern  # noqa: E402
+from oracle import gp2d_oracle as O  # noqa: E402
+
+
+def rel(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300))
+
+
+def test_laser_recipe_golden(golden):
+    """GP_laser.laser posterior (exec'd reference loops) — mean/var within 1e-10."""
+    g = golden("laser_mixed_N256.npz")
+    # feed the raw (pre-split) observations back in the reference's order
+    n = int(g["n_raw"])
+    xo = np.empty(n); yo = np.empty(n); uo = np.empty(n); vo = np.empty(n)
+    for arr, a, b in ((xo, "xo", "xt"), (yo, "yo", "yt"), (uo, "uo", "ut"), (vo, "vo", "vt")):
+        arr[g["samples"]] = g[a]
+        arr[g["test"]] = g[b]
+    out = krig.laser(xo, yo, uo, vo, l_df=5.0, l_cf=5.0, rate=0.5, noise=0.0025, dx=1.0)
+    x, y, uf, vf, _, _, _, _, uvar, vvar, xt, yt, ut, vt, uft, vft = out
+    assert np.array_equal(x, g["x"]) and np.array_equal(y, g["y"])
+    assert np.array_equal(xt, g["xt"])
+    for a, b in ((uf, "uf"), (vf, "vf"), (uvar, "uvar"), (vvar, "vvar"), (uft, "uft"), (vft, "vft")):
+        assert rel(a, g[b]) < 1e-10, b
+
+
+def test_kern_plugin_golden(golden):
+    g = golden("gp_scripts_small.npz")
+    xa = np.stack([g["x1"], g["x2"]], 1)
+    xb = np.stack([g["x1s"], g["x2s"]], 1)
+    s = float(g["sigma"])
+    assert rel(kern.nonDivK(2, [0, 1], s).K(xa), g["K_1"]) < 1e-13
+    assert rel(kern.nonRotK(2, [0, 1], s).K(xb, xa), g["Ks_2"]) < 1e-13
+    assert rel(kern.compute_K(g["x1"], g["x2"], s, 0), g["K_0"]) < 1e-13
+    assert rel(kern.compute_Ks(g["x1"], g["x2"], g["x1s"], g["x2s"], s, 1), g["Ks_1"]) < 1e-13
+    l_df, l_cf, r = g["myK_params"]
+    mk = kern.myKernel(2, [0, 1], l_df, l_cf, r)
+    assert rel(mk.K(xa), g["myK_mixed_aa"]) < 1e-13
+    assert rel(mk.K(xa, xb), g["myK_mixed_ab"]) < 1e-13
+    assert rel(kern.vector_K(xa, xb, l_df, l_cf, r), g["myK_mixed_ab"]) < 1e-13
+    assert np.allclose(mk.Kdiag(xa), np.diag(g["myK_mixed_aa"]), rtol=1e-14, atol=0)
+
+
+@pytest.mark.parametrize("kind", [0, 1, 2])
+def test_small_posterior_golden(golden, kind):
+    g = golden("gp_scripts_small.npz")
+    xa = np.stack([g["x1"], g["x2"]], 1)
+    xb = np.stack([g["x1s"], g["x2s"]], 1)
+    name = {0: "scalar", 1: "df", 2: "cf"}[kind]
+    k = krig.Krig(name, l_df=float(g["sigma"]), l_cf=float(g["sigma"]), noise=float(g["noise"])).fit(xa, g["y"])
+    mu, var = k.predict(xb)
+    M = xb.shape[0]
+    assert rel(mu[:, 0], g[f"mean_{kind}"]) < 1e-10
+    assert rel(var[:M, 0], g[f"uvar_{kind}"]) < 1e-10
+    assert rel(var[M:, 0], g[f"vvar_{kind}"]) < 1e-10
+
+
+def test_sklearn_config_A_golden(golden):
+    """krig.scikit_prior's model on the GPU ARD family vs sklearn 1.7.2 (fixture)."""
+    g = golden("sklearn_ard_N128.npz")
+    HP = g["HP"]
+    spec = E.KernelSpec(family="ard", variances=(HP[0], HP[4]), lengthscales=(tuple(HP[1:4]), tuple(HP[5:8])))
+    k = krig.Krig(spec, noise=HP[8], jitter=1e-10, var_mode="sklearn").fit(g["X"], g["u"])
+    mu, var = k.predict(g["Xp"])
+    assert rel(mu[:, 0], g["mean"]) < 1e-10
+    assert rel(np.sqrt(var[:, 0]), g["std"]) < 1e-10
+
+
+def test_var_modes_and_save_load(tmp_path):
+    rng = np.random.default_rng(5)
+    x = rng.uniform(0, 30, (150, 2))
+    y = rng.normal(0, 0.3, 300)
+    xg = rng.uniform(0, 30, (333, 2))
+    k = krig.Krig("mixed", l_df=4.0, l_cf=6.0, ratio=0.3, noise=0.01).fit(x, y)
+    m0, v0 = k.predict(xg)
+    _, v1 = k.predict(xg, var_mode="gpy")
+    assert np.allclose(v1 - v0, 0.01, rtol=0, atol=1e-12)
+    mo, vo = O.fit_predict(x, y, xg, kind="mixed", l_df=4.0, l_cf=6.0, ratio=0.3, noise=0.01)
+    assert rel(m0[:, 0], mo) < 1e-10 and rel(v0[:, 0], vo) < 1e-10
+    p = str(tmp_path / "m.npz")
+    k.save(p)
+    k2 = krig.Krig.load(p)
+    m2, v2 = k2.predict(xg)
+    assert np.array_equal(m2, m0) and np.array_equal(v2, v0)
+
+
+def test_kriging_predict_pipeline(tmp_path):
+    """kriging → predict → predictTest on synthetic drifters (kernelType 2 and 1)."""
+    tr = krig.Tracks.synthetic(n_time=24, n_drifters=40)
+    out = str(tmp_path / "model")
+    models = krig.kriging(0, 24, sample_step=-2, skip=2, nKernels=1, output=out, kernelType=2, tracks=tr)
+    k = models["_divFree"]
+    f = np.load(out + ".npz")
+    assert f["Xo"].shape[1] == 3 and f["obs"].shape[0] == 2 * f["Xo"].shape[0]
+    Xp, V, U, VV, UV = krig.predict(out, tlim=[0, 2], ylim=[-5, 40], xlim=[-5, 50], dt=1.0, dx=2.0)
+    assert V.shape == U.shape == VV.shape == UV.shape and V.shape[0] == 2
+    # same posterior as the oracle with obs=[v; u] on the (Y, X) columns
+    pts = Xp[:V.shape[1] * V.shape[2], 1:3]
+    mo, vo = O.fit_predict(f["Xo"][:, 1:3], f["obs"][:, 0], pts, kind="df", l_df=5.0, noise=0.0025,
+                           var_mode="gpy")
+    M = pts.shape[0]
+    assert rel(V[0].reshape(-1), mo[:M]) < 1e-10 and rel(U[0].reshape(-1), mo[M:]) < 1e-10
+    assert rel(VV[0].reshape(-1), vo[:M]) < 1e-10
+    V2, U2, VV2, UV2 = krig.predictTest(out)
+    assert V2.shape[0] == f["Xt"].shape[0]
+    models = krig.kriging(0, 24, sample_step=-2, skip=2, nKernels=2, output=out + "_rbf", kernelType=1, tracks=tr,
+                          hyper=dict(variance=0.1, lengthscale=(5.0, 8.0, 8.0), noise=0.001))
+    assert set(models) == {"u", "v"}
+    Xp, V, U, VV, UV = krig.predict(out + "_rbf", tlim=[0, 2], ylim=[-5, 40], xlim=[-5, 50], dt=1.0, dx=3.0)
+    assert np.all(np.isfinite(V)) and np.all(VV > 0)

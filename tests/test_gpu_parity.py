@@ -1,0 +1,78 @@
+"""HIP path vs the CPU oracle on identical seeded inputs (calls through the C ABI).
+
+Tolerances (north_star): fp64 posterior mean / variance within 1e-10 relative,
+measured normwise (max |a−b| / max |b|) per output vector; covariance entries
+within 1e-13 relative to the matrix max-norm.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("no HIP device", allow_module_level=True)
+
+from gp2d import engine as E  # noqa: E402
+from oracle import gp2d_oracle as O  # noqa: E402
+
+
+def rel(a, b):
+    a = np.asarray(a)
+    b = np.asarray(b)
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300))
+
+
+def tracks(n, seed=2016):
+    rng = np.random.default_rng(seed)
+    x = np.stack([rng.uniform(0, 60, n), rng.uniform(0, 45, n)], 1)
+    u = np.sin(x[:, 1] / 7) + rng.normal(0, 0.05, n)
+    v = np.cos(x[:, 0] / 9) + rng.normal(0, 0.05, n)
+    return x, np.concatenate([u, v])
+
+
+@pytest.mark.parametrize("kind,ratio", [("df", 1.0), ("cf", 0.0), ("mixed", 0.3), ("scalar", 1.0)])
+@pytest.mark.parametrize("na,nb", [(1, 1), (37, 100), (130, 64)])
+def test_assemble_matches_oracle(kind, ratio, na, nb):
+    rng = np.random.default_rng(na * 1000 + nb)
+    xa = rng.uniform(0, 10, (na, 2))
+    xb = rng.uniform(0, 10, (nb, 2))
+    ks = E.KernelSpec(kind=kind, l_df=2.5, l_cf=3.5, ratio=ratio)
+    K = E.assemble(ks, xa, xb).cpu().numpy()
+    R = O.vector_kernel(xa, xb, kind, 2.5, 3.5, ratio)
+    assert K.shape == R.shape
+    assert rel(K, R) < 1e-13
+
+
+def test_assemble_golden_small(golden):
+    g = golden("gp_scripts_small.npz")
+    xa = np.stack([g["x1"], g["x2"]], 1)
+    xb = np.stack([g["x1s"], g["x2s"]], 1)
+    for kind, name in ((1, "df"), (2, "cf"), (0, "scalar")):
+        ks = E.KernelSpec(kind=name, l_df=float(g["sigma"]), l_cf=float(g["sigma"]))
+        assert rel(E.assemble(ks, xa).cpu().numpy(), g[f"K_{kind}"]) < 1e-13
+        assert rel(E.assemble(ks, xb, xa).cpu().numpy(), g[f"Ks_{kind}"]) < 1e-13
+
+
+@pytest.mark.parametrize("ntr,m,kind", [(16, 64, "df"), (100, 300, "mixed"), (256, 1000, "cf"), (700, 2500, "df")])
+def test_fit_predict_matches_oracle(ntr, m, kind):
+    x, y = tracks(ntr, seed=ntr)
+    rng = np.random.default_rng(m)
+    xg = np.stack([rng.uniform(-5, 65, m), rng.uniform(-5, 50, m)], 1)
+    ks = E.KernelSpec(kind=kind, l_df=5.0, l_cf=4.0, ratio=0.5 if kind == "mixed" else 1.0)
+    gp = E.fit(ks, x, y, noise=0.0025)
+    mu, var = E.predict(gp, xg, chunk=256)
+    mo, vo = O.fit_predict(x, y, xg, kind=kind, l_df=5.0, l_cf=4.0, ratio=ks.ratio, noise=0.0025)
+    assert rel(mu.cpu().numpy(), mo) < 1e-10
+    assert rel(var.cpu().numpy(), vo) < 1e-10
+
+
+def test_golden_mykernel_N1024(golden):
+    g = golden("mykernel_mixed_N1024.npz")
+    x = np.stack([g["x"], g["y"]], 1)
+    y = np.concatenate([g["u"], g["v"]])
+    ks = E.KernelSpec(kind="mixed", l_df=5.0, l_cf=5.0, ratio=0.5)
+    gp = E.fit(ks, x, y, noise=float(g["noise"]))
+    mu, var = E.predict(gp, g["xg"])
+    assert rel(mu.cpu().numpy(), g["mean"]) < 1e-10
+    assert rel(var.cpu().numpy(), g["var"]) < 1e-10

@@ -1,0 +1,118 @@
+"""CPU-side checks: the C-ABI library loads and exports every symbol of
+include/gp2d.h, the host index/grid logic is bit-exact with the reference's
+golden vectors, and the compute path fails loudly without a HIP device."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+
+def header_symbols():
+    txt = open(os.path.join(ROOT, "include", "gp2d.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(gp2d_[a-z_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_header_symbol():
+    from gp2d import _native
+    L = _native.lib()
+    syms = header_symbols()
+    assert len(syms) >= 15
+    for s in syms:
+        assert hasattr(L, s), s
+    assert set(syms) == set(_native.EXPORTS)
+    assert L.gp2d_abi_version() == 1
+    assert L.gp2d_padded_points(1) == 64 and L.gp2d_padded_points(64) == 64 and L.gp2d_padded_points(65) == 128
+
+
+def test_kernel_diag_abi():
+    import ctypes
+    from gp2d import _native as N
+    L = N.lib()
+    k = N.vector_kernel_desc(N.KIND_MIXED, 2.0, 4.0, 0.25)
+    assert L.gp2d_kernel_diag(ctypes.byref(k)) == pytest.approx(0.25 / 4 + 0.75 / 16, rel=1e-15)
+    k = N.vector_kernel_desc(N.KIND_DIVFREE, 0.2)
+    assert L.gp2d_kernel_diag(ctypes.byref(k)) == pytest.approx(25.0, rel=1e-15)  # plots/Cov_divFree.png peak
+    a = N.ard_kernel_desc([0.8, 0.2], [[3, 4, 5], [10, 1.5, 2]])
+    assert L.gp2d_kernel_diag(ctypes.byref(a)) == pytest.approx(1.0)
+    assert L.gp2d_block_dim(ctypes.byref(a)) == 1 and L.gp2d_block_dim(ctypes.byref(k)) == 2
+
+
+def test_argument_errors_are_reported():
+    import ctypes
+    from gp2d import _native as N
+    L = N.lib()
+    k = N.vector_kernel_desc(N.KIND_DIVFREE, -1.0)
+    rc = L.gp2d_assemble(None, 1, 64, None, 1, 64, ctypes.byref(k), 0.0, 1, None, 128, None)
+    assert rc < 0 and b"l_df" in L.gp2d_last_error()
+    rc = L.gp2d_potrf(None, 100, 100, None, None, None, 0, None)
+    assert rc < 0 and b"multiple of 128" in L.gp2d_last_error()
+
+
+def test_no_cpu_fallback():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("HIP device present")
+    from gp2d import engine as E
+    from gp2d import NativeLibraryError
+    with pytest.raises(NativeLibraryError):
+        E.fit(E.KernelSpec(), np.zeros((4, 2)), np.zeros(8), 0.01)
+
+
+def test_split_indices_bit_exact(golden):
+    from gp2d import data as D
+    g = golden("split_indices.npz")
+    for step in (2, 3, 5):
+        for n in g["sizes"]:
+            s, t = D.split_indices(int(n), step)
+            assert np.array_equal(t, g[f"test_{step}_{n}"])
+            assert np.array_equal(s, np.arange(0, n, step))
+
+
+def test_laser_split_and_grid(golden):
+    from gp2d import data as D
+    g = golden("laser_mixed_N256.npz")
+    s, t = D.split_indices(int(g["n_raw"]), 3)
+    assert np.array_equal(s, g["samples"]) and np.array_equal(t, g["test"])
+    x, y, _, _ = D.laser_grid(g["xo"], g["yo"], g["xt"], g["yt"], dx=1.0)
+    assert np.array_equal(x, g["x"]) and np.array_equal(y, g["y"])
+
+
+def test_get_grid_bit_exact(golden):
+    import krig
+    g = golden("grids.npz")
+    for i in range(int(g["ncases"])):
+        X, tg, yg, xg = krig.getGrid(g[f"c{i}_to"], g[f"c{i}_yo"], g[f"c{i}_xo"], float(g[f"c{i}_dt"]),
+                                     float(g[f"c{i}_dx"]), float(g[f"c{i}_xL"]), float(g[f"c{i}_yL"]))
+        assert np.array_equal(X, g[f"c{i}_X"]) and np.array_equal(tg, g[f"c{i}_tg"])
+        assert np.array_equal(yg, g[f"c{i}_yg"]) and np.array_equal(xg, g[f"c{i}_xg"])
+
+
+def test_drifter_split_matches_reference_expression():
+    from gp2d import data as D
+    for nt, nd, ss, skip in [(96, 40, -2, 1), (96, 40, -1, 3), (50, 37, -4, 1), (50, 37, -1, 2)]:
+        samples, testt, testd = D.drifter_split(nt, nd, ss, skip)
+        # krig.py:304-316, verbatim numpy expressions
+        ss_ = abs(ss)
+        ref_s = np.arange(0, nt, ss_)
+        if skip > 1:
+            ref_tt = np.arange(nt)
+            ref_td = np.array(list(set(np.arange(0, nd)) - set(np.arange(0, nd, skip))))
+        else:
+            ref_td = np.arange(0, nd)
+            ref_tt = np.array(list(set(np.arange(0, nt)) - set(ref_s))) if ss_ > 1 else ref_s
+        assert np.array_equal(samples, ref_s) and np.array_equal(testt, ref_tt) and np.array_equal(testd, ref_td)
+
+
+def test_shard_ranges_cover_and_align():
+    from gp2d import data as D
+    for m in (1, 63, 64, 65, 65536, 262144 + 17):
+        for w in (1, 2, 3, 4, 8):
+            parts = [D.shard_range(m, w, r) for r in range(w)]
+            assert parts[0][0] == 0 and parts[-1][1] == m
+            for (a, b), (c, d) in zip(parts, parts[1:]):
+                assert b == c
+            assert all(a % 64 == 0 or a == m for a, _ in parts)

@@ -24,11 +24,11 @@ def test_compute_K_Ks_layout(golden, kind):
     xa = np.stack([g["x1"], g["x2"]], 1)
     xb = np.stack([g["x1s"], g["x2s"]], 1)
     s = float(g["sigma"])
-    K = O.vector_kernel(xa, xa, kind=kind, l_df=s)
-    Ks = O.vector_kernel(xb, xa, kind=kind, l_df=s)
+    K = O.vector_kernel(xa, xa, kind=kind, l_df=s, l_cf=s)
+    Ks = O.vector_kernel(xb, xa, kind=kind, l_df=s, l_cf=s)
     assert rel_err(K, g[f"K_{kind}"]) < 1e-13
     assert rel_err(Ks, g[f"Ks_{kind}"]) < 1e-13
-    assert np.allclose(np.full(2 * xb.shape[0], O.kernel_diag(kind, l_df=s)), g[f"Kssdiag_{kind}"], rtol=1e-15, atol=0)
+    assert np.allclose(np.full(2 * xb.shape[0], O.kernel_diag(kind, l_df=s, l_cf=s)), g[f"Kssdiag_{kind}"], rtol=1e-15, atol=0)
 
 
 @pytest.mark.parametrize("kind", [0, 1, 2])
@@ -37,7 +37,8 @@ def test_small_posterior(golden, kind, method):
     g = golden("gp_scripts_small.npz")
     xa = np.stack([g["x1"], g["x2"]], 1)
     xb = np.stack([g["x1s"], g["x2s"]], 1)
-    fit = O.OracleFit(xa, g["y"], kind, float(g["sigma"]), 1.0, 1.0, float(g["noise"]), method=method)
+    fit = O.OracleFit(xa, g["y"], kind, float(g["sigma"]), float(g["sigma"]), 1.0, float(g["noise"]),
+                      method=method)
     mu, var = fit.predict(xb)
     M = xb.shape[0]
     assert rel_err(mu, g[f"mean_{kind}"]) < 1e-10
@@ -123,7 +124,7 @@ def test_known_answers():
     # k(x,x) = I/ℓ²; plots/Cov_divFree.png peaks at 25 = 1/0.2²
     K = O.vector_kernel([[0.3, -1.2]], [[0.3, -1.2]], "df", 0.2)
     assert np.allclose(K, np.eye(2) * 25.0, rtol=0, atol=1e-12)
-    K = O.vector_kernel([[0.3, -1.2]], [[0.3, -1.2]], "cf", 0.2)
+    K = O.vector_kernel([[0.3, -1.2]], [[0.3, -1.2]], "cf", 0.2, 0.2)
     assert np.allclose(K, np.eye(2) * 25.0, rtol=0, atol=1e-12)
     # single observation at the origin, no noise: mean at origin = observation (GP_plots.py:457-484)
     for kind in ("df", "cf"):
