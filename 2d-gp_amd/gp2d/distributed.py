@@ -1,0 +1,108 @@
+"""Multi-GPU grid sharding: one process per GPU, fit once,
+broadcast the inverse Cholesky factor over RCCL (xGMI), predict disjoint,
+tile-aligned grid shards, gather in rank order.
+
+Grid points are independent given (X_train, W = L⁻¹, α, hyperparameters), and
+every per-point reduction in the predict kernels has a fixed order that does not
+depend on shard boundaries, so the concatenated result is bit-identical to the
+single-GPU result.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import data as D
+from . import engine as E
+
+
+def world():
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(), dist.get_rank()
+    return 1, 0
+
+
+def broadcast_fit(gp: E.GPFit | None, spec: E.KernelSpec, noise: float, x, device, src: int = 0) -> E.GPFit:
+    """Broadcast W, α and the training points from `src` to every rank (RCCL
+    ncclBroadcast under the 'nccl' backend).  Ranks other than `src` pass gp=None."""
+    ws, rank = world()
+    if ws == 1:
+        return gp
+    meta = torch.zeros(3, dtype=torch.int64, device=device)
+    if rank == src:
+        meta[0], meta[1], meta[2] = gp.n, gp.n_train, gp.n_pad
+    dist.broadcast(meta, src)
+    n, ntr, npad = (int(v) for v in meta.tolist())
+    if rank != src:
+        W = torch.empty((n, n), dtype=torch.float64, device=device)
+        alpha = torch.empty(n, dtype=torch.float64, device=device)
+        X = torch.empty((ntr, spec.input_dim), dtype=torch.float64, device=device)
+    else:
+        W, alpha, X = gp.W, gp.alpha, gp.x
+    dist.broadcast(W, src)
+    dist.broadcast(alpha, src)
+    dist.broadcast(X, src)
+    if rank == src:
+        return gp
+    return E.GPFit(kernel=spec, noise=float(noise), x=X, n_train=ntr, n_pad=npad, W=W, alpha=alpha,
+                   device=torch.device(device))
+
+
+def fit_sharded(spec: E.KernelSpec, x, y, noise: float, device, mode: str = "bcast", jitter: float = 0.0):
+    """mode 'bcast': rank 0 fits, factor broadcast over RCCL; 'replicate': every rank
+    fits redundantly (no communication)."""
+    ws, rank = world()
+    if ws == 1 or mode == "replicate":
+        return E.fit(spec, x, y, noise, jitter=jitter, device=device)
+    gp = E.fit(spec, x, y, noise, jitter=jitter, device=device) if rank == 0 else None
+    return broadcast_fit(gp, spec, noise, x, device)
+
+
+def predict_shard(pred: E.Predictor, xg_all, var_mode: str = "latent", compute_var: bool = True, align: int = 64):
+    """Predict this rank's contiguous shard of the flattened grid; returns
+    (lo, hi, mean, var) with mean/var in the [u..., v...] layout of the shard."""
+    ws, rank = world()
+    m = int(xg_all.shape[0])
+    lo, hi = D.shard_range(m, ws, rank, align)
+    mean, var = pred(xg_all[lo:hi], var_mode=var_mode, compute_var=compute_var)
+    return lo, hi, mean, var
+
+
+def gather_shards(m: int, bd: int, lo: int, hi: int, mean, var, device):
+    """All-gather the shards and reassemble the full [u(M)..., v(M)...] vectors in rank order."""
+    ws, rank = world()
+    if ws == 1:
+        return mean, var
+    ranges = [D.shard_range(m, ws, r) for r in range(ws)]
+    maxlen = max(b - a for a, b in ranges)
+    outs = []
+    for t in (mean, var):
+        buf = torch.zeros(bd * maxlen, dtype=torch.float64, device=device)
+        k = hi - lo
+        for c in range(bd):
+            buf[c * maxlen:c * maxlen + k] = t[c * k:(c + 1) * k]
+        parts = [torch.empty_like(buf) for _ in range(ws)]
+        dist.all_gather(parts, buf)
+        full = torch.empty(bd * m, dtype=torch.float64, device=device)
+        for (a, b), p in zip(ranges, parts):
+            k = b - a
+            for c in range(bd):
+                full[c * m + a:c * m + b] = p[c * maxlen:c * maxlen + k]
+        outs.append(full)
+    return outs[0], outs[1]
+
+
+def shard_layout(m: int, bd: int, world_size: int):
+    """Host-side description of the shards (used by tests): list of (lo, hi)."""
+    return [D.shard_range(m, world_size, r) for r in range(world_size)]
+
+
+def assemble_from_shards(m: int, bd: int, shards):
+    """Concatenate per-rank [u..., v...] shard vectors into the global layout (numpy)."""
+    full = np.empty(bd * m)
+    for lo, hi, vec in shards:
+        k = hi - lo
+        for c in range(bd):
+            full[c * m + lo:c * m + hi] = vec[c * k:(c + 1) * k]
+    return full

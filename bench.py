@@ -1,0 +1,204 @@
+"""Headline benchmark: posterior grid points/s (fit + predict), N_train = 4096,
+divergence-free 2-D SE vector kernel, 256×256 grid per GPU (BASELINE.json).
+
+One "step" = K_y assembly + POTRF + TRTRI + α (rank 0, W/α broadcast over RCCL
+when N > 1) + posterior mean AND variance at every point of this rank's grid
+shard.  Inputs are resident in HBM before the timed region.  Weak scaling: each
+GPU owns 65,536 points of a 256 × (256·N) global grid.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line (the driver contract) with `roofline` (dominant
+kernel: the variance contraction, timed live with HIP events on its stream) and
+`cpu_baseline` (the numpy oracle on the host cores, bounded sample, N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "2d-gp_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "posterior grid points/sec (fit+predict), N_train=4096, div-free 2D kernel"
+FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 matrix (= vector) dense peak; measured 76.5 (tools/microbench)
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--ntrain", type=int, default=4096)
+    ap.add_argument("--grid", type=int, default=256)
+    ap.add_argument("--kind", default="df")
+    ap.add_argument("--chunk", type=int, default=8192)
+    ap.add_argument("--fit-mode", default="bcast", choices=["bcast", "replicate"])
+    ap.add_argument("--cpu-baseline", type=int, default=1)
+    ap.add_argument("--cpu-sample-points", type=int, default=2048)
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"))
+    return ap.parse_args()
+
+
+def setup_dist(args):
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    if ws > 1:
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        return ws, dist.get_rank(), torch.device("cuda", local)
+    return 1, 0, torch.device("cuda", 0)
+
+
+def barrier(ws):
+    if ws > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def cpu_baseline(x, y, xg, kind, l, noise, sample_pts):
+    """Oracle (numpy/OpenBLAS) on the host: full fit + a bounded sample of grid points,
+    extrapolated linearly to the whole grid."""
+    from oracle import gp2d_oracle as O
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        cores = os.cpu_count()
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp:
+        cores = min(cores, int(omp))
+    t0 = time.perf_counter()
+    fit = O.OracleFit(x, y, kind, l, l, 1.0, noise, method="chol")
+    t1 = time.perf_counter()
+    fit.predict(xg[:sample_pts], chunk=sample_pts)
+    t2 = time.perf_counter()
+    M = xg.shape[0]
+    total = (t1 - t0) + (t2 - t1) * (M / sample_pts)
+    return {"value": M / total, "unit": "points/s", "cores": cores, "kind": "port",
+            "sample": f"numpy oracle: full fit N_train={x.shape[0]} ({t1 - t0:.2f} s) + {sample_pts} of {M} "
+                      f"grid points ({t2 - t1:.2f} s), predict extrapolated linearly; OpenBLAS threads={cores}"}
+
+
+def main():
+    args = parse()
+    ws, rank, dev = setup_dist(args)
+    from gp2d import data as D
+    from gp2d import distributed as GD
+    from gp2d import engine as E
+
+    G = args.grid
+    x1, x2, u, v = D.synthetic_tracks(args.ntrain, seed=2016)
+    x = np.stack([x1, x2], 1)
+    y = np.concatenate([u, v])
+    _, _, xg_all = D.bbox_grid(x1, x2, G, pad=5.0, Gy=G * ws)
+    m_all = xg_all.shape[0]
+    lo, hi = D.shard_range(m_all, ws, rank)
+    spec = E.KernelSpec(kind=args.kind, l_df=5.0, l_cf=5.0, ratio=1.0 if args.kind == "df" else 0.5)
+    noise = 0.0025
+    # inputs resident in HBM before the timed region
+    xt = torch.tensor(x, device=dev)
+    yt = torch.tensor(y, device=dev)
+    xg = torch.tensor(xg_all[lo:hi], device=dev)
+    m = hi - lo
+    mean = torch.empty(2 * m, dtype=torch.float64, device=dev)
+    var = torch.empty(2 * m, dtype=torch.float64, device=dev)
+    pred_cache = {}
+
+    def step():
+        gp = GD.fit_sharded(spec, xt, yt, noise, dev, mode=args.fit_mode)
+        pr = pred_cache.get("p")
+        if pr is None or pr.gp.n != gp.n:
+            pr = E.Predictor(gp, args.chunk)
+            pred_cache["p"] = pr
+        pr.gp = gp
+        pr(xg, out=(mean, var))
+        return gp
+
+    for _ in range(args.warmup):
+        step()
+    barrier(ws)
+    E.timing_enable(True)
+    E.timing_read()
+    barrier(ws)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier(ws)
+    t1 = time.perf_counter()
+    kms, klaunch, kflops = E.timing_read()
+    E.timing_enable(False)
+    dt = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if ws > 1:
+        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    elapsed = float(dt.item())
+    ms_per_step = 1e3 * elapsed / args.steps
+    value = m_all * args.steps / elapsed
+
+    # mean-only throughput (secondary, same fit)
+    barrier(ws)
+    t2 = time.perf_counter()
+    for _ in range(args.steps):
+        gp = GD.fit_sharded(spec, xt, yt, noise, dev, mode=args.fit_mode)
+        pred_cache["p"].gp = gp
+        pred_cache["p"](xg, compute_var=False, out=(mean, var))
+    barrier(ws)
+    t3 = time.perf_counter()
+    mean_only = m_all * args.steps / (t3 - t2)
+
+    if rank != 0:
+        if ws > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    achieved = kflops / (kms * 1e-3) / 1e12 if kms > 0 else None
+    traffic = None
+    try:
+        with open(args.pmc_json) as f:
+            pmc = json.load(f)
+        traffic = pmc.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "points/s",
+        "n_gpus": ws,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded drifter field, SURVEY.md §8d)",
+        "config": {"workload": f"{args.kind} kernel, N_train={args.ntrain}, {G}x{G} grid per GPU, fit+predict "
+                               f"(mean+variance)", "n_train": args.ntrain, "grid_per_gpu": f"{G}x{G}",
+                   "points_total": m_all, "length_scale_km": 5.0, "noise": noise,
+                   "parallelism": f"grid-sharded x{ws}, factor {args.fit_mode}" + (" (RCCL)" if ws > 1 else "")},
+        "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": (achieved / FP64_PEAK_TFLOPS) if achieved else None, "traffic": traffic,
+                     "kernel": "gemm_f64_kernel<NN,COLSQ> (variance ‖L⁻¹k*‖²)",
+                     "launches": klaunch, "avg_launch_ms": (kms / klaunch) if klaunch else None,
+                     "flops_per_launch": (kflops / klaunch) if klaunch else None},
+        "mean_only_value": mean_only,
+    }
+    if args.cpu_baseline and ws == 1:
+        out["cpu_baseline"] = cpu_baseline(x, y, xg_all, args.kind, 5.0, noise, args.cpu_sample_points)
+    print(json.dumps(out), flush=True)
+    if ws > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
