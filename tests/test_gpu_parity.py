@@ -76,3 +76,72 @@ def test_golden_mykernel_N1024(golden):
     mu, var = E.predict(gp, g["xg"])
     assert rel(mu.cpu().numpy(), g["mean"]) < 1e-10
     assert rel(var.cpu().numpy(), g["var"]) < 1e-10
+
+
+def _spd(n, seed):
+    rng = np.random.default_rng(seed)
+    A = rng.normal(size=(n, n))
+    return A @ A.T / n + np.eye(n) * 0.5
+
+
+@pytest.mark.parametrize("n", [128, 384, 1024])
+def test_potrf_trtri_potrs_abi(n):
+    """gp2d_potrf / gp2d_trtri / gp2d_potrs_inv vs LAPACK on a random SPD matrix."""
+    import ctypes
+    from gp2d import _native as N
+    L_ = N.lib()
+    K = _spd(n, n)
+    A = torch.tensor(K, device="cuda")
+    dinv = torch.empty((n // 128, 128, 128), dtype=torch.float64, device="cuda")
+    info = torch.zeros(1, dtype=torch.int32, device="cuda")
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    N.check(L_.gp2d_potrf(P(A), n, n, P(dinv), P(info), None, 0, s), "potrf")
+    assert int(info.item()) == 0
+    Lref = np.linalg.cholesky(K)
+    Lg = A.cpu().numpy()
+    assert np.array_equal(np.triu(Lg, 1), np.zeros_like(Lg))
+    assert rel(Lg, Lref) < 1e-13
+    wb = int(L_.gp2d_trtri_workspace(n))
+    work = torch.empty(wb // 8 + 1, dtype=torch.float64, device="cuda")
+    N.check(L_.gp2d_trtri(P(A), n, n, P(dinv), P(work), wb, s), "trtri")
+    W = A.cpu().numpy()
+    assert rel(W, np.linalg.inv(Lref)) < 1e-12
+    y = np.random.default_rng(1).normal(size=n)
+    yt = torch.tensor(y, device="cuda")
+    al = torch.empty(n, dtype=torch.float64, device="cuda")
+    pb = int(L_.gp2d_potrs_workspace(n))
+    pw = torch.empty(pb // 8 + 1, dtype=torch.float64, device="cuda")
+    N.check(L_.gp2d_potrs_inv(P(A), n, n, P(yt), P(al), P(pw), pb, s), "potrs")
+    assert rel(al.cpu().numpy(), np.linalg.solve(K, y)) < 1e-11
+    # trtri without the diagonal inverses (stand-alone path)
+    A2 = torch.tensor(Lref, device="cuda")
+    N.check(L_.gp2d_trtri(P(A2), n, n, None, P(work), wb, s), "trtri(no dinv)")
+    assert rel(A2.cpu().numpy(), np.linalg.inv(Lref)) < 1e-12
+
+
+def test_not_positive_definite_raises():
+    """Non-SPD K_y → LAPACK-style info → numpy.linalg.LinAlgError (np.linalg.inv / sklearn paths)."""
+    x = np.zeros((3, 2))  # three identical points, no noise: singular K
+    with pytest.raises(np.linalg.LinAlgError):
+        E.fit(E.KernelSpec(kind="df", l_df=1.0), x, np.zeros(6), noise=-1e-3)
+
+
+def test_sharded_predict_bit_identical():
+    """Grid shards (any split) concatenate to the single-launch result bit-for-bit."""
+    from gp2d import data as D
+    x, y = tracks(300, seed=3)
+    rng = np.random.default_rng(4)
+    xg = np.stack([rng.uniform(-5, 65, 5000), rng.uniform(-5, 50, 5000)], 1)
+    gp = E.fit(E.KernelSpec(kind="mixed", l_df=5.0, l_cf=3.0, ratio=0.4), x, y, noise=0.0025)
+    m_all, v_all = (t.cpu().numpy() for t in E.predict(gp, xg, chunk=1024))
+    for ws in (2, 3, 8):
+        shards_m, shards_v = [], []
+        for r in range(ws):
+            lo, hi = D.shard_range(xg.shape[0], ws, r)
+            mm, vv = E.predict(gp, xg[lo:hi], chunk=512)
+            shards_m.append((lo, hi, mm.cpu().numpy()))
+            shards_v.append((lo, hi, vv.cpu().numpy()))
+        from gp2d.distributed import assemble_from_shards
+        assert np.array_equal(assemble_from_shards(xg.shape[0], 2, shards_m), m_all)
+        assert np.array_equal(assemble_from_shards(xg.shape[0], 2, shards_v), v_all)
