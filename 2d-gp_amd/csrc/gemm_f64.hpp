@@ -43,6 +43,7 @@ struct GemmParams {
   int b_lower;   // (NN) B lower-triangular: column block j0 only needs k >= j0
   int c_lower;   // enumerate lower tiles of a square C; diagonal tiles store i >= j
   int rev_rows;  // dispatch heavy (large i0) row blocks first (a_lower)
+  int xcd_cols;  // 1-D grid: groups of 8 column tiles × all row blocks, column tile = XCD label
   double* P; int64_t ldp; int64_t sP;         // EPI_COLSQ partials [M/BM][N]
 };
 
@@ -61,6 +62,17 @@ __global__ __launch_bounds__(256, 2) void gemm_f64_kernel(GemmParams p) {
   int bi, bj;
   if (p.c_lower) {
     tri_tile(blockIdx.x, bi, bj);
+  } else if (p.xcd_cols) {
+    // Blocks b and b+8 share an XCD (round-robin dispatch).  Give every XCD one column
+    // tile of the current group of 8 and all row blocks: the K*ᵀ column panel slabs are
+    // then re-read from that XCD's L2 by all row blocks in step, and each W row panel is
+    // read by 8 concurrent workgroups (one per XCD) through the Infinity Cache.
+    const int nr = p.M / GBM;
+    const int t = blockIdx.x;
+    const int x = t & 7, q = t >> 3;
+    const int g = q / nr, r = q - g * nr;
+    bj = g * 8 + x;
+    bi = nr - 1 - r;  // heavy (long-K) row blocks first
   } else {
     bj = blockIdx.x;
     bi = p.rev_rows ? (int)(gridDim.y - 1 - blockIdx.y) : (int)blockIdx.y;
@@ -205,6 +217,12 @@ inline int launch_gemm(const GemmParams& p, int batch, hipStream_t s) {
   if (p.c_lower) {
     const int t = p.M / GBM;
     grid = dim3(t * (t + 1) / 2, 1, batch);
+  } else if (p.xcd_cols) {
+    if ((p.N / GBN) % 8) {
+      set_error("gemm: xcd_cols needs a multiple of 8 column tiles");
+      return -2;
+    }
+    grid = dim3((p.N / GBN) * (p.M / GBM), 1, batch);
   } else {
     grid = dim3(p.N / GBN, p.M / GBM, batch);
   }

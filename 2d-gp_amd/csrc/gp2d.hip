@@ -263,6 +263,7 @@ int gp2d_predict(const double* W, int64_t n, int64_t ldw, const double* alpha, c
       p.B = Bm; p.ldb = ncols;
       p.M = (int)n; p.N = (int)ncols; p.K = (int)n;
       p.a_lower = 1; p.rev_rows = 1;
+      p.xcd_cols = 0;  // XCD-grouped order measured 4% slower (64.9 vs 67.6 TF/s); kept for study
       p.P = P; p.ldp = ncols;
       hipEvent_t e0 = nullptr, e1 = nullptr;
       {
