@@ -8,9 +8,11 @@
 #include "gemm_f64.hpp"
 #include "factor.hpp"
 #include "predict.hpp"
+#include "ozaki.hpp"
 #include "../../include/gp2d.h"
 
 #include <algorithm>
+#include <cmath>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -73,6 +75,68 @@ static int assemble_impl(const double* xa, int64_t na, int64_t na_pad, const dou
                                              symmetric, out, ld);
   }
   return check_launch("assemble");
+}
+
+// ------------------------------------------------------------- Ozaki constants
+static const int kModuli[OZ_MAXMOD] = {256, 255, 253, 251, 247, 241, 239, 233,
+                                       229, 227, 223, 217, 211, 199, 197, 193};
+
+static int ozaki_nmod_for(int64_t n) {
+  // need Π m_l > n · 2^{2p} (|Pint| ≤ n·2^p·2^{p−1}) with one guard bit
+  const double need = std::log2((double)n) + 2.0 * OZ_P + 1.0;
+  double bits = 0.0;
+  for (int l = 0; l < OZ_MAXMOD; ++l) {
+    bits += std::log2((double)kModuli[l]);
+    if (bits > need) return l + 1;
+  }
+  return -1;
+}
+
+static int64_t modinv(int64_t a, int64_t m) {  // a⁻¹ mod m (a, m coprime)
+  int64_t t = 0, nt = 1, r = m, nr = ((a % m) + m) % m;
+  while (nr) {
+    const int64_t q = r / nr;
+    int64_t tmp = t - q * nt; t = nt; nt = tmp;
+    tmp = r - q * nr; r = nr; nr = tmp;
+  }
+  return (t % m + m) % m;
+}
+
+static double kstar_bound(const gp2d_kernel_t* k) {
+  // |K*| entries: div-free and curl-free parts are each bounded by 1/ℓ² (see ozaki.hpp)
+  switch (k->kind) {
+    case GP2D_KIND_SCALAR: return 1.0;
+    case GP2D_KIND_DIVFREE: return 1.0 / (k->l_df * k->l_df);
+    case GP2D_KIND_CURLFREE: return 1.0 / (k->l_cf * k->l_cf);
+    default: return std::max(1.0 / (k->l_df * k->l_df), 1.0 / (k->l_cf * k->l_cf));
+  }
+}
+
+static int make_ozaki_consts(int64_t n, const gp2d_kernel_t* k, OzakiConsts& oc) {
+  oc.nmod = ozaki_nmod_for(n);
+  GP2D_REQUIRE(oc.nmod > 0, "ozaki: matrix order too large for the modulus table");
+  double M = 1.0;
+  for (int l = 0; l < oc.nmod; ++l) M *= (double)kModuli[l];
+  oc.M = M;
+  for (int l = 0; l < OZ_MAXMOD; ++l) {
+    oc.m[l] = kModuli[l];
+    oc.inv_m[l] = 1.0 / (double)kModuli[l];
+    oc.h[l] = oc.t[l] = 0.0;
+  }
+  for (int l = 0; l < oc.nmod; ++l) {
+    const int64_t ml = kModuli[l];
+    int64_t Ml = 1;  // (M / m_l) mod m_l
+    for (int q = 0; q < oc.nmod; ++q)
+      if (q != l) Ml = (Ml * (kModuli[q] % ml)) % ml;
+    const int64_t inv = modinv(Ml, ml);
+    const double x = (double)inv / (double)ml;
+    const double h = std::ldexp(std::rint(std::ldexp(x, OZ_HBITS)), -OZ_HBITS);
+    oc.h[l] = h;
+    oc.t[l] = ((double)inv - h * (double)ml) / (double)ml;  // h·m_l is exact (≤ 41 bits)
+  }
+  const double bmax = kstar_bound(k);
+  oc.sB = OZ_P - 1 - (int)std::ceil(std::log2(bmax));
+  return 0;
 }
 
 }  // namespace gp2d
@@ -278,6 +342,100 @@ int gp2d_predict(const double* W, int64_t n, int64_t ldw, const double* alpha, c
         const double nv = (double)bd * (double)ntr;  // algorithmic order (valid points)
         g_timing.flops.push_back((double)bd * (double)cv * nv * nv);  // 2·(2N)² per point (vector2d)
       }
+    }
+    predict_finalize_kernel<<<(unsigned)((ncols + 255) / 256), 256, 0, s>>>(
+        pm, nmseg, P, npseg, ncols, cp, cv, c0, m, kss, add, clip, compute_var, mean, var);
+    GP2D_CHECK(check_launch("predict_finalize_kernel"));
+  }
+  return 0;
+}
+
+// ------------------------------------------------------------ PREDICT (Ozaki-II)
+int gp2d_ozaki_nmod(int64_t n) { return ozaki_nmod_for(n); }
+
+size_t gp2d_ozaki_wres_bytes(int64_t n) {
+  const int nm = ozaki_nmod_for(n);
+  return nm > 0 ? (size_t)nm * (size_t)n * (size_t)n : 0;
+}
+
+int gp2d_ozaki_prepare(const double* W, int64_t n, int64_t ldw, const gp2d_kernel_t* k, int8_t* wres,
+                       double* rowscale, void* stream) {
+  GP2D_CHECK(validate_kernel(k));
+  GP2D_REQUIRE(k->family == GP2D_FAMILY_VECTOR2D, "ozaki: vector2d family only");
+  GP2D_REQUIRE(n % IBM == 0 && n > 0, "ozaki: n must be a positive multiple of 256");
+  OzakiConsts oc;
+  GP2D_CHECK(make_ozaki_consts(n, k, oc));
+  ozaki_w_prep_kernel<<<(unsigned)n, 256, 0, S(stream)>>>(W, n, ldw, oc, wres, rowscale);
+  return check_launch("ozaki_w_prep_kernel");
+}
+
+size_t gp2d_predict_ozaki_workspace(int64_t n, int64_t chunk) {
+  const int nm = ozaki_nmod_for(n);
+  if (nm <= 0) return 0;
+  const int64_t cp = round_up(chunk < 1 ? 1 : chunk, IBN / 2);
+  const int64_t ncols = 2 * cp;
+  return 2 * (size_t)nm * (size_t)n * (size_t)ncols                        // Bres + Cres planes
+         + sizeof(double) * ((size_t)(n / 2 / OZ_KS_T + 1) + (size_t)(n / OZ_CRT_ROWS + 1)) * ncols;
+}
+
+int gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int64_t n, const double* alpha, const double* xtr,
+                       int64_t ntr, int64_t ntr_pad, const double* xg, int64_t m, const gp2d_kernel_t* k,
+                       int var_mode, double noise, int compute_var, double* mean, double* var, int64_t chunk,
+                       void* work, size_t work_bytes, void* stream) {
+  GP2D_CHECK(validate_kernel(k));
+  GP2D_REQUIRE(k->family == GP2D_FAMILY_VECTOR2D, "ozaki: vector2d family only");
+  GP2D_REQUIRE(n == 2 * ntr_pad && n % IBM == 0, "ozaki: n must equal 2·ntr_pad and be a multiple of 256");
+  GP2D_REQUIRE(chunk > 0 && chunk % (IBN / 2) == 0, "ozaki: chunk must be a positive multiple of 128");
+  GP2D_REQUIRE(work != nullptr && work_bytes >= gp2d_predict_ozaki_workspace(n, chunk), "ozaki: workspace too small");
+  GP2D_REQUIRE(var_mode >= 0 && var_mode <= 2, "predict: bad var_mode");
+  if (m <= 0) return 0;
+  hipStream_t s = S(stream);
+  OzakiConsts oc;
+  GP2D_CHECK(make_ozaki_consts(n, k, oc));
+  const int nm = oc.nmod;
+  const int64_t ncols_max = 2 * chunk;
+  int8_t* bres = reinterpret_cast<int8_t*>(work);
+  uint8_t* cres = reinterpret_cast<uint8_t*>(bres + (size_t)nm * n * ncols_max);
+  double* pm = reinterpret_cast<double*>(cres + (size_t)nm * n * ncols_max);
+  const int64_t nmseg = (ntr_pad + OZ_KS_T - 1) / OZ_KS_T;
+  double* P = pm + (size_t)(n / 2 / OZ_KS_T + 1) * ncols_max;
+  const int64_t npseg = (n + OZ_CRT_ROWS - 1) / OZ_CRT_ROWS;
+  const double kss = gp2d_kernel_diag(k);
+  const double add = (var_mode == GP2D_VAR_LATENT) ? 0.0 : noise;
+  const int clip = (var_mode == GP2D_VAR_CLIPPED);
+  const VecParams vp = make_vec_params(k);
+  for (int64_t c0 = 0; c0 < m; c0 += chunk) {
+    const int64_t cv = std::min<int64_t>(chunk, m - c0);
+    const int64_t cp = round_up(cv, IBN / 2);
+    const int64_t ncols = 2 * cp;
+    ozaki_kstar_kernel<<<dim3((unsigned)nmseg, (unsigned)(cp / OZ_KS_P)), 256, 0, s>>>(
+        xtr, ntr, ntr_pad, xg + 2 * c0, cv, cp, vp, alpha, oc, bres, pm);
+    GP2D_CHECK(check_launch("ozaki_kstar_kernel"));
+    if (compute_var) {
+      hipEvent_t e0 = nullptr, e1 = nullptr;
+      {
+        std::lock_guard<std::mutex> lk(g_timing.mu);
+        if (g_timing.on) { e0 = g_timing.get(); e1 = g_timing.get(); hipEventRecord(e0, s); }
+      }
+      const int nr = (int)(n / IBM), nc = (int)(ncols / IBN);
+      const bool xg8 = (nr % 4 == 0) && (nc % 8 == 0) && (((nr / 4) * (nc / 8)) % 8 == 0);
+      const dim3 ggrid = xg8 ? dim3((unsigned)(nr * nc)) : dim3((unsigned)nc, (unsigned)nr);
+      for (int l = 0; l < nm; ++l) {
+        igemm_nt_mod_kernel<<<ggrid, 256, 0, s>>>(
+            wres + (size_t)l * n * n, n, bres + (size_t)l * ncols * n, n, cres + (size_t)l * n * ncols, n,
+            (int)n, (int)ncols, (int)n, 1, oc.m[l], oc.inv_m[l], xg8 ? 1 : 0);
+        GP2D_CHECK(check_launch("igemm_nt_mod_kernel"));
+      }
+      if (e0) {
+        std::lock_guard<std::mutex> lk(g_timing.mu);
+        hipEventRecord(e1, s);
+        g_timing.ev.push_back({e0, e1});
+        const double nv = 2.0 * (double)ntr;
+        g_timing.flops.push_back(2.0 * (double)cv * nv * nv);  // FP64-equivalent algorithmic flop
+      }
+      ozaki_crt_colsq_kernel<<<dim3((unsigned)((ncols + 3) / 4), (unsigned)npseg), 256, 0, s>>>(
+          cres, n, ncols, oc, rowscale, P);
+      GP2D_CHECK(check_launch("ozaki_crt_colsq_kernel"));
     }
     predict_finalize_kernel<<<(unsigned)((ncols + 255) / 256), 256, 0, s>>>(
         pm, nmseg, P, npseg, ncols, cp, cv, c0, m, kss, add, clip, compute_var, mean, var);

@@ -1,0 +1,401 @@
+// ozaki.hpp — FP64-accurate variance contraction on the INT8 matrix cores
+// (Ozaki scheme II: error-free integer splitting + Chinese-remainder reconstruction).
+//
+// The variance needs q_j = Σ_i V_ij² with V = W·K*ᵀ (W = L⁻¹, lower-triangular).  On
+// MI355X the FP64 MFMA peak is 78.6 TF while v_mfma_i32_32x32x32_i8 runs at 4.7 POPS
+// (measured, tools/microbench/i8_mfma.hip), so the product is computed exactly in
+// integers instead:
+//   1. scale: Wint = rint(W_ik·2^{s_i}) (per-row power of two, |Wint| < 2^p) and
+//      Bint = rint(K*_jk·2^{s_B}) (one power of two from the analytic bound |K*| ≤ kss);
+//      both are exact integers held in fp64 (p = 42 < 53);
+//   2. residues: for L pairwise-coprime moduli m_l ≤ 256 (Π m_l > n·2^{2p}), the
+//      centred residues of Wint / Bint fit int8; P_l = Wres_l · Bres_lᵀ is exact in
+//      int32 (|P_l| ≤ n·128²) and reduced mod m_l in the GEMM epilogue (uint8 planes);
+//   3. CRT: Pint/M = frac(Σ_l c_l·inv_l/m_l), evaluated with an exact high part
+//      (inv_l/m_l rounded to 2^-33, products and sums exact in fp64) plus an fp64 low
+//      part, so V_ij = (Pint/M)·M·2^{-s_i-s_B} carries ~2^-50 relative error before the
+//      2^-p scaling error; the squares are summed per column in a fixed order.
+// Parity is gated by the same 1e-10 tests as the FP64 path (tests/test_gpu_ozaki.py).
+#pragma once
+#include "common.hpp"
+#include "assemble.hpp"
+
+namespace gp2d {
+
+constexpr int OZ_MAXMOD = 16;
+constexpr int OZ_P = 42;           // integer bits of the scaled operands
+constexpr int OZ_HBITS = 33;       // exact high part of inv_l / m_l
+
+struct OzakiConsts {
+  int nmod;
+  int m[OZ_MAXMOD];
+  double inv_m[OZ_MAXMOD];         // 1 / m_l
+  double h[OZ_MAXMOD];             // inv_l / m_l rounded to a multiple of 2^-33
+  double t[OZ_MAXMOD];             // inv_l / m_l − h_l
+  double M;                        // Π m_l (rounded)
+  int sB;                          // K* scale exponent
+};
+
+// residue of an exact integer x (|x| < 2^53) modulo m, centred into [−128, 127]
+__device__ __forceinline__ int centred_residue(double x, double m, double inv_m) {
+  const double q = rint(x * inv_m);
+  int r = (int)fma(-m, q, x);
+  if (r >= 128) r -= (int)m;       // only m = 256 can reach +128
+  if (r < -128) r += (int)m;
+  return r;
+}
+
+// ------------------------------------------------------------------ W preparation
+// One workgroup per row i: row max (k ≤ i) → s_i; residue planes Wres[l][i][k] (int8, full
+// row, zeros above the diagonal) and rowscale[i] = M·2^{−s_i−s_B}.
+__global__ __launch_bounds__(256) void ozaki_w_prep_kernel(const double* __restrict__ W, int64_t n, int64_t ldw,
+                                                           OzakiConsts oc, int8_t* __restrict__ wres,
+                                                           double* __restrict__ rowscale) {
+  __shared__ double red[256];
+  const int64_t i = blockIdx.x;
+  const int tid = threadIdx.x;
+  const double* w = W + i * ldw;
+  double mx = 0.0;
+  for (int64_t k = tid; k <= i; k += 256) mx = fmax(mx, fabs(w[k]));
+  red[tid] = mx;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (tid < s) red[tid] = fmax(red[tid], red[tid + s]);
+    __syncthreads();
+  }
+  mx = red[0];
+  const int e = (mx > 0.0) ? ilogb(mx) : 0;    // 2^e ≤ mx < 2^{e+1}
+  const int si = OZ_P - 1 - e;                 // |W·2^si| < 2^OZ_P
+  if (tid == 0) rowscale[i] = ldexp(oc.M, -si - oc.sB);
+  // 4 consecutive k per thread → one packed dword store per plane
+  for (int64_t k0 = (int64_t)tid * 4; k0 < n; k0 += 1024) {
+    double x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t k = k0 + u;
+      x[u] = (k <= i && k < n) ? rint(ldexp(w[k], si)) : 0.0;
+    }
+    for (int l = 0; l < oc.nmod; ++l) {
+      const double m = (double)oc.m[l];
+      uint32_t packed = 0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) packed |= (uint32_t)(uint8_t)(int8_t)centred_residue(x[u], m, oc.inv_m[l]) << (8 * u);
+      *reinterpret_cast<uint32_t*>(wres + ((int64_t)l * n + i) * n + k0) = packed;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ K*ᵀ residues + mean
+// Block: 64 lanes × 4 thread rows.  Lane tx covers training points t = 256·bx + 4tx..+3,
+// thread row ty covers grid points p = 16·by + ty + 4q (q < 4).  Writes the residue planes
+// Bres[l][j][k] (j = grid component row, k = training component column, K-contiguous)
+// and mean partials pm[bx][j] = Σ_{k in block} α_k·K*_jk (one wave = one grid point set,
+// reduced by shuffles in a fixed order).
+constexpr int OZ_KS_T = 256;   // training points per block
+constexpr int OZ_KS_P = 16;    // grid points per block
+
+__global__ __launch_bounds__(256) void ozaki_kstar_kernel(
+    const double* __restrict__ xtr, int64_t ntr, int64_t npad, const double* __restrict__ xg, int64_t cv,
+    int64_t cp, VecParams vp, const double* __restrict__ alpha, OzakiConsts oc, int8_t* __restrict__ bres,
+    double* __restrict__ pm) {
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int64_t t0 = (int64_t)blockIdx.x * OZ_KS_T + 4 * tx;
+  const int64_t n = 2 * npad, ncols = 2 * cp;
+  double a1[4], a2[4], x1[4], x2[4];
+  bool tv[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int64_t t = t0 + u;
+    tv[u] = t < ntr;
+    x1[u] = tv[u] ? xtr[2 * t] : 0.0;
+    x2[u] = tv[u] ? xtr[2 * t + 1] : 0.0;
+    a1[u] = (t < npad) ? alpha[t] : 0.0;
+    a2[u] = (t < npad) ? alpha[npad + t] : 0.0;
+  }
+  const double scale = ldexp(1.0, oc.sB);
+#pragma unroll 1
+  for (int q = 0; q < OZ_KS_P / 4; ++q) {
+    const int64_t p = (int64_t)blockIdx.y * OZ_KS_P + ty + 4 * q;
+    const bool pv = p < cv;
+    const double g1 = pv ? xg[2 * p] : 0.0, g2 = pv ? xg[2 * p + 1] : 0.0;
+    double k11[4], k12[4], k22[4];
+    double mu = 0.0, mv = 0.0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (pv && tv[u]) {
+        vec_block(vp, x1[u] - g1, x2[u] - g2, k11[u], k12[u], k22[u]);
+      } else {
+        k11[u] = k12[u] = k22[u] = 0.0;
+      }
+      mu += a1[u] * k11[u] + a2[u] * k12[u];   // row j = p      (u component of the grid point)
+      mv += a1[u] * k12[u] + a2[u] * k22[u];   // row j = cp + p (v component)
+    }
+    // fixed-order wave reduction of the mean partials (64 lanes = this block's 256 points)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      mu += __shfl_xor(mu, o);
+      mv += __shfl_xor(mv, o);
+    }
+    if (tx == 0 && p < cp) {
+      pm[(int64_t)blockIdx.x * ncols + p] = mu;
+      pm[(int64_t)blockIdx.x * ncols + cp + p] = mv;
+    }
+    if (p >= cp) continue;
+    double xi[4][4];  // [entry: (u,u) (u,v) (v,u) (v,v)][u]
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      xi[0][u] = rint(k11[u] * scale);
+      xi[1][u] = rint(k12[u] * scale);
+      xi[3][u] = rint(k22[u] * scale);
+      xi[2][u] = xi[1][u];
+    }
+    for (int l = 0; l < oc.nmod; ++l) {
+      const double m = (double)oc.m[l], im = oc.inv_m[l];
+      uint32_t pk[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) w |= (uint32_t)(uint8_t)(int8_t)centred_residue(xi[e][u], m, im) << (8 * u);
+        pk[e] = w;
+      }
+      if (t0 >= npad) continue;  // npad is a multiple of 64, so a 4-point group is all in or all out
+      int8_t* plane = bres + (int64_t)l * ncols * n;
+      // (grid comp, train comp): (u,u) → row p, col t ; (u,v) → row p, col npad+t ;
+      //                          (v,u) → row cp+p, col t ; (v,v) → row cp+p, col npad+t
+      *reinterpret_cast<uint32_t*>(plane + p * n + t0) = pk[0];
+      *reinterpret_cast<uint32_t*>(plane + p * n + npad + t0) = pk[1];
+      *reinterpret_cast<uint32_t*>(plane + (cp + p) * n + t0) = pk[2];
+      *reinterpret_cast<uint32_t*>(plane + (cp + p) * n + npad + t0) = pk[3];
+    }
+  }
+}
+
+// ------------------------------------------------------------------ INT8 NT GEMM mod m
+// C[i][j] = (Σ_k A[i][k]·B[j][k]) mod m, A lower-triangular (row block i0 needs k < i0+256).
+// 256×256 output tile per 256-thread workgroup: 4 waves as 2×2, each wave 128×128 =
+// 4×4 tiles of v_mfma_i32_32x32x32_i8 (256 int32 accumulators per lane in AGPRs, one
+// wave per SIMD).  K advances in 64-byte slabs loaded global→LDS directly
+// (global_load_lds_dwordx4) into a 4-stage ring with three slabs in flight: the per-CU
+// L2/MALL stream (~77 GB/s per CU at the int8 peak) needs ~100 KB outstanding to cover its
+// latency (MI355X_MICROARCH.md, gather / LDS-DMA rows).  Per slab, two 32-deep MFMA steps;
+// the barrier that publishes slab s+1 sits between them, so the fragment reads of the next
+// step always run under 16 MFMAs (512 cycles).  LDS rows are 64 B, unpadded (the DMA writes
+// lane-linear); the 16-B chunk index is XOR-swizzled with (row>>2)&3 on the global source
+// and on the fragment read, which puts every ds_read_b128 lane group on 16 bank slots.
+constexpr int IBM = 256, IBN = 256, IBK = 64;
+constexpr int I_OP = IBM * IBK;        // bytes per operand per stage (16 KB)
+constexpr int I_STAGE = 2 * I_OP;      // A then B
+constexpr int I_NSTAGE = 4;
+
+typedef int i4v __attribute__((ext_vector_type(4)));
+typedef int i16v __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+__device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 2) & 3); }
+
+#define GP2D_VMWAIT_BARRIER(N) asm volatile("s_waitcnt vmcnt(" #N ")\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
+
+__global__ __launch_bounds__(256, 1) void igemm_nt_mod_kernel(const int8_t* __restrict__ A, int64_t lda,
+                                                              const int8_t* __restrict__ B, int64_t ldb,
+                                                              uint8_t* __restrict__ C, int64_t ldc, int M, int N,
+                                                              int K, int a_lower, int modulus, double inv_mod,
+                                                              int xcd_groups) {
+  __shared__ __attribute__((aligned(16))) int8_t smem[I_NSTAGE * I_STAGE];
+  int bi, bj;
+  if (xcd_groups) {
+    // Blocks t and t+8 share an XCD.  Each XCD runs groups of 32 workgroups = 4 row blocks ×
+    // 8 column tiles, so one K-slab of 4 A panels + 8 B panels serves all 32 tiles.
+    const int nr = M / IBM, nc = N / IBN, ncg = nc / 8;
+    const int t = blockIdx.x, x = t & 7, q = t >> 3;
+    const int G = q >> 5, w = q & 31;
+    const int P = G * 8 + x;
+    const int rg = P / ncg, cg = P - rg * ncg;
+    bi = nr - 1 - (4 * rg + (w >> 3));   // heavy (long-K) row groups first
+    bj = 8 * cg + (w & 7);
+  } else {
+    bj = blockIdx.x;
+    bi = (int)(gridDim.y - 1 - blockIdx.y);   // heavy (long-K) row blocks first
+  }
+  const int i0 = bi * IBM, j0 = bj * IBN;
+  const int ke = a_lower ? min(K, i0 + IBM) : K;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int lr = lane & 31, lh = lane >> 5;
+
+  i16v acc[4][4];
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = i16v{0};
+
+  // DMA mapping: wave wid fills rows [64·wid, 64·wid+64) of both operands, 16 rows per
+  // instruction (4 per operand per slab); lane l lands at row +l/4, physical chunk l%4.
+  const int drow = lane >> 2, dchunk = lane & 3;
+  auto issue = [&](int k0, int st) {
+#ifdef GP2D_IGEMM_NO_DMA
+    return;
+#endif
+    int8_t* As = smem + st * I_STAGE;
+    int8_t* Bs = As + I_OP;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const int row = wid * 64 + h * 16 + drow;
+      const int c = swz(row, dchunk);
+      __builtin_amdgcn_global_load_lds((const void*)(A + (int64_t)(i0 + row) * lda + k0 + 16 * c),
+                                       (lds_ptr_t)(As + (wid * 64 + h * 16) * IBK), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(B + (int64_t)(j0 + row) * ldb + k0 + 16 * c),
+                                       (lds_ptr_t)(Bs + (wid * 64 + h * 16) * IBK), 16, 0, 0);
+    }
+  };
+  // Fragment reads are inline-asm ds_read_b128 so that the waits are ours (counted
+  // lgkmcnt) rather than the compiler's conservative lgkmcnt(0) at the loop header; every
+  // wait is followed by sched_barrier(0) so no MFMA is hoisted above it.
+  const uint32_t lds_base = (uint32_t)(size_t)(lds_ptr_t)smem;
+  auto readf = [&](int st, int kc, i4v (&a)[4], i4v (&b)[4]) {
+    const uint32_t As = lds_base + st * I_STAGE;
+    const uint32_t Bs = As + I_OP;
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+      const int row = wr * 128 + mi * 32 + lr;
+      const uint32_t ad = As + row * IBK + 16 * swz(row, 2 * kc + lh);
+      asm volatile("ds_read_b128 %0, %1" : "=v"(a[mi]) : "v"(ad) : "memory");
+    }
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int row = wc * 128 + ni * 32 + lr;
+      const uint32_t ad = Bs + row * IBK + 16 * swz(row, 2 * kc + lh);
+      asm volatile("ds_read_b128 %0, %1" : "=v"(b[ni]) : "v"(ad) : "memory");
+    }
+  };
+  auto mfmas = [&](const i4v (&a)[4], const i4v (&b)[4]) {
+#ifdef GP2D_IGEMM_NO_MFMA
+    acc[0][0][0] += a[0][0] ^ b[0][0];
+    return;
+#endif
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni)
+        acc[mi][ni] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
+  };
+  const int nsl = ke / IBK;   // ke is a multiple of 256
+  if (nsl > 0) {
+    // prologue: slabs 0..2 in flight, retire slab 0
+    issue(0, 0);
+    if (nsl > 1) issue(IBK, 1);
+    if (nsl > 2) issue(2 * IBK, 2);
+    if (nsl > 2) GP2D_VMWAIT_BARRIER(16);
+    else if (nsl > 1) GP2D_VMWAIT_BARRIER(8);
+    else GP2D_VMWAIT_BARRIER(0);
+    i4v a0[4], b0[4], a1[4], b1[4];
+    readf(0, 0, a0, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    int st = 0;
+    for (int s = 0; s < nsl; ++s) {
+      int st3 = st + 3;
+      if (st3 >= I_NSTAGE) st3 -= I_NSTAGE;
+      if (s + 3 < nsl) issue((s + 3) * IBK, st3);   // buffer of slab s−1: free since the last barrier
+      readf(st, 1, a1, b1);
+      asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");  // a0, b0 (the older 8 reads) have landed
+      __builtin_amdgcn_sched_barrier(0);
+      mfmas(a0, b0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (s + 1 < nsl) {
+        // publish slab s+1: this wave's DMAs for it are done (later slabs may stay in flight)
+        if (s + 3 < nsl) GP2D_VMWAIT_BARRIER(16);
+        else if (s + 2 < nsl) GP2D_VMWAIT_BARRIER(8);
+        else GP2D_VMWAIT_BARRIER(0);
+        int st1 = st + 1;
+        if (st1 >= I_NSTAGE) st1 -= I_NSTAGE;
+        readf(st1, 0, a0, b0);
+      }
+      else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      mfmas(a1, b1);   // a1, b1 completed at the barrier's lgkmcnt(0)
+      __builtin_amdgcn_sched_barrier(0);
+      st = (st + 1 == I_NSTAGE) ? 0 : st + 1;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+  // Epilogue: residues mod m (fp32 quotient estimate, exact int correction), packed 4 rows
+  // per dword into an LDS image of Cᵀ [col][row] (pitch 272 B), then written out as
+  // coalesced 16-B row runs of the column-major residue plane (ld = ldc rows).
+  uint8_t* T = reinterpret_cast<uint8_t*>(smem);
+  constexpr int TP = IBM + 16;
+  const float fim = (float)inv_mod;
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        uint32_t pk = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int v = acc[mi][ni][4 * g + u];
+          const int q = (int)floorf((float)v * fim);     // off by at most one
+          int res = v - q * modulus;
+          res += (res < 0) ? modulus : 0;
+          res -= (res >= modulus) ? modulus : 0;
+          pk |= (uint32_t)res << (8 * u);
+        }
+        const int rloc = wr * 128 + mi * 32 + 8 * g + 4 * lh;
+        const int cloc = wc * 128 + ni * 32 + lr;
+        *reinterpret_cast<uint32_t*>(T + cloc * TP + rloc) = pk;
+      }
+  __syncthreads();
+#pragma unroll
+  for (int p = 0; p < (IBM * IBN / 16) / 256; ++p) {
+    const int id = tid + 256 * p;
+    const int cloc = id >> 4, ch = id & 15;
+    const uint4 v = *reinterpret_cast<const uint4*>(T + cloc * TP + 16 * ch);
+    *reinterpret_cast<uint4*>(C + (int64_t)(j0 + cloc) * ldc + i0 + 16 * ch) = v;
+  }
+}
+
+// ------------------------------------------------------------------ CRT + column Σ V²
+// Residue planes are column-major ([j][i], ld = n).  One wave per column j and 1024-row
+// segment: lane l reconstructs rows 16l..16l+15 (one 16-B load per plane), squares, and the
+// wave reduces in a fixed shuffle order → partial[seg][j].
+constexpr int OZ_CRT_ROWS = 1024;
+
+__global__ __launch_bounds__(256) void ozaki_crt_colsq_kernel(const uint8_t* __restrict__ cres, int64_t n,
+                                                              int64_t ncols, OzakiConsts oc,
+                                                              const double* __restrict__ rowscale,
+                                                              double* __restrict__ P) {
+  const int lane = threadIdx.x & 63;
+  const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t seg = blockIdx.y;
+  const int64_t i0 = seg * OZ_CRT_ROWS + 16 * lane;
+  if (j >= ncols) return;
+  double acc = 0.0;
+  if (i0 < n) {
+    double H[16], T[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) { H[c] = 0.0; T[c] = 0.0; }
+    const int64_t plane = n * ncols;
+    for (int l = 0; l < oc.nmod; ++l) {
+      const uint4 v = *reinterpret_cast<const uint4*>(cres + l * plane + j * n + i0);
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+      const double h = oc.h[l], t = oc.t[l];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        const double cl = (double)((w[c >> 2] >> (8 * (c & 3))) & 0xffu);
+        H[c] = fma(cl, h, H[c]);   // exact: multiples of 2^-33 below 2^12
+        T[c] = fma(cl, t, T[c]);
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      const double f = (H[c] - rint(H[c])) + T[c];   // Pint / M, centred
+      const double vij = f * rowscale[i0 + c];
+      acc = fma(vij, vij, acc);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if (lane == 0) P[seg * ncols + j] = acc;
+}
+
+}  // namespace gp2d

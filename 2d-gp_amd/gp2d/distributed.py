@@ -49,14 +49,19 @@ def broadcast_fit(gp: E.GPFit | None, spec: E.KernelSpec, noise: float, x, devic
                    device=torch.device(device))
 
 
-def fit_sharded(spec: E.KernelSpec, x, y, noise: float, device, mode: str = "bcast", jitter: float = 0.0):
+def fit_sharded(spec: E.KernelSpec, x, y, noise: float, device, mode: str = "bcast", jitter: float = 0.0,
+                variance: str = "f64"):
     """mode 'bcast': rank 0 fits, factor broadcast over RCCL; 'replicate': every rank
-    fits redundantly (no communication)."""
+    fits redundantly (no communication).  With variance='ozaki' every rank derives its
+    INT8 residue planes from the broadcast factor locally (no extra traffic)."""
     ws, rank = world()
     if ws == 1 or mode == "replicate":
-        return E.fit(spec, x, y, noise, jitter=jitter, device=device)
-    gp = E.fit(spec, x, y, noise, jitter=jitter, device=device) if rank == 0 else None
-    return broadcast_fit(gp, spec, noise, x, device)
+        return E.fit(spec, x, y, noise, jitter=jitter, device=device, variance=variance)
+    gp = E.fit(spec, x, y, noise, jitter=jitter, device=device, variance=variance) if rank == 0 else None
+    gp = broadcast_fit(gp, spec, noise, x, device)
+    if variance == "ozaki" and "ozaki" not in gp.extra:
+        E.ozaki_prepare(gp)
+    return gp
 
 
 def predict_shard(pred: E.Predictor, xg_all, var_mode: str = "latent", compute_var: bool = True, align: int = 64):

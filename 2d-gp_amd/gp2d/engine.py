@@ -144,12 +144,22 @@ def _pad_obs(y, n_train: int, n_pad: int, bd: int, device) -> torch.Tensor:
     return out
 
 
-def fit(kernel: KernelSpec, x, y, noise: float, jitter: float = 0.0, device=None) -> GPFit:
+VARIANCE_ENGINES = ("f64", "ozaki")
+
+
+def fit(kernel: KernelSpec, x, y, noise: float, jitter: float = 0.0, device=None, variance: str = "f64") -> GPFit:
     """K_y = K(x,x) + (noise+jitter)·I → L = chol(K_y) → W = L⁻¹ → α = Wᵀ W y.
 
+    variance: 'f64'   — predictive variance by the FP64-MFMA contraction;
+              'ozaki' — the same contraction emulated exactly on the INT8 matrix cores
+                        (Ozaki scheme II, csrc/ozaki.hpp); vector2d family only.
     Raises numpy.linalg.LinAlgError if K_y is not positive definite (the
     reference's np.linalg.inv / GPy jitchol / sklearn error paths).
     """
+    if variance not in VARIANCE_ENGINES:
+        raise ValueError(f"variance must be one of {VARIANCE_ENGINES}")
+    if variance == "ozaki" and kernel.family != "vector2d":
+        raise ValueError("the ozaki variance engine supports the vector2d family only")
     dev = _require_device(device)
     L = N.lib()
     d, bd = kernel.input_dim, kernel.block_dim
@@ -161,6 +171,9 @@ def fit(kernel: KernelSpec, x, y, noise: float, jitter: float = 0.0, device=None
     n = bd * npad
     if n % NB:  # scalar (ARD) family: the matrix order itself must be a multiple of 128
         npad = (npad + NB - 1) // NB * NB
+        n = bd * npad
+    if variance == "ozaki" and n % 256:  # int8 GEMM tiles are 256 wide
+        npad = (npad + 127) // 128 * 128
         n = bd * npad
     s = _stream_handle(dev)
     desc = kernel.desc()
@@ -184,7 +197,23 @@ def fit(kernel: KernelSpec, x, y, noise: float, jitter: float = 0.0, device=None
     pbytes = int(L.gp2d_potrs_workspace(n))
     pwork = torch.empty(pbytes // 8 + 1, dtype=torch.float64, device=dev)
     N.check(L.gp2d_potrs_inv(_ptr(A), n, n, _ptr(Y), _ptr(alpha), _ptr(pwork), pbytes, s), "gp2d_potrs_inv")
-    return GPFit(kernel=kernel, noise=float(noise), x=X, n_train=ntr, n_pad=npad, W=A, alpha=alpha, device=dev)
+    gp = GPFit(kernel=kernel, noise=float(noise), x=X, n_train=ntr, n_pad=npad, W=A, alpha=alpha, device=dev)
+    if variance == "ozaki":
+        ozaki_prepare(gp)
+    return gp
+
+
+def ozaki_prepare(gp: GPFit) -> GPFit:
+    """Residue planes of W for the INT8 variance engine (once per fit)."""
+    L = N.lib()
+    n = gp.n
+    wres = torch.empty(int(L.gp2d_ozaki_wres_bytes(n)), dtype=torch.int8, device=gp.device)
+    rowscale = torch.empty(n, dtype=torch.float64, device=gp.device)
+    desc = gp.kernel.desc()
+    N.check(L.gp2d_ozaki_prepare(_ptr(gp.W), n, n, ctypes.byref(desc), _ptr(wres), _ptr(rowscale),
+                                 _stream_handle(gp.device)), "gp2d_ozaki_prepare")
+    gp.extra["ozaki"] = (wres, rowscale)
+    return gp
 
 
 _VAR_MODES = {"latent": N.VAR_LATENT, "gpy": N.VAR_NOISY, "noisy": N.VAR_NOISY, "sklearn": N.VAR_CLIPPED,
@@ -197,9 +226,13 @@ class Predictor:
     def __init__(self, gp: GPFit, chunk: int = 8192):
         self.gp = gp
         bd = gp.kernel.block_dim
-        unit = 64 if bd == 2 else 128
+        self.ozaki = "ozaki" in gp.extra
+        unit = 128 if (bd == 1 or self.ozaki) else 64
         self.chunk = max(unit, (int(chunk) + unit - 1) // unit * unit)
-        self.wbytes = int(N.lib().gp2d_predict_workspace(gp.n, self.chunk, bd))
+        if self.ozaki:
+            self.wbytes = int(N.lib().gp2d_predict_ozaki_workspace(gp.n, self.chunk))
+        else:
+            self.wbytes = int(N.lib().gp2d_predict_workspace(gp.n, self.chunk, bd))
         self.work = torch.empty(self.wbytes // 8 + 1, dtype=torch.float64, device=gp.device)
 
     def __call__(self, xg, var_mode: str = "latent", compute_var: bool = True, out=None):
@@ -214,6 +247,14 @@ class Predictor:
         else:
             mean, var = out
         desc = gp.kernel.desc()
+        if self.ozaki and "ozaki" in gp.extra:
+            wres, rowscale = gp.extra["ozaki"]
+            N.check(L.gp2d_predict_ozaki(_ptr(wres), _ptr(rowscale), gp.n, _ptr(gp.alpha), _ptr(gp.x), gp.n_train,
+                                         gp.n_pad, _ptr(G), m, ctypes.byref(desc), _VAR_MODES[var_mode],
+                                         float(gp.noise), int(bool(compute_var)), _ptr(mean), _ptr(var), self.chunk,
+                                         _ptr(self.work), self.wbytes, _stream_handle(gp.device)),
+                    "gp2d_predict_ozaki")
+            return mean, (var if compute_var else None)
         N.check(L.gp2d_predict(_ptr(gp.W), gp.n, gp.n, _ptr(gp.alpha), _ptr(gp.x), gp.n_train, gp.n_pad,
                                _ptr(G), m, ctypes.byref(desc), _VAR_MODES[var_mode], float(gp.noise),
                                int(bool(compute_var)), _ptr(mean), _ptr(var), self.chunk, _ptr(self.work),

@@ -31,6 +31,7 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "posterior grid points/sec (fit+predict), N_train=4096, div-free 2D kernel"
 FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 matrix (= vector) dense peak; measured 76.5 (tools/microbench)
 HBM_PEAK_GBS = 8000.0
+INT8_PEAK_TOPS = 5000.0   # MI355X dense int8 MFMA (2x bf16 2.5 PF); measured 4.7 POPS (tools/microbench/i8_mfma.hip)
 
 
 def parse():
@@ -43,9 +44,11 @@ def parse():
     ap.add_argument("--kind", default="df")
     ap.add_argument("--chunk", type=int, default=8192)
     ap.add_argument("--fit-mode", default="bcast", choices=["bcast", "replicate"])
+    ap.add_argument("--variance", default="ozaki", choices=["ozaki", "f64"],
+                    help="variance contraction: exact INT8 Ozaki-II emulation (default) or FP64 MFMA")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-sample-points", type=int, default=2048)
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"))
+    ap.add_argument("--pmc-json", default=None)
     return ap.parse_args()
 
 
@@ -114,9 +117,9 @@ def main():
     pred_cache = {}
 
     def step():
-        gp = GD.fit_sharded(spec, xt, yt, noise, dev, mode=args.fit_mode)
+        gp = GD.fit_sharded(spec, xt, yt, noise, dev, mode=args.fit_mode, variance=args.variance)
         pr = pred_cache.get("p")
-        if pr is None or pr.gp.n != gp.n:
+        if pr is None or pr.gp.n != gp.n or pr.ozaki != ("ozaki" in gp.extra):
             pr = E.Predictor(gp, args.chunk)
             pred_cache["p"] = pr
         pr.gp = gp
@@ -147,7 +150,7 @@ def main():
     barrier(ws)
     t2 = time.perf_counter()
     for _ in range(args.steps):
-        gp = GD.fit_sharded(spec, xt, yt, noise, dev, mode=args.fit_mode)
+        gp = GD.fit_sharded(spec, xt, yt, noise, dev, mode=args.fit_mode, variance=args.variance)
         pred_cache["p"].gp = gp
         pred_cache["p"](xg, compute_var=False, out=(mean, var))
     barrier(ws)
@@ -161,9 +164,28 @@ def main():
         return
 
     achieved = kflops / (kms * 1e-3) / 1e12 if kms > 0 else None
+    if args.variance == "ozaki":
+        # dominant kernel = the nmod int8 GEMMs; executed int8 ops per launch = nmod × the
+        # FP64-equivalent algorithmic count (one exact product per modulus)
+        from gp2d import _native as NN
+        nmod = int(NN.lib().gp2d_ozaki_nmod(2 * ((args.ntrain + 127) // 128 * 128)))
+        roof = {"bound": "mfma", "achieved": achieved * nmod if achieved else None, "peak": INT8_PEAK_TOPS,
+                "unit": "TOP/s (int8)", "frac": (achieved * nmod / INT8_PEAK_TOPS) if achieved else None,
+                "traffic": traffic, "kernel": f"igemm_nt_mod_kernel x{nmod} moduli (Ozaki-II variance, exact)",
+                "launches": klaunch * nmod, "avg_launch_ms": (kms / klaunch / nmod) if klaunch else None,
+                "ops_per_launch": (kflops / klaunch) if klaunch else None,
+                "fp64_equivalent_tflops": achieved, "fp64_equivalent_frac_of_fp64_peak":
+                    (achieved / FP64_PEAK_TFLOPS) if achieved else None}
+    else:
+        roof = {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": (achieved / FP64_PEAK_TFLOPS) if achieved else None, "traffic": traffic,
+                "kernel": "gemm_f64_kernel<NN,COLSQ> (variance ‖L⁻¹k*‖²)",
+                "launches": klaunch, "avg_launch_ms": (kms / klaunch) if klaunch else None,
+                "flops_per_launch": (kflops / klaunch) if klaunch else None}
     traffic = None
+    pmc_json = args.pmc_json or os.path.join(ROOT, "profiles", f"r01_pmc_traffic_{args.variance}.json")
     try:
-        with open(args.pmc_json) as f:
+        with open(pmc_json) as f:
             pmc = json.load(f)
         traffic = pmc.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
@@ -179,17 +201,13 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f64",
+        "dtype": "f64" if args.variance == "f64" else "f64 (variance GEMM as exact int8 Ozaki-II)",
         "data": "synthetic (seeded drifter field, SURVEY.md §8d)",
         "config": {"workload": f"{args.kind} kernel, N_train={args.ntrain}, {G}x{G} grid per GPU, fit+predict "
                                f"(mean+variance)", "n_train": args.ntrain, "grid_per_gpu": f"{G}x{G}",
                    "points_total": m_all, "length_scale_km": 5.0, "noise": noise,
                    "parallelism": f"grid-sharded x{ws}, factor {args.fit_mode}" + (" (RCCL)" if ws > 1 else "")},
-        "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": (achieved / FP64_PEAK_TFLOPS) if achieved else None, "traffic": traffic,
-                     "kernel": "gemm_f64_kernel<NN,COLSQ> (variance ‖L⁻¹k*‖²)",
-                     "launches": klaunch, "avg_launch_ms": (kms / klaunch) if klaunch else None,
-                     "flops_per_launch": (kflops / klaunch) if klaunch else None},
+        "roofline": roof,
         "mean_only_value": mean_only,
     }
     if args.cpu_baseline and ws == 1:

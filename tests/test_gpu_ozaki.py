@@ -1,0 +1,75 @@
+"""INT8 (Ozaki scheme II) variance engine vs the CPU oracle and the FP64 engine.
+
+Same gate as the FP64 path: posterior mean / variance within 1e-10 relative
+(normwise per output vector), through the C ABI.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("no HIP device", allow_module_level=True)
+
+from gp2d import engine as E  # noqa: E402
+from oracle import gp2d_oracle as O  # noqa: E402
+
+
+def rel(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300))
+
+
+def tracks(n, seed):
+    rng = np.random.default_rng(seed)
+    x = np.stack([rng.uniform(0, 60, n), rng.uniform(0, 45, n)], 1)
+    y = np.concatenate([np.sin(x[:, 1] / 7), np.cos(x[:, 0] / 9)]) + rng.normal(0, 0.05, 2 * n)
+    return x, y
+
+
+@pytest.mark.parametrize("ntr,m,kind,l", [(100, 700, "df", 5.0), (300, 1500, "mixed", 4.0), (1000, 3000, "cf", 3.0),
+                                          (1024, 2048, "df", 5.0), (64, 130, "scalar", 6.0)])
+def test_ozaki_matches_oracle(ntr, m, kind, l):
+    x, y = tracks(ntr, ntr)
+    rng = np.random.default_rng(m)
+    xg = np.stack([rng.uniform(-5, 65, m), rng.uniform(-5, 50, m)], 1)
+    ratio = 0.5 if kind == "mixed" else 1.0
+    ks = E.KernelSpec(kind=kind, l_df=l, l_cf=l * 1.3, ratio=ratio)
+    gp = E.fit(ks, x, y, noise=0.0025, variance="ozaki")
+    mu, var = E.predict(gp, xg, chunk=1024)
+    mo, vo = O.fit_predict(x, y, xg, kind=kind, l_df=l, l_cf=l * 1.3, ratio=ratio, noise=0.0025)
+    assert rel(mu.cpu().numpy(), mo) < 1e-10
+    assert rel(var.cpu().numpy(), vo) < 1e-10
+
+
+def test_ozaki_vs_f64_engine_and_golden(golden):
+    g = golden("mykernel_divfree_N1024.npz")
+    x = np.stack([g["x"], g["y"]], 1)
+    y = np.concatenate([g["u"], g["v"]])
+    ks = E.KernelSpec(kind="df", l_df=5.0)
+    gpo = E.fit(ks, x, y, noise=float(g["noise"]), variance="ozaki")
+    gpf = E.fit(ks, x, y, noise=float(g["noise"]))
+    mo, vo = (t.cpu().numpy() for t in E.predict(gpo, g["xg"]))
+    mf, vf = (t.cpu().numpy() for t in E.predict(gpf, g["xg"]))
+    assert rel(vo, g["var"]) < 1e-10 and rel(mo, g["mean"]) < 1e-10
+    assert rel(vo, vf) < 1e-11
+    # elementwise check on the small-variance points (near observations)
+    assert np.max(np.abs(vo - vf) / np.abs(vf)) < 1e-9
+
+
+def test_ozaki_sharding_bit_identical():
+    from gp2d import data as D
+    from gp2d.distributed import assemble_from_shards
+    x, y = tracks(500, 9)
+    rng = np.random.default_rng(10)
+    xg = np.stack([rng.uniform(-5, 65, 3000), rng.uniform(-5, 50, 3000)], 1)
+    gp = E.fit(E.KernelSpec(kind="df", l_df=5.0), x, y, noise=0.0025, variance="ozaki")
+    m_all, v_all = (t.cpu().numpy() for t in E.predict(gp, xg, chunk=1024))
+    shards_m, shards_v = [], []
+    for r in range(3):
+        lo, hi = D.shard_range(xg.shape[0], 3, r)
+        mm, vv = E.predict(gp, xg[lo:hi], chunk=512)
+        shards_m.append((lo, hi, mm.cpu().numpy()))
+        shards_v.append((lo, hi, vv.cpu().numpy()))
+    assert np.array_equal(assemble_from_shards(xg.shape[0], 2, shards_v), v_all)
+    assert np.array_equal(assemble_from_shards(xg.shape[0], 2, shards_m), m_all)
