@@ -164,6 +164,14 @@ def main():
         return
 
     achieved = kflops / (kms * 1e-3) / 1e12 if kms > 0 else None
+    traffic = None
+    pmc_json = args.pmc_json or os.path.join(ROOT, "profiles", f"r01_pmc_traffic_{args.variance}.json")
+    try:
+        with open(pmc_json) as f:
+            pmc = json.load(f)
+        traffic = pmc.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
     if args.variance == "ozaki":
         # dominant kernel = the nmod int8 GEMMs; executed int8 ops per launch = nmod × the
         # FP64-equivalent algorithmic count (one exact product per modulus)
@@ -182,14 +190,6 @@ def main():
                 "kernel": "gemm_f64_kernel<NN,COLSQ> (variance ‖L⁻¹k*‖²)",
                 "launches": klaunch, "avg_launch_ms": (kms / klaunch) if klaunch else None,
                 "flops_per_launch": (kflops / klaunch) if klaunch else None}
-    traffic = None
-    pmc_json = args.pmc_json or os.path.join(ROOT, "profiles", f"r01_pmc_traffic_{args.variance}.json")
-    try:
-        with open(pmc_json) as f:
-            pmc = json.load(f)
-        traffic = pmc.get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
-        pass
     out = {
         "metric": METRIC,
         "value": value,

@@ -27,7 +27,10 @@ def main():
     w = per_launch(write_csv, "WRITE_SIZE", pat)
     fetch_b = 2.0 * 1024.0 * sum(f) / len(f)
     write_b = 1024.0 * sum(w) / len(w)
-    alg = 8.0 * (n * (n + 128) / 2 + n * ncols + (n // 128) * ncols)  # W lower half + K* chunk + partials
+    if "igemm" in pat:  # int8 residue planes: W lower half + K* chunk (read) + residue plane (written)
+        alg = 1.0 * (n * (n + 256) / 2 + n * ncols + n * ncols)
+    else:               # fp64: W lower half + K* chunk + partials
+        alg = 8.0 * (n * (n + 128) / 2 + n * ncols + (n // 128) * ncols)
     res = {"kernel": pat, "launches_fetch": len(f), "launches_write": len(w),
            "fetch_bytes_per_launch_raw": 1024.0 * sum(f) / len(f), "fetch_bytes_per_launch": fetch_b,
            "write_bytes_per_launch": write_b, "hbm_bytes_per_launch": fetch_b + write_b,
