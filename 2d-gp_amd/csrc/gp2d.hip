@@ -81,9 +81,9 @@ static int assemble_impl(const double* xa, int64_t na, int64_t na_pad, const dou
 static const int kModuli[OZ_MAXMOD] = {256, 255, 253, 251, 247, 241, 239, 233,
                                        229, 227, 223, 217, 211, 199, 197, 193};
 
-static int ozaki_nmod_for(int64_t n) {
-  // need Π m_l > n · 2^{2p} (|Pint| ≤ n·2^p·2^{p−1}) with one guard bit
-  const double need = std::log2((double)n) + 2.0 * OZ_P + 1.0;
+// number of moduli for a bound on log2 max|Pint| (one guard bit: Π m_l > 2·max|Pint|)
+static int ozaki_nmod_bits(double log2_pmax) {
+  const double need = log2_pmax + 2.0;
   double bits = 0.0;
   for (int l = 0; l < OZ_MAXMOD; ++l) {
     bits += std::log2((double)kModuli[l]);
@@ -91,6 +91,8 @@ static int ozaki_nmod_for(int64_t n) {
   }
   return -1;
 }
+// worst case (sizing): |Pint| ≤ n·2^p·2^{p−1}
+static int ozaki_nmod_for(int64_t n) { return ozaki_nmod_bits(std::log2((double)n) + 2.0 * OZ_P - 1.0); }
 
 static int64_t modinv(int64_t a, int64_t m) {  // a⁻¹ mod m (a, m coprime)
   int64_t t = 0, nt = 1, r = m, nr = ((a % m) + m) % m;
@@ -112,9 +114,9 @@ static double kstar_bound(const gp2d_kernel_t* k) {
   }
 }
 
-static int make_ozaki_consts(int64_t n, const gp2d_kernel_t* k, OzakiConsts& oc) {
-  oc.nmod = ozaki_nmod_for(n);
-  GP2D_REQUIRE(oc.nmod > 0, "ozaki: matrix order too large for the modulus table");
+static int make_ozaki_consts(int nmod, const gp2d_kernel_t* k, OzakiConsts& oc) {
+  oc.nmod = nmod;
+  GP2D_REQUIRE(oc.nmod > 0 && oc.nmod <= OZ_MAXMOD, "ozaki: bad number of moduli");
   double M = 1.0;
   for (int l = 0; l < oc.nmod; ++l) M *= (double)kModuli[l];
   oc.M = M;
@@ -174,34 +176,96 @@ int gp2d_assemble(const double* xa, int64_t na, int64_t na_pad, const double* xb
 // ------------------------------------------------------------------------ POTRF
 size_t gp2d_potrf_workspace(int64_t) { return 0; }
 
+namespace {
+// Side stream + event pool for the POTRF look-ahead (one per device, created lazily).
+struct SideStreams {
+  std::mutex mu;
+  std::vector<hipStream_t> side;   // indexed by device
+  std::vector<std::vector<hipEvent_t>> ev;
+};
+SideStreams g_side;
+
+int side_stream(hipStream_t* out, std::vector<hipEvent_t>** evs) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) { set_error("hipGetDevice failed"); return -1; }
+  std::lock_guard<std::mutex> lk(g_side.mu);
+  if ((int)g_side.side.size() <= dev) { g_side.side.resize(dev + 1, nullptr); g_side.ev.resize(dev + 1); }
+  if (!g_side.side[dev]) {
+    if (hipStreamCreateWithFlags(&g_side.side[dev], hipStreamNonBlocking) != hipSuccess) {
+      set_error("hipStreamCreate failed"); return -1;
+    }
+    g_side.ev[dev].resize(2);
+    for (auto& e : g_side.ev[dev])
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) { set_error("hipEventCreate failed"); return -1; }
+  }
+  *out = g_side.side[dev];
+  *evs = &g_side.ev[dev];
+  return 0;
+}
+
+int launch_panel(double* A, int64_t lda, int k, int64_t n, const double* dinv, hipStream_t s) {
+  const int k0 = k * NB;
+  const int rows = (int)(n - k0 - NB);
+  if (rows <= 0) return 0;
+  // in-place panel TRSM  L21 = A21 · inv(L11)ᵀ
+  GemmParams p = gemm_params();
+  p.A = A + (int64_t)(k0 + NB) * lda + k0; p.lda = lda;
+  p.B = dinv + (int64_t)k * NB * NB; p.ldb = NB;
+  p.C = A + (int64_t)(k0 + NB) * lda + k0; p.ldc = lda;
+  p.M = rows; p.N = NB; p.K = NB;
+  return launch_gemm<true, EPI_STORE>(p, 1, s);
+}
+}  // namespace
+
+// Right-looking blocked Cholesky with one step of look-ahead: after step k's panel, the
+// update of block column k+1 runs first; block column k+1's diagonal factorisation and
+// panel then run on a side stream while the rest of step k's trailing SYRK (columns ≥ k+2)
+// runs on the caller's stream, so the single-workgroup diagonal kernel hides under the
+// chip-wide SYRK.  Data regions of the two streams are disjoint (column block k+1 vs ≥ k+2).
 int gp2d_potrf(double* A, int64_t n, int64_t lda, double* dinv, int* info_dev, void*, size_t, void* stream) {
   GP2D_REQUIRE(n % NB == 0 && n > 0, "potrf: n must be a positive multiple of 128");
   GP2D_REQUIRE(lda >= n && lda % 2 == 0, "potrf: lda must be >= n and even");
+  GP2D_REQUIRE(dinv != nullptr, "potrf: dinv buffer is required");
   hipStream_t s = S(stream);
   const int nb = (int)(n / NB);
-  for (int k = 0; k < nb; ++k) {
-    const int k0 = k * NB;
-    potrf_diag_kernel<<<1, 256, 0, s>>>(A, lda, k0, dinv, info_dev);
+  hipStream_t s2;
+  std::vector<hipEvent_t>* ev;
+  GP2D_CHECK(side_stream(&s2, &ev));
+  hipEvent_t e_col = (*ev)[0], e_pan = (*ev)[1];
+  potrf_diag_kernel<<<1, 256, 0, s>>>(A, lda, 0, dinv, info_dev);
+  GP2D_CHECK(check_launch("potrf_diag_kernel"));
+  GP2D_CHECK(launch_panel(A, lda, 0, n, dinv, s));
+  for (int k = 0; k + 1 < nb; ++k) {
+    const int k0 = k * NB, k1 = k0 + NB;
+    const double* Lk = A + (int64_t)k1 * lda + k0;     // panel k, rows ≥ k+1
+    // (1) update block column k+1:  A[k+1.., k+1] −= L[k+1.., k] · L[k+1, k]ᵀ
+    GemmParams c = gemm_params();
+    c.A = Lk; c.lda = lda;
+    c.B = Lk; c.ldb = lda;                              // rows of block k+1 = first NB rows of the panel
+    c.C = A + (int64_t)k1 * lda + k1; c.ldc = lda;
+    c.M = (int)(n - k1); c.N = NB; c.K = NB;
+    c.alpha = -1.0; c.beta = 1.0;
+    GP2D_CHECK((launch_gemm<true, EPI_STORE>(c, 1, s)));
+    if (hipEventRecord(e_col, s) != hipSuccess) { set_error("hipEventRecord failed"); return -1; }
+    // (2) side stream: factor diagonal block k+1 and its panel
+    if (hipStreamWaitEvent(s2, e_col, 0) != hipSuccess) { set_error("hipStreamWaitEvent failed"); return -1; }
+    potrf_diag_kernel<<<1, 256, 0, s2>>>(A, lda, k1, dinv, info_dev);
     GP2D_CHECK(check_launch("potrf_diag_kernel"));
-    if (k == nb - 1) break;
-    const int rows = (int)(n - k0 - NB);
-    // in-place panel TRSM  L21 = A21 · inv(L11)ᵀ   (needs inv(L11): from dinv or recomputed)
-    const double* inv_kk = dinv ? dinv + (int64_t)k * NB * NB : nullptr;
-    GP2D_REQUIRE(inv_kk != nullptr, "potrf: dinv buffer is required");
-    GemmParams p = gemm_params();
-    p.A = A + (int64_t)(k0 + NB) * lda + k0; p.lda = lda;
-    p.B = inv_kk; p.ldb = NB;
-    p.C = A + (int64_t)(k0 + NB) * lda + k0; p.ldc = lda;
-    p.M = rows; p.N = NB; p.K = NB;
-    GP2D_CHECK((launch_gemm<true, EPI_STORE>(p, 1, s)));
-    // trailing SYRK  A22 −= L21 L21ᵀ  (lower tiles)
-    GemmParams q = gemm_params();
-    q.A = A + (int64_t)(k0 + NB) * lda + k0; q.lda = lda;
-    q.B = q.A; q.ldb = lda;
-    q.C = A + (int64_t)(k0 + NB) * lda + (k0 + NB); q.ldc = lda;
-    q.M = rows; q.N = rows; q.K = NB;
-    q.alpha = -1.0; q.beta = 1.0; q.c_lower = 1;
-    GP2D_CHECK((launch_gemm<true, EPI_STORE>(q, 1, s)));
+    GP2D_CHECK(launch_panel(A, lda, k + 1, n, dinv, s2));
+    if (hipEventRecord(e_pan, s2) != hipSuccess) { set_error("hipEventRecord failed"); return -1; }
+    // (3) rest of the trailing update, columns ≥ k+2 (lower tiles)
+    const int rest = (int)(n - k1 - NB);
+    if (rest > 0) {
+      GemmParams q = gemm_params();
+      q.A = Lk + (int64_t)NB * lda; q.lda = lda;
+      q.B = q.A; q.ldb = lda;
+      q.C = A + (int64_t)(k1 + NB) * lda + (k1 + NB); q.ldc = lda;
+      q.M = rest; q.N = rest; q.K = NB;
+      q.alpha = -1.0; q.beta = 1.0; q.c_lower = 1;
+      GP2D_CHECK((launch_gemm<true, EPI_STORE>(q, 1, s)));
+    }
+    // next step needs panel k+1
+    if (hipStreamWaitEvent(s, e_pan, 0) != hipSuccess) { set_error("hipStreamWaitEvent failed"); return -1; }
   }
   dim3 zg((unsigned)((n / 2 + 255) / 256), (unsigned)n);
   zero_upper_kernel<<<zg, 256, 0, s>>>(A, n, lda);
@@ -359,14 +423,32 @@ size_t gp2d_ozaki_wres_bytes(int64_t n) {
 }
 
 int gp2d_ozaki_prepare(const double* W, int64_t n, int64_t ldw, const gp2d_kernel_t* k, int8_t* wres,
-                       double* rowscale, void* stream) {
+                       double* rowscale, int* nmod_out, void* stream) {
   GP2D_CHECK(validate_kernel(k));
   GP2D_REQUIRE(k->family == GP2D_FAMILY_VECTOR2D, "ozaki: vector2d family only");
   GP2D_REQUIRE(n % IBM == 0 && n > 0, "ozaki: n must be a positive multiple of 256");
+  GP2D_REQUIRE(nmod_out != nullptr, "ozaki: nmod_out is NULL");
+  hipStream_t s = S(stream);
+  double* l1 = reinterpret_cast<double*>(wres);  // scratch: the planes are written afterwards
+  ozaki_w_scale_kernel<<<(unsigned)n, 256, 0, s>>>(W, n, ldw, rowscale, l1);
+  GP2D_CHECK(check_launch("ozaki_w_scale_kernel"));
+  std::vector<double> hl1((size_t)n);
+  if (hipMemcpyAsync(hl1.data(), l1, sizeof(double) * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess) {
+    set_error("ozaki: reading the row bounds failed");
+    return -1;
+  }
+  double mx = 0.0;
+  for (double v : hl1) mx = std::max(mx, v);
+  // |Pint_ij| ≤ l1_i · 2^{p−1}; the fp64 row sums carry ≤ n·2^-53 relative error → 1 % margin
+  const int nmod = ozaki_nmod_bits(std::log2(std::max(mx, 1.0) * 1.01) + (OZ_P - 1));
+  GP2D_REQUIRE(nmod > 0, "ozaki: row bound exceeds the modulus table");
   OzakiConsts oc;
-  GP2D_CHECK(make_ozaki_consts(n, k, oc));
-  ozaki_w_prep_kernel<<<(unsigned)n, 256, 0, S(stream)>>>(W, n, ldw, oc, wres, rowscale);
-  return check_launch("ozaki_w_prep_kernel");
+  GP2D_CHECK(make_ozaki_consts(nmod, k, oc));
+  ozaki_w_res_kernel<<<(unsigned)n, 256, 0, s>>>(W, n, ldw, oc, wres, rowscale);
+  GP2D_CHECK(check_launch("ozaki_w_res_kernel"));
+  *nmod_out = nmod;
+  return 0;
 }
 
 size_t gp2d_predict_ozaki_workspace(int64_t n, int64_t chunk) {
@@ -378,7 +460,8 @@ size_t gp2d_predict_ozaki_workspace(int64_t n, int64_t chunk) {
          + sizeof(double) * ((size_t)(n / 2 / OZ_KS_T + 1) + (size_t)(n / OZ_CRT_ROWS + 1)) * ncols;
 }
 
-int gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int64_t n, const double* alpha, const double* xtr,
+int gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int nmod, int64_t n, const double* alpha,
+                       const double* xtr,
                        int64_t ntr, int64_t ntr_pad, const double* xg, int64_t m, const gp2d_kernel_t* k,
                        int var_mode, double noise, int compute_var, double* mean, double* var, int64_t chunk,
                        void* work, size_t work_bytes, void* stream) {
@@ -390,8 +473,9 @@ int gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int64_t n, co
   GP2D_REQUIRE(var_mode >= 0 && var_mode <= 2, "predict: bad var_mode");
   if (m <= 0) return 0;
   hipStream_t s = S(stream);
+  GP2D_REQUIRE(nmod > 0 && nmod <= ozaki_nmod_for(n), "ozaki: nmod exceeds the worst-case count the workspace is sized for");
   OzakiConsts oc;
-  GP2D_CHECK(make_ozaki_consts(n, k, oc));
+  GP2D_CHECK(make_ozaki_consts(nmod, k, oc));
   const int nm = oc.nmod;
   const int64_t ncols_max = 2 * chunk;
   int8_t* bres = reinterpret_cast<int8_t*>(work);

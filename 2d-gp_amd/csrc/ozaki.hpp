@@ -23,7 +23,7 @@
 namespace gp2d {
 
 constexpr int OZ_MAXMOD = 16;
-constexpr int OZ_P = 42;           // integer bits of the scaled operands
+constexpr int OZ_P = 50;           // integer bits of the scaled operands (≤ 50: residues stay exact)
 constexpr int OZ_HBITS = 33;       // exact high part of inv_l / m_l
 
 struct OzakiConsts {
@@ -46,26 +46,53 @@ __device__ __forceinline__ int centred_residue(double x, double m, double inv_m)
 }
 
 // ------------------------------------------------------------------ W preparation
-// One workgroup per row i: row max (k ≤ i) → s_i; residue planes Wres[l][i][k] (int8, full
-// row, zeros above the diagonal) and rowscale[i] = M·2^{−s_i−s_B}.
-__global__ __launch_bounds__(256) void ozaki_w_prep_kernel(const double* __restrict__ W, int64_t n, int64_t ldw,
-                                                           OzakiConsts oc, int8_t* __restrict__ wres,
-                                                           double* __restrict__ rowscale) {
+// Pass 1 (one workgroup per row i): row max (k ≤ i) → s_i (stored in rowscale[i]) and the
+// row's L1 norm Σ_k |rint(W_ik·2^{s_i})| (stored in l1[i]).  The host turns max_i l1_i into
+// the number of moduli: |Pint_ij| ≤ l1_i·max|Bint| < M/2 (a per-row bound, far tighter than
+// the worst case n·2^{2p}).
+__device__ __forceinline__ double block_reduce(double v, double* red, bool is_max) {
+  const int tid = threadIdx.x;
+  red[tid] = v;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (tid < s) red[tid] = is_max ? fmax(red[tid], red[tid + s]) : red[tid] + red[tid + s];
+    __syncthreads();
+  }
+  const double r = red[0];
+  __syncthreads();
+  return r;
+}
+
+__global__ __launch_bounds__(256) void ozaki_w_scale_kernel(const double* __restrict__ W, int64_t n, int64_t ldw,
+                                                            double* __restrict__ rowscale, double* __restrict__ l1) {
   __shared__ double red[256];
   const int64_t i = blockIdx.x;
   const int tid = threadIdx.x;
   const double* w = W + i * ldw;
   double mx = 0.0;
   for (int64_t k = tid; k <= i; k += 256) mx = fmax(mx, fabs(w[k]));
-  red[tid] = mx;
-  __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if (tid < s) red[tid] = fmax(red[tid], red[tid + s]);
-    __syncthreads();
-  }
-  mx = red[0];
+  mx = block_reduce(mx, red, true);
   const int e = (mx > 0.0) ? ilogb(mx) : 0;    // 2^e ≤ mx < 2^{e+1}
   const int si = OZ_P - 1 - e;                 // |W·2^si| < 2^OZ_P
+  double sum = 0.0;
+  for (int64_t k = tid; k <= i; k += 256) sum += fabs(rint(ldexp(w[k], si)));
+  sum = block_reduce(sum, red, false);
+  if (tid == 0) {
+    rowscale[i] = (double)si;
+    l1[i] = sum;
+  }
+}
+
+// Pass 2: residue planes Wres[l][i][k] (int8, full row, zeros above the diagonal) and the
+// final rowscale[i] = M·2^{−s_i−s_B}.
+__global__ __launch_bounds__(256) void ozaki_w_res_kernel(const double* __restrict__ W, int64_t n, int64_t ldw,
+                                                          OzakiConsts oc, int8_t* __restrict__ wres,
+                                                          double* __restrict__ rowscale) {
+  const int64_t i = blockIdx.x;
+  const int tid = threadIdx.x;
+  const double* w = W + i * ldw;
+  const int si = (int)rowscale[i];
+  __syncthreads();
   if (tid == 0) rowscale[i] = ldexp(oc.M, -si - oc.sB);
   // 4 consecutive k per thread → one packed dword store per plane
   for (int64_t k0 = (int64_t)tid * 4; k0 < n; k0 += 1024) {

@@ -75,10 +75,10 @@ _SIGS = {
     "gp2d_predict": (_I, [_P, _I64, _I64, _P, _P, _I64, _I64, _P, _I64, _KP, _I, _D, _I, _P, _P, _I64, _P, _SZ, _P]),
     "gp2d_ozaki_nmod": (_I, [_I64]),
     "gp2d_ozaki_wres_bytes": (_SZ, [_I64]),
-    "gp2d_ozaki_prepare": (_I, [_P, _I64, _I64, _KP, _P, _P, _P]),
+    "gp2d_ozaki_prepare": (_I, [_P, _I64, _I64, _KP, _P, _P, ctypes.POINTER(_I), _P]),
     "gp2d_predict_ozaki_workspace": (_SZ, [_I64, _I64]),
-    "gp2d_predict_ozaki": (_I, [_P, _P, _I64, _P, _P, _I64, _I64, _P, _I64, _KP, _I, _D, _I, _P, _P, _I64, _P, _SZ,
-                                _P]),
+    "gp2d_predict_ozaki": (_I, [_P, _P, _I, _I64, _P, _P, _I64, _I64, _P, _I64, _KP, _I, _D, _I, _P, _P, _I64, _P,
+                                _SZ, _P]),
     "gp2d_timing_enable": (None, [_I]),
     "gp2d_timing_read": (_I, [ctypes.POINTER(_D), ctypes.POINTER(_I64), ctypes.POINTER(_D)]),
     "gp2d_last_error": (ctypes.c_char_p, []),

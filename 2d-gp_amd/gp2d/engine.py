@@ -210,9 +210,10 @@ def ozaki_prepare(gp: GPFit) -> GPFit:
     wres = torch.empty(int(L.gp2d_ozaki_wres_bytes(n)), dtype=torch.int8, device=gp.device)
     rowscale = torch.empty(n, dtype=torch.float64, device=gp.device)
     desc = gp.kernel.desc()
+    nmod = ctypes.c_int(0)
     N.check(L.gp2d_ozaki_prepare(_ptr(gp.W), n, n, ctypes.byref(desc), _ptr(wres), _ptr(rowscale),
-                                 _stream_handle(gp.device)), "gp2d_ozaki_prepare")
-    gp.extra["ozaki"] = (wres, rowscale)
+                                 ctypes.byref(nmod), _stream_handle(gp.device)), "gp2d_ozaki_prepare")
+    gp.extra["ozaki"] = (wres, rowscale, int(nmod.value))
     return gp
 
 
@@ -248,8 +249,8 @@ class Predictor:
             mean, var = out
         desc = gp.kernel.desc()
         if self.ozaki and "ozaki" in gp.extra:
-            wres, rowscale = gp.extra["ozaki"]
-            N.check(L.gp2d_predict_ozaki(_ptr(wres), _ptr(rowscale), gp.n, _ptr(gp.alpha), _ptr(gp.x), gp.n_train,
+            wres, rowscale, nmod = gp.extra["ozaki"]
+            N.check(L.gp2d_predict_ozaki(_ptr(wres), _ptr(rowscale), nmod, gp.n, _ptr(gp.alpha), _ptr(gp.x), gp.n_train,
                                          gp.n_pad, _ptr(G), m, ctypes.byref(desc), _VAR_MODES[var_mode],
                                          float(gp.noise), int(bool(compute_var)), _ptr(mean), _ptr(var), self.chunk,
                                          _ptr(self.work), self.wbytes, _stream_handle(gp.device)),

@@ -175,8 +175,7 @@ def main():
     if args.variance == "ozaki":
         # dominant kernel = the nmod int8 GEMMs; executed int8 ops per launch = nmod × the
         # FP64-equivalent algorithmic count (one exact product per modulus)
-        from gp2d import _native as NN
-        nmod = int(NN.lib().gp2d_ozaki_nmod(2 * ((args.ntrain + 127) // 128 * 128)))
+        nmod = int(pred_cache["p"].gp.extra["ozaki"][2])
         roof = {"bound": "mfma", "achieved": achieved * nmod if achieved else None, "peak": INT8_PEAK_TOPS,
                 "unit": "TOP/s (int8)", "frac": (achieved * nmod / INT8_PEAK_TOPS) if achieved else None,
                 "traffic": traffic, "kernel": f"igemm_nt_mod_kernel x{nmod} moduli (Ozaki-II variance, exact)",

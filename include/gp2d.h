@@ -123,18 +123,20 @@ int gp2d_predict(const double* W, int64_t n, int64_t ldw, const double* alpha,
 
 /* ---- predict, FP64-accurate variance on the INT8 matrix cores (Ozaki scheme II) -----
  * Same results contract as gp2d_predict (1e-10 relative parity gate) for the vector2d
- * family; the variance contraction ‖W k*‖² runs as gp2d_ozaki_nmod(n) exact int8 GEMMs
+ * family; the variance contraction ‖W k*‖² runs as nmod exact int8 GEMMs
  * (v_mfma_i32_32x32x32_i8) on residues modulo pairwise-coprime m_l ≤ 256, followed by
  * a Chinese-remainder reconstruction in fp64.  Requires n % 256 == 0.
- * gp2d_ozaki_prepare: once per fit, W → residue planes wres (nmod × n × n int8) and
- * per-row scales rowscale (n doubles).                                                   */
+ * gp2d_ozaki_prepare: once per fit, W → residue planes wres (≤ gp2d_ozaki_wres_bytes(n)
+ * bytes) and per-row scales rowscale (n doubles); *nmod_out receives the number of moduli
+ * the data needs (from per-row L1 bounds of the scaled W; synchronises the stream once).
+ * gp2d_ozaki_nmod(n) is the worst-case count used for sizing.                           */
 int    gp2d_ozaki_nmod(int64_t n);
 size_t gp2d_ozaki_wres_bytes(int64_t n);
 int    gp2d_ozaki_prepare(const double* W, int64_t n, int64_t ldw, const gp2d_kernel_t* k,
-                          int8_t* wres, double* rowscale, void* stream);
+                          int8_t* wres, double* rowscale, int* nmod_out, void* stream);
 size_t gp2d_predict_ozaki_workspace(int64_t n, int64_t chunk);
-int    gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int64_t n, const double* alpha,
-                          const double* xtr, int64_t ntr, int64_t ntr_pad,
+int    gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int nmod, int64_t n,
+                          const double* alpha, const double* xtr, int64_t ntr, int64_t ntr_pad,
                           const double* xg, int64_t m, const gp2d_kernel_t* k,
                           int var_mode, double noise, int compute_var,
                           double* mean, double* var, int64_t chunk,

@@ -53,8 +53,10 @@ def test_ozaki_vs_f64_engine_and_golden(golden):
     mf, vf = (t.cpu().numpy() for t in E.predict(gpf, g["xg"]))
     assert rel(vo, g["var"]) < 1e-10 and rel(mo, g["mean"]) < 1e-10
     assert rel(vo, vf) < 1e-11
-    # elementwise check on the small-variance points (near observations)
-    assert np.max(np.abs(vo - vf) / np.abs(vf)) < 1e-9
+    # elementwise relative check: the small-variance points (near observations) carry the
+    # cancellation kss − ‖W k*‖², so this is the strict form of the 1e-10 gate
+    assert np.max(np.abs(vo - vf) / np.abs(vf)) < 1e-10
+    assert 1 <= gpo.extra["ozaki"][2] <= E.N.lib().gp2d_ozaki_nmod(gpo.n)
 
 
 def test_ozaki_sharding_bit_identical():
