@@ -191,7 +191,11 @@ int side_stream(hipStream_t* out, std::vector<hipEvent_t>** evs) {
   std::lock_guard<std::mutex> lk(g_side.mu);
   if ((int)g_side.side.size() <= dev) { g_side.side.resize(dev + 1, nullptr); g_side.ev.resize(dev + 1); }
   if (!g_side.side[dev]) {
-    if (hipStreamCreateWithFlags(&g_side.side[dev], hipStreamNonBlocking) != hipSuccess) {
+    // highest priority: the side stream carries the POTRF critical path (diagonal block +
+    // panel), whose single-workgroup kernel must not queue behind the trailing SYRK tiles
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) { lo = 0; hi = 0; }
+    if (hipStreamCreateWithPriority(&g_side.side[dev], hipStreamNonBlocking, hi) != hipSuccess) {
       set_error("hipStreamCreate failed"); return -1;
     }
     g_side.ev[dev].resize(2);
@@ -501,14 +505,16 @@ int gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int nmod, int
         std::lock_guard<std::mutex> lk(g_timing.mu);
         if (g_timing.on) { e0 = g_timing.get(); e1 = g_timing.get(); hipEventRecord(e0, s); }
       }
+      // two waves per SIMD (igemm_nt_mod_w8_kernel): 0.57 ms vs 0.62-0.70 ms per 8192×16384×8192
+      // launch for one wave per SIMD on random residues (tools/microbench/igemm_bench.hip); the
+      // XCD-grouped tile order measured no faster for it, so row-major heavy-first order is used.
       const int nr = (int)(n / IBM), nc = (int)(ncols / IBN);
-      const bool xg8 = (nr % 4 == 0) && (nc % 8 == 0) && (((nr / 4) * (nc / 8)) % 8 == 0);
-      const dim3 ggrid = xg8 ? dim3((unsigned)(nr * nc)) : dim3((unsigned)nc, (unsigned)nr);
+      const dim3 ggrid((unsigned)nc, (unsigned)nr);
       for (int l = 0; l < nm; ++l) {
-        igemm_nt_mod_kernel<<<ggrid, 256, 0, s>>>(
+        igemm_nt_mod_w8_kernel<<<ggrid, 512, 0, s>>>(
             wres + (size_t)l * n * n, n, bres + (size_t)l * ncols * n, n, cres + (size_t)l * n * ncols, n,
-            (int)n, (int)ncols, (int)n, 1, oc.m[l], oc.inv_m[l], xg8 ? 1 : 0);
-        GP2D_CHECK(check_launch("igemm_nt_mod_kernel"));
+            (int)n, (int)ncols, (int)n, 1, oc.m[l], oc.inv_m[l], 0);
+        GP2D_CHECK(check_launch("igemm_nt_mod_w8_kernel"));
       }
       if (e0) {
         std::lock_guard<std::mutex> lk(g_timing.mu);

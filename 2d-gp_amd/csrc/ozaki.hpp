@@ -381,6 +381,162 @@ __global__ __launch_bounds__(256, 1) void igemm_nt_mod_kernel(const int8_t* __re
   }
 }
 
+// Two waves per SIMD variant: 512 threads = 8 waves as 2×4, each wave 128×64 (4×2 tiles of
+// 32x32x32, 128 accumulators, ≤ 256 registers).  While one wave of a SIMD issues its LDS-DMA
+// pieces and fragment reads, the other keeps the matrix core busy — with one wave per SIMD
+// the issue cost of the DMA pieces stalls the MFMA stream.  Same LDS ring, swizzle, slab
+// pipeline and epilogue as igemm_nt_mod_kernel; each wave moves 4 DMA pieces per slab.
+__device__ __forceinline__ void igemm_tile_coords(int xcd_groups, int M, int N, int& bi, int& bj) {
+  if (xcd_groups) {
+    const int nr = M / IBM, nc = N / IBN, ncg = nc / 8;
+    const int t = blockIdx.x, x = t & 7, q = t >> 3;
+    const int G = q >> 5, w = q & 31;
+    const int P = G * 8 + x;
+    const int rg = P / ncg, cg = P - rg * ncg;
+    bi = nr - 1 - (4 * rg + (w >> 3));
+    bj = 8 * cg + (w & 7);
+  } else {
+    bj = blockIdx.x;
+    bi = (int)(gridDim.y - 1 - blockIdx.y);
+  }
+}
+
+__global__ __launch_bounds__(512, 1) void igemm_nt_mod_w8_kernel(const int8_t* __restrict__ A, int64_t lda,
+                                                                 const int8_t* __restrict__ B, int64_t ldb,
+                                                                 uint8_t* __restrict__ C, int64_t ldc, int M, int N,
+                                                                 int K, int a_lower, int modulus, double inv_mod,
+                                                                 int xcd_groups) {
+  __shared__ __attribute__((aligned(16))) int8_t smem[I_NSTAGE * I_STAGE];
+  int bi, bj;
+  igemm_tile_coords(xcd_groups, M, N, bi, bj);
+  const int i0 = bi * IBM, j0 = bj * IBN;
+  const int ke = a_lower ? min(K, i0 + IBM) : K;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+  const int lr = lane & 31, lh = lane >> 5;
+
+  i16v acc[4][2];
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) acc[mi][ni] = i16v{0};
+
+  // wave wid fills rows [32·wid, 32·wid+32) of both operands: 2 pieces of 16 rows each
+  const int drow = lane >> 2, dchunk = lane & 3;
+  auto issue = [&](int k0, int st) {
+#ifdef GP2D_IGEMM_NO_DMA
+    return;
+#endif
+    int8_t* As = smem + st * I_STAGE;
+    int8_t* Bs = As + I_OP;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int row = wid * 32 + h * 16 + drow;
+      const int c = swz(row, dchunk);
+      __builtin_amdgcn_global_load_lds((const void*)(A + (int64_t)(i0 + row) * lda + k0 + 16 * c),
+                                       (lds_ptr_t)(As + (wid * 32 + h * 16) * IBK), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(B + (int64_t)(j0 + row) * ldb + k0 + 16 * c),
+                                       (lds_ptr_t)(Bs + (wid * 32 + h * 16) * IBK), 16, 0, 0);
+    }
+  };
+  const uint32_t lds_base = (uint32_t)(size_t)(lds_ptr_t)smem;
+  auto readf = [&](int st, int kc, i4v (&a)[4], i4v (&b)[2]) {
+    const uint32_t As = lds_base + st * I_STAGE;
+    const uint32_t Bs = As + I_OP;
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+      const int row = wr * 128 + mi * 32 + lr;
+      const uint32_t ad = As + row * IBK + 16 * swz(row, 2 * kc + lh);
+      asm volatile("ds_read_b128 %0, %1" : "=v"(a[mi]) : "v"(ad) : "memory");
+    }
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) {
+      const int row = wc * 64 + ni * 32 + lr;
+      const uint32_t ad = Bs + row * IBK + 16 * swz(row, 2 * kc + lh);
+      asm volatile("ds_read_b128 %0, %1" : "=v"(b[ni]) : "v"(ad) : "memory");
+    }
+  };
+  auto mfmas = [&](const i4v (&a)[4], const i4v (&b)[2]) {
+#ifdef GP2D_IGEMM_NO_MFMA
+    acc[0][0][0] += a[0][0] ^ b[0][0];
+    return;
+#endif
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+        acc[mi][ni] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
+  };
+  const int nsl = ke / IBK;
+  if (nsl > 0) {
+    issue(0, 0);
+    if (nsl > 1) issue(IBK, 1);
+    if (nsl > 2) issue(2 * IBK, 2);
+    if (nsl > 2) GP2D_VMWAIT_BARRIER(8);
+    else if (nsl > 1) GP2D_VMWAIT_BARRIER(4);
+    else GP2D_VMWAIT_BARRIER(0);
+    i4v a0[4], b0[2], a1[4], b1[2];
+    readf(0, 0, a0, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    int st = 0;
+    for (int s = 0; s < nsl; ++s) {
+      int st3 = st + 3;
+      if (st3 >= I_NSTAGE) st3 -= I_NSTAGE;
+      if (s + 3 < nsl) issue((s + 3) * IBK, st3);
+      readf(st, 1, a1, b1);
+      asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      mfmas(a0, b0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (s + 1 < nsl) {
+        if (s + 3 < nsl) GP2D_VMWAIT_BARRIER(8);
+        else if (s + 2 < nsl) GP2D_VMWAIT_BARRIER(4);
+        else GP2D_VMWAIT_BARRIER(0);
+        int st1 = st + 1;
+        if (st1 >= I_NSTAGE) st1 -= I_NSTAGE;
+        readf(st1, 0, a0, b0);
+      }
+      else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      mfmas(a1, b1);
+      __builtin_amdgcn_sched_barrier(0);
+      st = (st + 1 == I_NSTAGE) ? 0 : st + 1;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+  uint8_t* T = reinterpret_cast<uint8_t*>(smem);
+  constexpr int TP = IBM + 16;
+  const float fim = (float)inv_mod;
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        uint32_t pk = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int v = acc[mi][ni][4 * g + u];
+          const int q = (int)floorf((float)v * fim);
+          int res = v - q * modulus;
+          res += (res < 0) ? modulus : 0;
+          res -= (res >= modulus) ? modulus : 0;
+          pk |= (uint32_t)res << (8 * u);
+        }
+        const int rloc = wr * 128 + mi * 32 + 8 * g + 4 * lh;
+        const int cloc = wc * 64 + ni * 32 + lr;
+        *reinterpret_cast<uint32_t*>(T + cloc * TP + rloc) = pk;
+      }
+  __syncthreads();
+#pragma unroll
+  for (int p = 0; p < (IBM * IBN / 16) / 512; ++p) {
+    const int id = tid + 512 * p;
+    const int cloc = id >> 4, ch = id & 15;
+    const uint4 v = *reinterpret_cast<const uint4*>(T + cloc * TP + 16 * ch);
+    *reinterpret_cast<uint4*>(C + (int64_t)(j0 + cloc) * ldc + i0 + 16 * ch) = v;
+  }
+}
+
 // ------------------------------------------------------------------ CRT + column Σ V²
 // Residue planes are column-major ([j][i], ld = n).  One wave per column j and 1024-row
 // segment: lane l reconstructs rows 16l..16l+15 (one 16-B load per plane), squares, and the
