@@ -505,16 +505,12 @@ int gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int nmod, int
         std::lock_guard<std::mutex> lk(g_timing.mu);
         if (g_timing.on) { e0 = g_timing.get(); e1 = g_timing.get(); hipEventRecord(e0, s); }
       }
-      // two waves per SIMD (igemm_nt_mod_w8_kernel): 0.57 ms vs 0.62-0.70 ms per 8192×16384×8192
-      // launch for one wave per SIMD on random residues (tools/microbench/igemm_bench.hip); the
-      // XCD-grouped tile order measured no faster for it, so row-major heavy-first order is used.
-      const int nr = (int)(n / IBM), nc = (int)(ncols / IBN);
-      const dim3 ggrid((unsigned)nc, (unsigned)nr);
+      const dim3 ggrid((unsigned)(ncols / IBN), (unsigned)(n / IBM));
       for (int l = 0; l < nm; ++l) {
-        igemm_nt_mod_w8_kernel<<<ggrid, 512, 0, s>>>(
-            wres + (size_t)l * n * n, n, bres + (size_t)l * ncols * n, n, cres + (size_t)l * n * ncols, n,
-            (int)n, (int)ncols, (int)n, 1, oc.m[l], oc.inv_m[l], 0);
-        GP2D_CHECK(check_launch("igemm_nt_mod_w8_kernel"));
+        igemm_nt_mod_kernel<<<ggrid, 512, 0, s>>>(wres + (size_t)l * n * n, bres + (size_t)l * ncols * n,
+                                                  cres + (size_t)l * n * ncols, n, (int)n, (int)ncols, (int)n, 1,
+                                                  oc.m[l], oc.inv_m[l]);
+        GP2D_CHECK(check_launch("igemm_nt_mod_kernel"));
       }
       if (e0) {
         std::lock_guard<std::mutex> lk(g_timing.mu);

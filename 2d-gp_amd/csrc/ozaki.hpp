@@ -45,6 +45,12 @@ __device__ __forceinline__ int centred_residue(double x, double m, double inv_m)
   return r;
 }
 
+// Slab-blocked residue planes (see the INT8 GEMM below): element (row, k) of a plane with K
+// columns; a 256-row × 64-byte tile is one contiguous 16 KB.
+__host__ __device__ __forceinline__ int64_t slab_offset(int64_t row, int64_t k, int64_t K) {
+  return (((row >> 8) * (K >> 6) + (k >> 6)) << 14) + ((row & 255) << 6) + (k & 63);
+}
+
 // ------------------------------------------------------------------ W preparation
 // Pass 1 (one workgroup per row i): row max (k ≤ i) → s_i (stored in rowscale[i]) and the
 // row's L1 norm Σ_k |rint(W_ik·2^{s_i})| (stored in l1[i]).  The host turns max_i l1_i into
@@ -83,7 +89,7 @@ __global__ __launch_bounds__(256) void ozaki_w_scale_kernel(const double* __rest
   }
 }
 
-// Pass 2: residue planes Wres[l][i][k] (int8, full row, zeros above the diagonal) and the
+// Pass 2: residue planes Wres[l] (int8, slab-blocked, zeros above the diagonal) and the
 // final rowscale[i] = M·2^{−s_i−s_B}.
 __global__ __launch_bounds__(256) void ozaki_w_res_kernel(const double* __restrict__ W, int64_t n, int64_t ldw,
                                                           OzakiConsts oc, int8_t* __restrict__ wres,
@@ -107,7 +113,7 @@ __global__ __launch_bounds__(256) void ozaki_w_res_kernel(const double* __restri
       uint32_t packed = 0;
 #pragma unroll
       for (int u = 0; u < 4; ++u) packed |= (uint32_t)(uint8_t)(int8_t)centred_residue(x[u], m, oc.inv_m[l]) << (8 * u);
-      *reinterpret_cast<uint32_t*>(wres + ((int64_t)l * n + i) * n + k0) = packed;
+      *reinterpret_cast<uint32_t*>(wres + (int64_t)l * n * n + slab_offset(i, k0, n)) = packed;
     }
   }
 }
@@ -115,7 +121,7 @@ __global__ __launch_bounds__(256) void ozaki_w_res_kernel(const double* __restri
 // ------------------------------------------------------------------ K*ᵀ residues + mean
 // Block: 64 lanes × 4 thread rows.  Lane tx covers training points t = 256·bx + 4tx..+3,
 // thread row ty covers grid points p = 16·by + ty + 4q (q < 4).  Writes the residue planes
-// Bres[l][j][k] (j = grid component row, k = training component column, K-contiguous)
+// Bres[l] (rows j = grid components, columns k = training components, slab-blocked)
 // and mean partials pm[bx][j] = Σ_{k in block} α_k·K*_jk (one wave = one grid point set,
 // reduced by shuffles in a fixed order).
 constexpr int OZ_KS_T = 256;   // training points per block
@@ -190,343 +196,197 @@ __global__ __launch_bounds__(256) void ozaki_kstar_kernel(
       int8_t* plane = bres + (int64_t)l * ncols * n;
       // (grid comp, train comp): (u,u) → row p, col t ; (u,v) → row p, col npad+t ;
       //                          (v,u) → row cp+p, col t ; (v,v) → row cp+p, col npad+t
-      *reinterpret_cast<uint32_t*>(plane + p * n + t0) = pk[0];
-      *reinterpret_cast<uint32_t*>(plane + p * n + npad + t0) = pk[1];
-      *reinterpret_cast<uint32_t*>(plane + (cp + p) * n + t0) = pk[2];
-      *reinterpret_cast<uint32_t*>(plane + (cp + p) * n + npad + t0) = pk[3];
+      // (slab-blocked plane: 4 consecutive columns stay inside one 64-B row segment)
+      *reinterpret_cast<uint32_t*>(plane + slab_offset(p, t0, n)) = pk[0];
+      *reinterpret_cast<uint32_t*>(plane + slab_offset(p, npad + t0, n)) = pk[1];
+      *reinterpret_cast<uint32_t*>(plane + slab_offset(cp + p, t0, n)) = pk[2];
+      *reinterpret_cast<uint32_t*>(plane + slab_offset(cp + p, npad + t0, n)) = pk[3];
     }
   }
 }
 
 // ------------------------------------------------------------------ INT8 NT GEMM mod m
 // C[i][j] = (Σ_k A[i][k]·B[j][k]) mod m, A lower-triangular (row block i0 needs k < i0+256).
-// 256×256 output tile per 256-thread workgroup: 4 waves as 2×2, each wave 128×128 =
-// 4×4 tiles of v_mfma_i32_32x32x32_i8 (256 int32 accumulators per lane in AGPRs, one
-// wave per SIMD).  K advances in 64-byte slabs loaded global→LDS directly
-// (global_load_lds_dwordx4) into a 4-stage ring with three slabs in flight: the per-CU
-// L2/MALL stream (~77 GB/s per CU at the int8 peak) needs ~100 KB outstanding to cover its
-// latency (MI355X_MICROARCH.md, gather / LDS-DMA rows).  Per slab, two 32-deep MFMA steps;
-// the barrier that publishes slab s+1 sits between them, so the fragment reads of the next
-// step always run under 16 MFMAs (512 cycles).  LDS rows are 64 B, unpadded (the DMA writes
-// lane-linear); the 16-B chunk index is XOR-swizzled with (row>>2)&3 on the global source
-// and on the fragment read, which puts every ds_read_b128 lane group on 16 bank slots.
+//
+// Operand layout ("slab-blocked"): residue planes are stored as 256-row × 64-byte tiles,
+// each one contiguous 16 KB — element (row, k) of a plane with K columns lives at
+//   ((row/256)·(K/64) + k/64)·16384 + (row%256)·64 + k%64.
+// A K-slab of a 256-row operand panel is then ONE contiguous 16 KB read, and every 1 KB
+// LDS-DMA piece is contiguous: with row-major planes the same slab is 256 scattered 64-B
+// segments, one per DRAM page, and the L2-miss stream ran far below HBM bandwidth.
+//
+// 256×256 output tile per 512-thread workgroup: 8 waves as 2×4, two waves per SIMD, each
+// wave 128×64 = 8×4 tiles of v_mfma_i32_16x16x64_i8 (128 accumulators).  While one wave of
+// a SIMD issues its LDS-DMA pieces and fragment reads the other keeps the matrix core busy.
+// K advances in 64-byte slabs loaded global→LDS directly (global_load_lds_dwordx4) into a
+// 4-stage ring with three slabs in flight; one barrier per slab, between the slab's two MFMA
+// halves, publishes the next one.
+// Lane l reads A[row l&15][k 16(l>>4)..+15]; a ds_read_b128 lane group covers rows
+// {0-3,12-15} of one k-chunk and rows 4-11 of the next, so the LDS chunk index is swizzled
+// chunk ^ g((row>>2)&3) with g = [0,2,3,1], which spreads every group over 16 distinct
+// 4-bank slots.  The DMA writes LDS lane-linearly; the swizzle is applied on the global
+// source address (an involution, so the same formula maps both ways).
 constexpr int IBM = 256, IBN = 256, IBK = 64;
-constexpr int I_OP = IBM * IBK;        // bytes per operand per stage (16 KB)
+constexpr int I_OP = IBM * IBK;        // bytes per operand per stage (16 KB) = one layout tile
 constexpr int I_STAGE = 2 * I_OP;      // A then B
 constexpr int I_NSTAGE = 4;
 
 typedef int i4v __attribute__((ext_vector_type(4)));
-typedef int i16v __attribute__((ext_vector_type(16)));
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-__device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 2) & 3); }
+__device__ __forceinline__ int swz16(int row, int chunk) {
+  const int q = (row >> 2) & 3;
+  const int g = (0x78 >> (2 * q)) & 3;  // 0x78 = 0b01_11_10_00 → g(0)=0, g(1)=2, g(2)=3, g(3)=1
+  return chunk ^ g;
+}
 
 #define GP2D_VMWAIT_BARRIER(N) asm volatile("s_waitcnt vmcnt(" #N ")\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
 
-__global__ __launch_bounds__(256, 1) void igemm_nt_mod_kernel(const int8_t* __restrict__ A, int64_t lda,
-                                                              const int8_t* __restrict__ B, int64_t ldb,
+// A: M×K plane, B: N×K plane (both slab-blocked); C: column-major N×M bytes (ldc ≥ M).
+__global__ __launch_bounds__(512, 1) void igemm_nt_mod_kernel(const int8_t* __restrict__ A,
+                                                              const int8_t* __restrict__ B,
                                                               uint8_t* __restrict__ C, int64_t ldc, int M, int N,
-                                                              int K, int a_lower, int modulus, double inv_mod,
-                                                              int xcd_groups) {
+                                                              int K, int a_lower, int modulus, double inv_mod) {
   __shared__ __attribute__((aligned(16))) int8_t smem[I_NSTAGE * I_STAGE];
-  int bi, bj;
-  if (xcd_groups) {
-    // Blocks t and t+8 share an XCD.  Each XCD runs groups of 32 workgroups = 4 row blocks ×
-    // 8 column tiles, so one K-slab of 4 A panels + 8 B panels serves all 32 tiles.
-    const int nr = M / IBM, nc = N / IBN, ncg = nc / 8;
-    const int t = blockIdx.x, x = t & 7, q = t >> 3;
-    const int G = q >> 5, w = q & 31;
-    const int P = G * 8 + x;
-    const int rg = P / ncg, cg = P - rg * ncg;
-    bi = nr - 1 - (4 * rg + (w >> 3));   // heavy (long-K) row groups first
-    bj = 8 * cg + (w & 7);
-  } else {
-    bj = blockIdx.x;
-    bi = (int)(gridDim.y - 1 - blockIdx.y);   // heavy (long-K) row blocks first
-  }
-  const int i0 = bi * IBM, j0 = bj * IBN;
-  const int ke = a_lower ? min(K, i0 + IBM) : K;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = wid >> 1, wc = wid & 1;
-  const int lr = lane & 31, lh = lane >> 5;
-
-  i16v acc[4][4];
-#pragma unroll
-  for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = i16v{0};
-
-  // DMA mapping: wave wid fills rows [64·wid, 64·wid+64) of both operands, 16 rows per
-  // instruction (4 per operand per slab); lane l lands at row +l/4, physical chunk l%4.
-  const int drow = lane >> 2, dchunk = lane & 3;
-  auto issue = [&](int k0, int st) {
-#ifdef GP2D_IGEMM_NO_DMA
-    return;
-#endif
-    int8_t* As = smem + st * I_STAGE;
-    int8_t* Bs = As + I_OP;
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      const int row = wid * 64 + h * 16 + drow;
-      const int c = swz(row, dchunk);
-      __builtin_amdgcn_global_load_lds((const void*)(A + (int64_t)(i0 + row) * lda + k0 + 16 * c),
-                                       (lds_ptr_t)(As + (wid * 64 + h * 16) * IBK), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(B + (int64_t)(j0 + row) * ldb + k0 + 16 * c),
-                                       (lds_ptr_t)(Bs + (wid * 64 + h * 16) * IBK), 16, 0, 0);
-    }
-  };
-  // Fragment reads are inline-asm ds_read_b128 so that the waits are ours (counted
-  // lgkmcnt) rather than the compiler's conservative lgkmcnt(0) at the loop header; every
-  // wait is followed by sched_barrier(0) so no MFMA is hoisted above it.
-  const uint32_t lds_base = (uint32_t)(size_t)(lds_ptr_t)smem;
-  auto readf = [&](int st, int kc, i4v (&a)[4], i4v (&b)[4]) {
-    const uint32_t As = lds_base + st * I_STAGE;
-    const uint32_t Bs = As + I_OP;
-#pragma unroll
-    for (int mi = 0; mi < 4; ++mi) {
-      const int row = wr * 128 + mi * 32 + lr;
-      const uint32_t ad = As + row * IBK + 16 * swz(row, 2 * kc + lh);
-      asm volatile("ds_read_b128 %0, %1" : "=v"(a[mi]) : "v"(ad) : "memory");
-    }
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni) {
-      const int row = wc * 128 + ni * 32 + lr;
-      const uint32_t ad = Bs + row * IBK + 16 * swz(row, 2 * kc + lh);
-      asm volatile("ds_read_b128 %0, %1" : "=v"(b[ni]) : "v"(ad) : "memory");
-    }
-  };
-  auto mfmas = [&](const i4v (&a)[4], const i4v (&b)[4]) {
-#ifdef GP2D_IGEMM_NO_MFMA
-    acc[0][0][0] += a[0][0] ^ b[0][0];
-    return;
-#endif
-#pragma unroll
-    for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni)
-        acc[mi][ni] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
-  };
-  const int nsl = ke / IBK;   // ke is a multiple of 256
-  if (nsl > 0) {
-    // prologue: slabs 0..2 in flight, retire slab 0
-    issue(0, 0);
-    if (nsl > 1) issue(IBK, 1);
-    if (nsl > 2) issue(2 * IBK, 2);
-    if (nsl > 2) GP2D_VMWAIT_BARRIER(16);
-    else if (nsl > 1) GP2D_VMWAIT_BARRIER(8);
-    else GP2D_VMWAIT_BARRIER(0);
-    i4v a0[4], b0[4], a1[4], b1[4];
-    readf(0, 0, a0, b0);
-    __builtin_amdgcn_sched_barrier(0);
-    int st = 0;
-    for (int s = 0; s < nsl; ++s) {
-      int st3 = st + 3;
-      if (st3 >= I_NSTAGE) st3 -= I_NSTAGE;
-      if (s + 3 < nsl) issue((s + 3) * IBK, st3);   // buffer of slab s−1: free since the last barrier
-      readf(st, 1, a1, b1);
-      asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");  // a0, b0 (the older 8 reads) have landed
-      __builtin_amdgcn_sched_barrier(0);
-      mfmas(a0, b0);
-      __builtin_amdgcn_sched_barrier(0);
-      if (s + 1 < nsl) {
-        // publish slab s+1: this wave's DMAs for it are done (later slabs may stay in flight)
-        if (s + 3 < nsl) GP2D_VMWAIT_BARRIER(16);
-        else if (s + 2 < nsl) GP2D_VMWAIT_BARRIER(8);
-        else GP2D_VMWAIT_BARRIER(0);
-        int st1 = st + 1;
-        if (st1 >= I_NSTAGE) st1 -= I_NSTAGE;
-        readf(st1, 0, a0, b0);
-      }
-      else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      mfmas(a1, b1);   // a1, b1 completed at the barrier's lgkmcnt(0)
-      __builtin_amdgcn_sched_barrier(0);
-      st = (st + 1 == I_NSTAGE) ? 0 : st + 1;
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  }
-  // Epilogue: residues mod m (fp32 quotient estimate, exact int correction), packed 4 rows
-  // per dword into an LDS image of Cᵀ [col][row] (pitch 272 B), then written out as
-  // coalesced 16-B row runs of the column-major residue plane (ld = ldc rows).
-  uint8_t* T = reinterpret_cast<uint8_t*>(smem);
-  constexpr int TP = IBM + 16;
-  const float fim = (float)inv_mod;
-#pragma unroll
-  for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        uint32_t pk = 0;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int v = acc[mi][ni][4 * g + u];
-          const int q = (int)floorf((float)v * fim);     // off by at most one
-          int res = v - q * modulus;
-          res += (res < 0) ? modulus : 0;
-          res -= (res >= modulus) ? modulus : 0;
-          pk |= (uint32_t)res << (8 * u);
-        }
-        const int rloc = wr * 128 + mi * 32 + 8 * g + 4 * lh;
-        const int cloc = wc * 128 + ni * 32 + lr;
-        *reinterpret_cast<uint32_t*>(T + cloc * TP + rloc) = pk;
-      }
-  __syncthreads();
-#pragma unroll
-  for (int p = 0; p < (IBM * IBN / 16) / 256; ++p) {
-    const int id = tid + 256 * p;
-    const int cloc = id >> 4, ch = id & 15;
-    const uint4 v = *reinterpret_cast<const uint4*>(T + cloc * TP + 16 * ch);
-    *reinterpret_cast<uint4*>(C + (int64_t)(j0 + cloc) * ldc + i0 + 16 * ch) = v;
-  }
-}
-
-// Two waves per SIMD variant: 512 threads = 8 waves as 2×4, each wave 128×64 (4×2 tiles of
-// 32x32x32, 128 accumulators, ≤ 256 registers).  While one wave of a SIMD issues its LDS-DMA
-// pieces and fragment reads, the other keeps the matrix core busy — with one wave per SIMD
-// the issue cost of the DMA pieces stalls the MFMA stream.  Same LDS ring, swizzle, slab
-// pipeline and epilogue as igemm_nt_mod_kernel; each wave moves 4 DMA pieces per slab.
-__device__ __forceinline__ void igemm_tile_coords(int xcd_groups, int M, int N, int& bi, int& bj) {
-  if (xcd_groups) {
-    const int nr = M / IBM, nc = N / IBN, ncg = nc / 8;
-    const int t = blockIdx.x, x = t & 7, q = t >> 3;
-    const int G = q >> 5, w = q & 31;
-    const int P = G * 8 + x;
-    const int rg = P / ncg, cg = P - rg * ncg;
-    bi = nr - 1 - (4 * rg + (w >> 3));
-    bj = 8 * cg + (w & 7);
-  } else {
-    bj = blockIdx.x;
-    bi = (int)(gridDim.y - 1 - blockIdx.y);
-  }
-}
-
-__global__ __launch_bounds__(512, 1) void igemm_nt_mod_w8_kernel(const int8_t* __restrict__ A, int64_t lda,
-                                                                 const int8_t* __restrict__ B, int64_t ldb,
-                                                                 uint8_t* __restrict__ C, int64_t ldc, int M, int N,
-                                                                 int K, int a_lower, int modulus, double inv_mod,
-                                                                 int xcd_groups) {
-  __shared__ __attribute__((aligned(16))) int8_t smem[I_NSTAGE * I_STAGE];
-  int bi, bj;
-  igemm_tile_coords(xcd_groups, M, N, bi, bj);
+  const int bj = blockIdx.x;
+  const int bi = (int)(gridDim.y - 1 - blockIdx.y);   // heavy (long-K) row blocks first
   const int i0 = bi * IBM, j0 = bj * IBN;
   const int ke = a_lower ? min(K, i0 + IBM) : K;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 2, wc = wid & 3;
-  const int lr = lane & 31, lh = lane >> 5;
+  const int l16 = lane & 15, lq = lane >> 4;
+  const int64_t kslabs = K / IBK;
+  const int8_t* Ap = A + (int64_t)bi * kslabs * I_OP;   // this row block's slab tiles
+  const int8_t* Bp = B + (int64_t)bj * kslabs * I_OP;
 
-  i16v acc[4][2];
+  i4v acc[8][4];
 #pragma unroll
-  for (int mi = 0; mi < 4; ++mi)
+  for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
-    for (int ni = 0; ni < 2; ++ni) acc[mi][ni] = i16v{0};
+    for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = i4v{0, 0, 0, 0};
 
-  // wave wid fills rows [32·wid, 32·wid+32) of both operands: 2 pieces of 16 rows each
+  // wave w moves rows [32w, 32w+32) of both operands: 2 contiguous 1 KB pieces each
   const int drow = lane >> 2, dchunk = lane & 3;
-  auto issue = [&](int k0, int st) {
+  auto issue = [&](int s, int st) {
 #ifdef GP2D_IGEMM_NO_DMA
     return;
 #endif
     int8_t* As = smem + st * I_STAGE;
     int8_t* Bs = As + I_OP;
+    const int8_t* Ag = Ap + (int64_t)s * I_OP;
+    const int8_t* Bg = Bp + (int64_t)s * I_OP;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int row = wid * 32 + h * 16 + drow;
-      const int c = swz(row, dchunk);
-      __builtin_amdgcn_global_load_lds((const void*)(A + (int64_t)(i0 + row) * lda + k0 + 16 * c),
-                                       (lds_ptr_t)(As + (wid * 32 + h * 16) * IBK), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(B + (int64_t)(j0 + row) * ldb + k0 + 16 * c),
-                                       (lds_ptr_t)(Bs + (wid * 32 + h * 16) * IBK), 16, 0, 0);
+      const int off = row * IBK + 16 * swz16(row, dchunk);
+      __builtin_amdgcn_global_load_lds((const void*)(Ag + off), (lds_ptr_t)(As + (wid * 32 + h * 16) * IBK), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(Bg + off), (lds_ptr_t)(Bs + (wid * 32 + h * 16) * IBK), 16, 0, 0);
     }
   };
   const uint32_t lds_base = (uint32_t)(size_t)(lds_ptr_t)smem;
-  auto readf = [&](int st, int kc, i4v (&a)[4], i4v (&b)[2]) {
+  auto reada = [&](int st, int half, i4v (&a)[4]) {  // A fragments mi = 4·half .. 4·half+3
     const uint32_t As = lds_base + st * I_STAGE;
-    const uint32_t Bs = As + I_OP;
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi) {
-      const int row = wr * 128 + mi * 32 + lr;
-      const uint32_t ad = As + row * IBK + 16 * swz(row, 2 * kc + lh);
-      asm volatile("ds_read_b128 %0, %1" : "=v"(a[mi]) : "v"(ad) : "memory");
+    for (int u = 0; u < 4; ++u) {
+      const int row = wr * 128 + (4 * half + u) * 16 + l16;
+      const uint32_t ad = As + row * IBK + 16 * swz16(row, lq);
+      asm volatile("ds_read_b128 %0, %1" : "=v"(a[u]) : "v"(ad) : "memory");
     }
+  };
+  auto readb = [&](int st, i4v (&b)[4]) {
+    const uint32_t Bs = lds_base + st * I_STAGE + I_OP;
 #pragma unroll
-    for (int ni = 0; ni < 2; ++ni) {
-      const int row = wc * 64 + ni * 32 + lr;
-      const uint32_t ad = Bs + row * IBK + 16 * swz(row, 2 * kc + lh);
+    for (int ni = 0; ni < 4; ++ni) {
+      const int row = wc * 64 + ni * 16 + l16;
+      const uint32_t ad = Bs + row * IBK + 16 * swz16(row, lq);
       asm volatile("ds_read_b128 %0, %1" : "=v"(b[ni]) : "v"(ad) : "memory");
     }
   };
-  auto mfmas = [&](const i4v (&a)[4], const i4v (&b)[2]) {
+  auto mfmas = [&](int half, const i4v (&a)[4], const i4v (&b)[4]) {
 #ifdef GP2D_IGEMM_NO_MFMA
     acc[0][0][0] += a[0][0] ^ b[0][0];
     return;
 #endif
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi)
+    for (int u = 0; u < 4; ++u)
 #pragma unroll
-      for (int ni = 0; ni < 2; ++ni)
-        acc[mi][ni] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
+      for (int ni = 0; ni < 4; ++ni)
+        acc[4 * half + u][ni] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[u], b[ni], acc[4 * half + u][ni], 0, 0, 0);
   };
   const int nsl = ke / IBK;
   if (nsl > 0) {
     issue(0, 0);
-    if (nsl > 1) issue(IBK, 1);
-    if (nsl > 2) issue(2 * IBK, 2);
+    if (nsl > 1) issue(1, 1);
+    if (nsl > 2) issue(2, 2);
     if (nsl > 2) GP2D_VMWAIT_BARRIER(8);
     else if (nsl > 1) GP2D_VMWAIT_BARRIER(4);
     else GP2D_VMWAIT_BARRIER(0);
-    i4v a0[4], b0[2], a1[4], b1[2];
-    readf(0, 0, a0, b0);
+    // Per slab: MFMA half 0 (A rows 0-63 of the wave) → barrier publishing slab s+1 → reads
+    // of slab s+1's B and A-half-0 fragments into the other register set → MFMA half 1.
+    // Both waves of a SIMD leave the barrier together, so the next slab's first fragments
+    // must already be in flight behind half 1's 16 MFMAs rather than be read after it.
+    i4v bA[4], a0A[4], bB[4], a0B[4], a1[4];
+    readb(0, bA);
+    reada(0, 0, a0A);
     __builtin_amdgcn_sched_barrier(0);
     int st = 0;
-    for (int s = 0; s < nsl; ++s) {
+    auto step = [&](int s, i4v (&b)[4], i4v (&a0)[4], i4v (&bn)[4], i4v (&a0n)[4]) {
       int st3 = st + 3;
       if (st3 >= I_NSTAGE) st3 -= I_NSTAGE;
-      if (s + 3 < nsl) issue((s + 3) * IBK, st3);
-      readf(st, 1, a1, b1);
-      asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory");
+      if (s + 3 < nsl) issue(s + 3, st3);   // buffer of slab s−1: free since the last barrier
+      reada(st, 1, a1);
+      asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");  // b, a0 landed
       __builtin_amdgcn_sched_barrier(0);
-      mfmas(a0, b0);
+      mfmas(0, a0, b);
       __builtin_amdgcn_sched_barrier(0);
       if (s + 1 < nsl) {
+        // publish slab s+1 (waits for a1 as well: lgkmcnt(0) inside)
         if (s + 3 < nsl) GP2D_VMWAIT_BARRIER(8);
         else if (s + 2 < nsl) GP2D_VMWAIT_BARRIER(4);
         else GP2D_VMWAIT_BARRIER(0);
         int st1 = st + 1;
         if (st1 >= I_NSTAGE) st1 -= I_NSTAGE;
-        readf(st1, 0, a0, b0);
+        readb(st1, bn);
+        reada(st1, 0, a0n);
+        asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");  // nothing older than the 8 new reads
+      } else {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       }
-      else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
-      mfmas(a1, b1);
+      mfmas(1, a1, b);
       __builtin_amdgcn_sched_barrier(0);
       st = (st + 1 == I_NSTAGE) ? 0 : st + 1;
+    };
+    for (int s = 0; s < nsl; s += 2) {
+      step(s, bA, a0A, bB, a0B);
+      if (s + 1 < nsl) step(s + 1, bB, a0B, bA, a0A);
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
+  // Epilogue: residues mod m (fp32 quotient estimate, exact int correction), packed 4 rows
+  // per dword into an LDS image of Cᵀ [col][row] (pitch 272 B), then written out as
+  // coalesced 16-B row runs of the column-major residue plane.
   uint8_t* T = reinterpret_cast<uint8_t*>(smem);
   constexpr int TP = IBM + 16;
   const float fim = (float)inv_mod;
 #pragma unroll
-  for (int mi = 0; mi < 4; ++mi)
+  for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
-    for (int ni = 0; ni < 2; ++ni)
+    for (int ni = 0; ni < 4; ++ni) {
+      uint32_t pk = 0;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        uint32_t pk = 0;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int v = acc[mi][ni][4 * g + u];
-          const int q = (int)floorf((float)v * fim);
-          int res = v - q * modulus;
-          res += (res < 0) ? modulus : 0;
-          res -= (res >= modulus) ? modulus : 0;
-          pk |= (uint32_t)res << (8 * u);
-        }
-        const int rloc = wr * 128 + mi * 32 + 8 * g + 4 * lh;
-        const int cloc = wc * 64 + ni * 32 + lr;
-        *reinterpret_cast<uint32_t*>(T + cloc * TP + rloc) = pk;
+      for (int u = 0; u < 4; ++u) {
+        const int v = acc[mi][ni][u];
+        const int q = (int)floorf((float)v * fim);     // off by at most one
+        int res = v - q * modulus;
+        res += (res < 0) ? modulus : 0;
+        res -= (res >= modulus) ? modulus : 0;
+        pk |= (uint32_t)res << (8 * u);
       }
+      const int rloc = wr * 128 + mi * 16 + 4 * lq;
+      const int cloc = wc * 64 + ni * 16 + l16;
+      *reinterpret_cast<uint32_t*>(T + cloc * TP + rloc) = pk;
+    }
   __syncthreads();
 #pragma unroll
   for (int p = 0; p < (IBM * IBN / 16) / 512; ++p) {

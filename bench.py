@@ -178,7 +178,7 @@ def main():
         nmod = int(pred_cache["p"].gp.extra["ozaki"][2])
         roof = {"bound": "mfma", "achieved": achieved * nmod if achieved else None, "peak": INT8_PEAK_TOPS,
                 "unit": "TOP/s (int8)", "frac": (achieved * nmod / INT8_PEAK_TOPS) if achieved else None,
-                "traffic": traffic, "kernel": f"igemm_nt_mod_w8_kernel x{nmod} moduli (Ozaki-II variance, exact)",
+                "traffic": traffic, "kernel": f"igemm_nt_mod_kernel x{nmod} moduli (Ozaki-II variance, exact)",
                 "launches": klaunch * nmod, "avg_launch_ms": (kms / klaunch / nmod) if klaunch else None,
                 "ops_per_launch": (kflops / klaunch) if klaunch else None,
                 "fp64_equivalent_tflops": achieved, "fp64_equivalent_frac_of_fp64_peak":
