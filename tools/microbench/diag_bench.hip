@@ -7,6 +7,106 @@ __device__ unsigned long long g_stamps[16];
 #include <cmath>
 namespace gp2d { void set_error(const std::string&) {} }
 using namespace gp2d;
+
+// The previous register-resident diagonal kernel (one workgroup barrier per pivot), kept
+// here as the comparison point for potrf_diag_kernel.
+__global__ __launch_bounds__(256) void potrf_diag_reg_kernel(double* __restrict__ A, int64_t lda, int k0,
+                                                             double* __restrict__ dinv, int* info) {
+  __shared__ double Ls[NB * DSP];
+  __shared__ double buf[2 * NB];
+  __shared__ double rdiag[NB];
+  const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
+  double* Ab = A + (int64_t)k0 * lda + k0;
+  double r[8][8];
+  GP2D_STAMP(0);
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const int i = ty + 16 * a, k = tx + 16 * b;
+      const double t = Ab[(int64_t)i * lda + k];  // unconditional: loads issue back-to-back
+      r[a][b] = (k <= i) ? t : 0.0;
+    }
+  GP2D_STAMP(1);
+  // right-looking Cholesky: column j is published by its owner lanes (tx == j & 15)
+#pragma unroll
+  for (int jb = 0; jb < 8; ++jb)
+  for (int jt = 0; jt < 16; ++jt) {
+    const int j = 16 * jb + jt;
+    double* cb = buf + (j & 1) * NB;
+    if (tx == jt) {
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        if (b != jb) continue;
+#pragma unroll
+        for (int a = 0; a < 8; ++a) cb[ty + 16 * a] = r[a][b];
+      }
+    }
+    __syncthreads();
+    const double d = cb[j];
+    const double rd = sqrt(d);
+    const double ird = 1.0 / rd;
+    if (tid == 0 && !(d > 0.0) && info) atomicCAS(info, 0, k0 + j + 1);
+    double li[8], lk[8];
+#pragma unroll
+    for (int a = 0; a < 8; ++a) li[a] = cb[ty + 16 * a] * ird;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) lk[b] = cb[tx + 16 * b] * ird;
+#pragma unroll
+    for (int a = 0; a < 8; ++a) {
+      if (a < jb) continue;
+      const int i = ty + 16 * a;
+#pragma unroll
+      for (int b = 0; b <= a; ++b) {
+        if (b < jb) continue;
+        if (b > jb && b < a) {  // interior block: j < k < i for every lane
+          r[a][b] = fma(-li[a], lk[b], r[a][b]);
+        } else {
+          const int k = tx + 16 * b;
+          const double nv = fma(-li[a], lk[b], r[a][b]);
+          r[a][b] = (k > j && k <= i) ? nv : r[a][b];
+        }
+      }
+    }
+    if (tx == jt) {
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        if (b != jb) continue;
+#pragma unroll
+        for (int a = 0; a < 8; ++a) {
+          const int i = ty + 16 * a;
+          r[a][b] = (i > j) ? li[a] : ((i == j) ? rd : r[a][b]);
+        }
+      }
+    }
+  }
+  GP2D_STAMP(2);
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const int i = ty + 16 * a, k = tx + 16 * b;
+      const double v = (k <= i) ? r[a][b] : 0.0;
+      Ab[(int64_t)i * lda + k] = v;
+      Ls[i * DSP + k] = v;
+    }
+  __syncthreads();
+  GP2D_STAMP(3);
+  reg_trtri_lower(Ls, r, buf, rdiag, tid);
+  GP2D_STAMP(4);
+  if (dinv) {
+    double* D = dinv + (int64_t)(k0 / NB) * NB * NB;
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        const int i = ty + 16 * a, k = tx + 16 * b;
+        D[i * NB + k] = (k <= i) ? r[a][b] : 0.0;
+      }
+  }
+}
+
+
 __global__ void noop_kernel(double* p) { if (threadIdx.x == 9999) p[0] = 1; }
 __global__ __launch_bounds__(256) void barrier_only(double* p) {
   __shared__ double S[128];
