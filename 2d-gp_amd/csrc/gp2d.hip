@@ -138,6 +138,7 @@ static int make_ozaki_consts(int nmod, const gp2d_kernel_t* k, OzakiConsts& oc) 
   }
   const double bmax = kstar_bound(k);
   oc.sB = OZ_P - 1 - (int)std::ceil(std::log2(bmax));
+  oc.vlimit = 4.0 * std::sqrt(gp2d_kernel_diag(k));
   return 0;
 }
 
@@ -436,16 +437,33 @@ int gp2d_ozaki_prepare(const double* W, int64_t n, int64_t ldw, const gp2d_kerne
   double* l1 = reinterpret_cast<double*>(wres);  // scratch: the planes are written afterwards
   ozaki_w_scale_kernel<<<(unsigned)n, 256, 0, s>>>(W, n, ldw, rowscale, l1);
   GP2D_CHECK(check_launch("ozaki_w_scale_kernel"));
-  std::vector<double> hl1((size_t)n);
+  std::vector<double> hl1((size_t)n), hs((size_t)n);
   if (hipMemcpyAsync(hl1.data(), l1, sizeof(double) * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipMemcpyAsync(hs.data(), rowscale, sizeof(double) * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
       hipStreamSynchronize(s) != hipSuccess) {
     set_error("ozaki: reading the row bounds failed");
     return -1;
   }
-  double mx = 0.0;
-  for (double v : hl1) mx = std::max(mx, v);
-  // |Pint_ij| ≤ l1_i · 2^{p−1}; the fp64 row sums carry ≤ n·2^-53 relative error → 1 % margin
-  const int nmod = ozaki_nmod_bits(std::log2(std::max(mx, 1.0) * 1.01) + (OZ_P - 1));
+  // Bound on |Pint_ij| = |Σ_k Wint_ik·Bint_kj| per row i, the smaller of
+  //   (a) ‖Wint_i‖₁ · max|Bint|  ≤ l1_i · 2^{p−1}                       (always valid), and
+  //   (b) 2^{s_i+s_B}·|V_ij| + rounding terms, with |V_ij| ≤ ‖V_j‖₂ ≤ √kss (the posterior
+  //       variance kss − ‖V_j‖² is ≥ 0; factor 2 of slack), rounding ≤ n·2^{p−2} + l1_i + n.
+  // (b) is ≈ 5 bits tighter on the rows of L⁻¹; the identity rows of padded points take (a).
+  // A violated bound cannot pass silently: the CRT kernel poisons columns with |V| > 4√kss.
+  int sB = 0;
+  {
+    OzakiConsts probe;
+    GP2D_CHECK(make_ozaki_consts(1, k, probe));
+    sB = probe.sB;
+  }
+  const double sq = 2.0 * std::sqrt(gp2d_kernel_diag(k));
+  double bmax = 1.0;
+  for (int64_t i = 0; i < n; ++i) {
+    const double a = std::ldexp(hl1[i] * 1.01, OZ_P - 1);
+    const double b = std::ldexp(sq, (int)hs[i] + sB) + std::ldexp((double)n, OZ_P - 2) + hl1[i] + (double)n;
+    bmax = std::max(bmax, std::min(a, b));
+  }
+  const int nmod = ozaki_nmod_bits(std::log2(bmax));
   GP2D_REQUIRE(nmod > 0, "ozaki: row bound exceeds the modulus table");
   OzakiConsts oc;
   GP2D_CHECK(make_ozaki_consts(nmod, k, oc));

@@ -34,6 +34,7 @@ struct OzakiConsts {
   double t[OZ_MAXMOD];             // inv_l / m_l − h_l
   double M;                        // Π m_l (rounded)
   int sB;                          // K* scale exponent
+  double vlimit;                   // |V_ij| above this means the CRT range was exceeded
 };
 
 // residue of an exact integer x (|x| < 2^53) modulo m, centred into [−128, 127]
@@ -434,6 +435,9 @@ __global__ __launch_bounds__(256) void ozaki_crt_colsq_kernel(const uint8_t* __r
       const double f = (H[c] - rint(H[c])) + T[c];   // Pint / M, centred
       const double vij = f * rowscale[i0 + c];
       acc = fma(vij, vij, acc);
+      // |V_ij| ≤ ‖V_j‖₂ ≤ √kss: a value past the limit can only come from a CRT wrap-around
+      // (|Pint| ≥ M/2, i.e. too few moduli) — poison the column instead of returning garbage
+      if (fabs(vij) > oc.vlimit) acc = __builtin_nan("");
     }
   }
 #pragma unroll

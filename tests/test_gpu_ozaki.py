@@ -75,3 +75,21 @@ def test_ozaki_sharding_bit_identical():
         shards_v.append((lo, hi, vv.cpu().numpy()))
     assert np.array_equal(assemble_from_shards(xg.shape[0], 2, shards_v), v_all)
     assert np.array_equal(assemble_from_shards(xg.shape[0], 2, shards_m), m_all)
+
+
+def test_ozaki_too_few_moduli_poisons_instead_of_wrapping():
+    """A CRT range overflow (too few moduli) must not return plausible numbers: the
+    reconstruction kernel flags |V_ij| > 4·sqrt(kss) and the column's variance becomes NaN."""
+    x, y = tracks(300, 3)
+    rng = np.random.default_rng(4)
+    xg = np.stack([rng.uniform(0, 60, 500), rng.uniform(0, 45, 500)], 1)
+    gp = E.fit(E.KernelSpec(kind="df", l_df=5.0), x, y, noise=0.0025, variance="ozaki")
+    wres, rowscale, nmod = gp.extra["ozaki"]
+    assert nmod >= 12
+    mu_ok, var_ok = E.predict(gp, xg)
+    assert np.isfinite(var_ok.cpu().numpy()).all()
+    gp.extra["ozaki"] = (wres, rowscale, 6)   # ≈ 47 bits of CRT range for ≈ 100-bit products
+    mu, var = E.predict(gp, xg)
+    v = var.cpu().numpy()
+    assert np.isnan(v).mean() > 0.5
+    np.testing.assert_array_equal(mu.cpu().numpy(), mu_ok.cpu().numpy())  # the mean path is separate
