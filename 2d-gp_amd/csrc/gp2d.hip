@@ -213,12 +213,10 @@ int launch_panel(double* A, int64_t lda, int k, int64_t n, const double* dinv, h
   const int rows = (int)(n - k0 - NB);
   if (rows <= 0) return 0;
   // in-place panel TRSM  L21 = A21 · inv(L11)ᵀ
-  GemmParams p = gemm_params();
-  p.A = A + (int64_t)(k0 + NB) * lda + k0; p.lda = lda;
-  p.B = dinv + (int64_t)k * NB * NB; p.ldb = NB;
-  p.C = A + (int64_t)(k0 + NB) * lda + k0; p.ldc = lda;
-  p.M = rows; p.N = NB; p.K = NB;
-  return launch_gemm<true, EPI_STORE>(p, 1, s);
+  double* P = A + (int64_t)(k0 + NB) * lda + k0;
+  gemm_f64_panel_kernel<<<(unsigned)(rows / PNL_R), 256, 0, s>>>(P, lda, dinv + (int64_t)k * NB * NB, NB, P, lda,
+                                                                1.0, 0.0);
+  return check_launch("gemm_f64_panel_kernel");
 }
 }  // namespace
 
@@ -244,13 +242,10 @@ int gp2d_potrf(double* A, int64_t n, int64_t lda, double* dinv, int* info_dev, v
     const int k0 = k * NB, k1 = k0 + NB;
     const double* Lk = A + (int64_t)k1 * lda + k0;     // panel k, rows ≥ k+1
     // (1) update block column k+1:  A[k+1.., k+1] −= L[k+1.., k] · L[k+1, k]ᵀ
-    GemmParams c = gemm_params();
-    c.A = Lk; c.lda = lda;
-    c.B = Lk; c.ldb = lda;                              // rows of block k+1 = first NB rows of the panel
-    c.C = A + (int64_t)k1 * lda + k1; c.ldc = lda;
-    c.M = (int)(n - k1); c.N = NB; c.K = NB;
-    c.alpha = -1.0; c.beta = 1.0;
-    GP2D_CHECK((launch_gemm<true, EPI_STORE>(c, 1, s)));
+    //     (B = rows of block k+1 = the first NB rows of the panel)
+    gemm_f64_panel_kernel<<<(unsigned)((n - k1) / PNL_R), 256, 0, s>>>(Lk, lda, Lk, lda, A + (int64_t)k1 * lda + k1,
+                                                                       lda, -1.0, 1.0);
+    GP2D_CHECK(check_launch("gemm_f64_panel_kernel"));
     if (hipEventRecord(e_col, s) != hipSuccess) { set_error("hipEventRecord failed"); return -1; }
     // (2) side stream: factor diagonal block k+1 and its panel
     if (hipStreamWaitEvent(s2, e_col, 0) != hipSuccess) { set_error("hipStreamWaitEvent failed"); return -1; }

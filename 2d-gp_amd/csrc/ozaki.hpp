@@ -241,7 +241,11 @@ __device__ __forceinline__ int swz16(int row, int chunk) {
   return chunk ^ g;
 }
 
+#if defined(GP2D_IGEMM_NO_DMA) && defined(GP2D_IGEMM_NO_BARRIER)  // dev timing only: no DMA, no data hazard
+#define GP2D_VMWAIT_BARRIER(N) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+#else
 #define GP2D_VMWAIT_BARRIER(N) asm volatile("s_waitcnt vmcnt(" #N ")\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
+#endif
 
 // A: M×K plane, B: N×K plane (both slab-blocked); C: column-major N×M bytes (ldc ≥ M).
 __global__ __launch_bounds__(512, 1) void igemm_nt_mod_kernel(const int8_t* __restrict__ A,
@@ -286,6 +290,9 @@ __global__ __launch_bounds__(512, 1) void igemm_nt_mod_kernel(const int8_t* __re
   };
   const uint32_t lds_base = (uint32_t)(size_t)(lds_ptr_t)smem;
   auto reada = [&](int st, int half, i4v (&a)[4]) {  // A fragments mi = 4·half .. 4·half+3
+#ifdef GP2D_IGEMM_NO_LDSREAD
+    return;
+#endif
     const uint32_t As = lds_base + st * I_STAGE;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -295,6 +302,9 @@ __global__ __launch_bounds__(512, 1) void igemm_nt_mod_kernel(const int8_t* __re
     }
   };
   auto readb = [&](int st, i4v (&b)[4]) {
+#ifdef GP2D_IGEMM_NO_LDSREAD
+    return;
+#endif
     const uint32_t Bs = lds_base + st * I_STAGE + I_OP;
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) {
@@ -314,7 +324,11 @@ __global__ __launch_bounds__(512, 1) void igemm_nt_mod_kernel(const int8_t* __re
       for (int ni = 0; ni < 4; ++ni)
         acc[4 * half + u][ni] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[u], b[ni], acc[4 * half + u][ni], 0, 0, 0);
   };
+#ifdef GP2D_IGEMM_EPI_ONLY
+  const int nsl = 0;
+#else
   const int nsl = ke / IBK;
+#endif
   if (nsl > 0) {
     issue(0, 0);
     if (nsl > 1) issue(1, 1);
@@ -327,6 +341,10 @@ __global__ __launch_bounds__(512, 1) void igemm_nt_mod_kernel(const int8_t* __re
     // Both waves of a SIMD leave the barrier together, so the next slab's first fragments
     // must already be in flight behind half 1's 16 MFMAs rather than be read after it.
     i4v bA[4], a0A[4], bB[4], a0B[4], a1[4];
+#ifdef GP2D_IGEMM_NO_LDSREAD
+#pragma unroll
+    for (int u = 0; u < 4; ++u) bA[u] = a0A[u] = bB[u] = a0B[u] = a1[u] = i4v{lane, u, wid, 1};
+#endif
     readb(0, bA);
     reada(0, 0, a0A);
     __builtin_amdgcn_sched_barrier(0);
