@@ -17,6 +17,7 @@
 //      2^-p scaling error; the squares are summed per column in a fixed order.
 // Parity is gated by the same 1e-10 tests as the FP64 path (tests/test_gpu_ozaki.py).
 #pragma once
+#include <type_traits>
 #include "common.hpp"
 #include "assemble.hpp"
 
@@ -331,11 +332,9 @@ __global__ __launch_bounds__(512, 1) void igemm_nt_mod_kernel(const int8_t* __re
 #endif
   if (nsl > 0) {
     issue(0, 0);
-    if (nsl > 1) issue(1, 1);
-    if (nsl > 2) issue(2, 2);
-    if (nsl > 2) GP2D_VMWAIT_BARRIER(8);
-    else if (nsl > 1) GP2D_VMWAIT_BARRIER(4);
-    else GP2D_VMWAIT_BARRIER(0);
+    issue(1, 1);
+    issue(2, 2);
+    GP2D_VMWAIT_BARRIER(8);   // slab 0 landed (nsl ≥ 4)
     // Per slab: MFMA half 0 (A rows 0-63 of the wave) → barrier publishing slab s+1 → reads
     // of slab s+1's B and A-half-0 fragments into the other register set → MFMA half 1.
     // Both waves of a SIMD leave the barrier together, so the next slab's first fragments
@@ -348,23 +347,26 @@ __global__ __launch_bounds__(512, 1) void igemm_nt_mod_kernel(const int8_t* __re
     readb(0, bA);
     reada(0, 0, a0A);
     __builtin_amdgcn_sched_barrier(0);
-    int st = 0;
-    auto step = [&](int s, i4v (&b)[4], i4v (&a0)[4], i4v (&bn)[4], i4v (&a0n)[4]) {
-      int st3 = st + 3;
-      if (st3 >= I_NSTAGE) st3 -= I_NSTAGE;
-      if (s + 3 < nsl) issue(s + 3, st3);   // buffer of slab s−1: free since the last barrier
+    // Step kinds: FULL (issue slab s+3, publish s+1 leaving s+2, s+3 in flight), then the
+    // tail: NODMA4 (publish s+1, s+2 in flight), NODMA0 (publish s+1), LAST (no barrier).
+    // The steady-state loop runs only FULL steps, unrolled by two for the register ping-pong,
+    // so it carries no per-slab branches; the ring stage is s & 3.
+    enum { FULL = 0, NODMA4 = 1, NODMA0 = 2, LAST = 3 };
+    auto step = [&](auto kind_c, int s, i4v (&b)[4], i4v (&a0)[4], i4v (&bn)[4], i4v (&a0n)[4]) {
+      constexpr int kind = decltype(kind_c)::value;
+      const int st = s & 3;
+      if constexpr (kind == FULL) issue(s + 3, (s + 3) & 3);   // stage of slab s−1: free since the last barrier
       reada(st, 1, a1);
       asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");  // b, a0 landed
       __builtin_amdgcn_sched_barrier(0);
       mfmas(0, a0, b);
       __builtin_amdgcn_sched_barrier(0);
-      if (s + 1 < nsl) {
+      if constexpr (kind != LAST) {
         // publish slab s+1 (waits for a1 as well: lgkmcnt(0) inside)
-        if (s + 3 < nsl) GP2D_VMWAIT_BARRIER(8);
-        else if (s + 2 < nsl) GP2D_VMWAIT_BARRIER(4);
+        if constexpr (kind == FULL) GP2D_VMWAIT_BARRIER(8);
+        else if constexpr (kind == NODMA4) GP2D_VMWAIT_BARRIER(4);
         else GP2D_VMWAIT_BARRIER(0);
-        int st1 = st + 1;
-        if (st1 >= I_NSTAGE) st1 -= I_NSTAGE;
+        const int st1 = (s + 1) & 3;
         readb(st1, bn);
         reada(st1, 0, a0n);
         asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");  // nothing older than the 8 new reads
@@ -374,12 +376,30 @@ __global__ __launch_bounds__(512, 1) void igemm_nt_mod_kernel(const int8_t* __re
       __builtin_amdgcn_sched_barrier(0);
       mfmas(1, a1, b);
       __builtin_amdgcn_sched_barrier(0);
-      st = (st + 1 == I_NSTAGE) ? 0 : st + 1;
     };
-    for (int s = 0; s < nsl; s += 2) {
-      step(s, bA, a0A, bB, a0B);
-      if (s + 1 < nsl) step(s + 1, bB, a0B, bA, a0A);
+    using K_FULL = std::integral_constant<int, FULL>;
+    using K_N4 = std::integral_constant<int, NODMA4>;
+    using K_N0 = std::integral_constant<int, NODMA0>;
+    using K_LAST = std::integral_constant<int, LAST>;
+    // nsl ≥ 4 (ke is a multiple of 256): steps 0 .. nsl−4 are FULL, then the three tail steps
+    const int m = nsl - 3;
+    int s = 0;
+    for (; s + 1 < m; s += 2) {
+      step(K_FULL{}, s, bA, a0A, bB, a0B);
+      step(K_FULL{}, s + 1, bB, a0B, bA, a0A);
     }
+    if (s < m) {   // odd number of FULL steps: one more, then move its fragments back to set A
+      step(K_FULL{}, s, bA, a0A, bB, a0B);
+      ++s;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        bA[u] = bB[u];
+        a0A[u] = a0B[u];
+      }
+    }
+    step(K_N4{}, s, bA, a0A, bB, a0B);
+    step(K_N0{}, s + 1, bB, a0B, bA, a0A);
+    step(K_LAST{}, s + 2, bA, a0A, bB, a0B);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
   // Epilogue: residues mod m (fp32 quotient estimate, exact int correction), packed 4 rows
