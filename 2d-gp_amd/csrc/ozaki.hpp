@@ -231,7 +231,11 @@ __global__ __launch_bounds__(256) void ozaki_kstar_kernel(
 constexpr int IBM = 256, IBN = 256, IBK = 64;
 constexpr int I_OP = IBM * IBK;        // bytes per operand per stage (16 KB) = one layout tile
 constexpr int I_STAGE = 2 * I_OP;      // A then B
-constexpr int I_NSTAGE = 4;
+#ifndef GP2D_IGEMM_NSTAGE
+#define GP2D_IGEMM_NSTAGE 4
+#endif
+constexpr int I_NSTAGE = GP2D_IGEMM_NSTAGE;   // ring stages; I_NSTAGE − 1 slabs in flight
+static_assert(I_NSTAGE == 4 || I_NSTAGE == 5, "ring depth 4 or 5 (the tail is written out for both)");
 
 typedef int i4v __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -242,11 +246,20 @@ __device__ __forceinline__ int swz16(int row, int chunk) {
   return chunk ^ g;
 }
 
-#if defined(GP2D_IGEMM_NO_DMA) && defined(GP2D_IGEMM_NO_BARRIER)  // dev timing only: no DMA, no data hazard
-#define GP2D_VMWAIT_BARRIER(N) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+// s_waitcnt vmcnt(4·W) + lgkmcnt(0) + s_barrier: this wave's LDS-DMA pieces of all but the
+// W youngest slabs (4 pieces per slab per wave) have landed, then the workgroup syncs.
+template <int W>
+__device__ __forceinline__ void vmwait_barrier(std::integral_constant<int, W>) {
+#if defined(GP2D_IGEMM_NO_DMA) && defined(GP2D_IGEMM_NO_BARRIER)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #else
-#define GP2D_VMWAIT_BARRIER(N) asm volatile("s_waitcnt vmcnt(" #N ")\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
+  if constexpr (W == 0) asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else if constexpr (W == 1) asm volatile("s_waitcnt vmcnt(4)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else if constexpr (W == 2) asm volatile("s_waitcnt vmcnt(8)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else if constexpr (W == 3) asm volatile("s_waitcnt vmcnt(12)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 #endif
+}
+
 
 // A: M×K plane, B: N×K plane (both slab-blocked); C: column-major N×M bytes (ldc ≥ M).
 __global__ __launch_bounds__(512, 1) void igemm_nt_mod_kernel(const int8_t* __restrict__ A,
@@ -331,10 +344,9 @@ __global__ __launch_bounds__(512, 1) void igemm_nt_mod_kernel(const int8_t* __re
   const int nsl = ke / IBK;
 #endif
   if (nsl > 0) {
-    issue(0, 0);
-    issue(1, 1);
-    issue(2, 2);
-    GP2D_VMWAIT_BARRIER(8);   // slab 0 landed (nsl ≥ 4)
+#pragma unroll
+    for (int q = 0; q < I_NSTAGE - 1; ++q) issue(q, q);
+    vmwait_barrier(std::integral_constant<int, I_NSTAGE - 2>{});   // slab 0 landed (nsl ≥ 4 ≥ I_NSTAGE − 1)
     // Per slab: MFMA half 0 (A rows 0-63 of the wave) → barrier publishing slab s+1 → reads
     // of slab s+1's B and A-half-0 fragments into the other register set → MFMA half 1.
     // Both waves of a SIMD leave the barrier together, so the next slab's first fragments
@@ -347,26 +359,25 @@ __global__ __launch_bounds__(512, 1) void igemm_nt_mod_kernel(const int8_t* __re
     readb(0, bA);
     reada(0, 0, a0A);
     __builtin_amdgcn_sched_barrier(0);
-    // Step kinds: FULL (issue slab s+3, publish s+1 leaving s+2, s+3 in flight), then the
-    // tail: NODMA4 (publish s+1, s+2 in flight), NODMA0 (publish s+1), LAST (no barrier).
-    // The steady-state loop runs only FULL steps, unrolled by two for the register ping-pong,
-    // so it carries no per-slab branches; the ring stage is s & 3.
-    enum { FULL = 0, NODMA4 = 1, NODMA0 = 2, LAST = 3 };
-    auto step = [&](auto kind_c, int s, i4v (&b)[4], i4v (&a0)[4], i4v (&bn)[4], i4v (&a0n)[4]) {
-      constexpr int kind = decltype(kind_c)::value;
-      const int st = s & 3;
-      if constexpr (kind == FULL) issue(s + 3, (s + 3) & 3);   // stage of slab s−1: free since the last barrier
+    // Step kinds: FULL steps issue slab s + I_NSTAGE − 1 and publish s+1 leaving the younger
+    // I_NSTAGE − 2 slabs in flight; the tail steps issue nothing and leave W = I_NSTAGE−3 .. 0
+    // slabs in flight; the LAST step has no barrier.  The steady-state loop runs only FULL
+    // steps, unrolled by two for the register ping-pong, so it carries no per-slab branches.
+    constexpr int LAST = -1;
+    auto step = [&](auto dma_c, auto w_c, int s, i4v (&b)[4], i4v (&a0)[4], i4v (&bn)[4], i4v (&a0n)[4]) {
+      constexpr bool dma = decltype(dma_c)::value;
+      constexpr int w = decltype(w_c)::value;
+      const int st = s % I_NSTAGE;
+      // the stage written is slab s−1's: nobody reads it after the previous barrier
+      if constexpr (dma) issue(s + I_NSTAGE - 1, (s + I_NSTAGE - 1) % I_NSTAGE);
       reada(st, 1, a1);
       asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");  // b, a0 landed
       __builtin_amdgcn_sched_barrier(0);
       mfmas(0, a0, b);
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (kind != LAST) {
-        // publish slab s+1 (waits for a1 as well: lgkmcnt(0) inside)
-        if constexpr (kind == FULL) GP2D_VMWAIT_BARRIER(8);
-        else if constexpr (kind == NODMA4) GP2D_VMWAIT_BARRIER(4);
-        else GP2D_VMWAIT_BARRIER(0);
-        const int st1 = (s + 1) & 3;
+      if constexpr (w != LAST) {
+        vmwait_barrier(w_c);   // publish slab s+1 (lgkmcnt(0) inside: a1 landed)
+        const int st1 = (s + 1) % I_NSTAGE;
         readb(st1, bn);
         reada(st1, 0, a0n);
         asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");  // nothing older than the 8 new reads
@@ -377,19 +388,17 @@ __global__ __launch_bounds__(512, 1) void igemm_nt_mod_kernel(const int8_t* __re
       mfmas(1, a1, b);
       __builtin_amdgcn_sched_barrier(0);
     };
-    using K_FULL = std::integral_constant<int, FULL>;
-    using K_N4 = std::integral_constant<int, NODMA4>;
-    using K_N0 = std::integral_constant<int, NODMA0>;
-    using K_LAST = std::integral_constant<int, LAST>;
-    // nsl ≥ 4 (ke is a multiple of 256): steps 0 .. nsl−4 are FULL, then the three tail steps
-    const int m = nsl - 3;
+    using T_ = std::true_type;
+    using F_ = std::false_type;
+    using W_FULL = std::integral_constant<int, I_NSTAGE - 2>;
+    const int m = nsl - (I_NSTAGE - 1);   // FULL steps
     int s = 0;
     for (; s + 1 < m; s += 2) {
-      step(K_FULL{}, s, bA, a0A, bB, a0B);
-      step(K_FULL{}, s + 1, bB, a0B, bA, a0A);
+      step(T_{}, W_FULL{}, s, bA, a0A, bB, a0B);
+      step(T_{}, W_FULL{}, s + 1, bB, a0B, bA, a0A);
     }
     if (s < m) {   // odd number of FULL steps: one more, then move its fragments back to set A
-      step(K_FULL{}, s, bA, a0A, bB, a0B);
+      step(T_{}, W_FULL{}, s, bA, a0A, bB, a0B);
       ++s;
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -397,9 +406,17 @@ __global__ __launch_bounds__(512, 1) void igemm_nt_mod_kernel(const int8_t* __re
         a0A[u] = a0B[u];
       }
     }
-    step(K_N4{}, s, bA, a0A, bB, a0B);
-    step(K_N0{}, s + 1, bB, a0B, bA, a0A);
-    step(K_LAST{}, s + 2, bA, a0A, bB, a0B);
+    // tail: I_NSTAGE − 1 steps, W = I_NSTAGE−3, ..., 0, then LAST
+    if constexpr (I_NSTAGE == 5) {
+      step(F_{}, std::integral_constant<int, 2>{}, s, bA, a0A, bB, a0B);
+      step(F_{}, std::integral_constant<int, 1>{}, s + 1, bB, a0B, bA, a0A);
+      step(F_{}, std::integral_constant<int, 0>{}, s + 2, bA, a0A, bB, a0B);
+      step(F_{}, std::integral_constant<int, LAST>{}, s + 3, bB, a0B, bA, a0A);
+    } else {
+      step(F_{}, std::integral_constant<int, 1>{}, s, bA, a0A, bB, a0B);
+      step(F_{}, std::integral_constant<int, 0>{}, s + 1, bB, a0B, bA, a0A);
+      step(F_{}, std::integral_constant<int, LAST>{}, s + 2, bA, a0A, bB, a0B);
+    }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
   // Epilogue: residues mod m (fp32 quotient estimate, exact int correction), packed 4 rows
