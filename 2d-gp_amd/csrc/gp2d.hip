@@ -471,7 +471,7 @@ int gp2d_ozaki_prepare(const double* W, int64_t n, int64_t ldw, const gp2d_kerne
 size_t gp2d_predict_ozaki_workspace(int64_t n, int64_t chunk) {
   const int nm = ozaki_nmod_for(n);
   if (nm <= 0) return 0;
-  const int64_t cp = round_up(chunk < 1 ? 1 : chunk, IBN / 2);
+  const int64_t cp = round_up(chunk < 1 ? 1 : chunk, IBN);
   const int64_t ncols = 2 * cp;
   return 2 * (size_t)nm * (size_t)n * (size_t)ncols                        // Bres + Cres planes
          + sizeof(double) * ((size_t)(n / 2 / OZ_KS_T + 1) + (size_t)(n / OZ_CRT_ROWS + 1)) * ncols;
@@ -494,7 +494,7 @@ int gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int nmod, int
   OzakiConsts oc;
   GP2D_CHECK(make_ozaki_consts(nmod, k, oc));
   const int nm = oc.nmod;
-  const int64_t ncols_max = 2 * chunk;
+  const int64_t ncols_max = 2 * round_up(chunk, IBN);
   int8_t* bres = reinterpret_cast<int8_t*>(work);
   uint8_t* cres = reinterpret_cast<uint8_t*>(bres + (size_t)nm * n * ncols_max);
   double* pm = reinterpret_cast<double*>(cres + (size_t)nm * n * ncols_max);
@@ -507,7 +507,7 @@ int gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int nmod, int
   const VecParams vp = make_vec_params(k);
   for (int64_t c0 = 0; c0 < m; c0 += chunk) {
     const int64_t cv = std::min<int64_t>(chunk, m - c0);
-    const int64_t cp = round_up(cv, IBN / 2);
+    const int64_t cp = round_up(cv, IBN);   // whole 256-row tiles per component half (B aliasing)
     const int64_t ncols = 2 * cp;
     ozaki_kstar_kernel<<<dim3((unsigned)nmseg, (unsigned)(cp / OZ_KS_P)), 256, 0, s>>>(
         xtr, ntr, ntr_pad, xg + 2 * c0, cv, cp, vp, alpha, oc, bres, pm);
@@ -522,7 +522,7 @@ int gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int nmod, int
       for (int l = 0; l < nm; ++l) {
         igemm_nt_mod_kernel<<<ggrid, 512, 0, s>>>(wres + (size_t)l * n * n, bres + (size_t)l * ncols * n,
                                                   cres + (size_t)l * n * ncols, n, (int)n, (int)ncols, (int)n, 1,
-                                                  oc.m[l], oc.inv_m[l]);
+                                                  oc.m[l], oc.inv_m[l], (int)(cp / IBN), (int)(ntr_pad / IBK));
         GP2D_CHECK(check_launch("igemm_nt_mod_kernel"));
       }
       if (e0) {

@@ -176,19 +176,20 @@ __global__ __launch_bounds__(256) void ozaki_kstar_kernel(
       pm[(int64_t)blockIdx.x * ncols + cp + p] = mv;
     }
     if (p >= cp) continue;
-    double xi[4][4];  // [entry: (u,u) (u,v) (v,u) (v,v)][u]
+    // The (v,u) block equals the (u,v) block (k12 is symmetric in the 2×2 kernel block), so
+    // only (u,u), (u,v) and (v,v) are stored: the GEMM reads (v,u) tiles from (u,v).
+    double xi[3][4];  // [entry: (u,u) (u,v) (v,v)][u]
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       xi[0][u] = rint(k11[u] * scale);
       xi[1][u] = rint(k12[u] * scale);
-      xi[3][u] = rint(k22[u] * scale);
-      xi[2][u] = xi[1][u];
+      xi[2][u] = rint(k22[u] * scale);
     }
     for (int l = 0; l < oc.nmod; ++l) {
       const double m = (double)oc.m[l], im = oc.inv_m[l];
-      uint32_t pk[4];
+      uint32_t pk[3];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
+      for (int e = 0; e < 3; ++e) {
         uint32_t w = 0;
 #pragma unroll
         for (int u = 0; u < 4; ++u) w |= (uint32_t)(uint8_t)(int8_t)centred_residue(xi[e][u], m, im) << (8 * u);
@@ -197,12 +198,11 @@ __global__ __launch_bounds__(256) void ozaki_kstar_kernel(
       if (t0 >= npad) continue;  // npad is a multiple of 64, so a 4-point group is all in or all out
       int8_t* plane = bres + (int64_t)l * ncols * n;
       // (grid comp, train comp): (u,u) → row p, col t ; (u,v) → row p, col npad+t ;
-      //                          (v,u) → row cp+p, col t ; (v,v) → row cp+p, col npad+t
+      //                          (v,v) → row cp+p, col npad+t ; (v,u) not stored
       // (slab-blocked plane: 4 consecutive columns stay inside one 64-B row segment)
       *reinterpret_cast<uint32_t*>(plane + slab_offset(p, t0, n)) = pk[0];
       *reinterpret_cast<uint32_t*>(plane + slab_offset(p, npad + t0, n)) = pk[1];
-      *reinterpret_cast<uint32_t*>(plane + slab_offset(cp + p, t0, n)) = pk[2];
-      *reinterpret_cast<uint32_t*>(plane + slab_offset(cp + p, npad + t0, n)) = pk[3];
+      *reinterpret_cast<uint32_t*>(plane + slab_offset(cp + p, npad + t0, n)) = pk[2];
     }
   }
 }
@@ -262,10 +262,14 @@ __device__ __forceinline__ void vmwait_barrier(std::integral_constant<int, W>) {
 
 
 // A: M×K plane, B: N×K plane (both slab-blocked); C: column-major N×M bytes (ldc ≥ M).
+// B tiles (row block rb ≥ alias_rb, k slab s < alias_ks) are read from (rb − alias_rb,
+// s + alias_ks): the K* planes store the (v,u) block only as its equal (u,v) block.
+// alias_rb = INT_MAX disables the aliasing.
 __global__ __launch_bounds__(512, 1) void igemm_nt_mod_kernel(const int8_t* __restrict__ A,
                                                               const int8_t* __restrict__ B,
                                                               uint8_t* __restrict__ C, int64_t ldc, int M, int N,
-                                                              int K, int a_lower, int modulus, double inv_mod) {
+                                                              int K, int a_lower, int modulus, double inv_mod,
+                                                              int alias_rb, int alias_ks) {
   __shared__ __attribute__((aligned(16))) int8_t smem[I_NSTAGE * I_STAGE];
   const int bj = blockIdx.x;
   const int bi = (int)(gridDim.y - 1 - blockIdx.y);   // heavy (long-K) row blocks first
@@ -276,7 +280,9 @@ __global__ __launch_bounds__(512, 1) void igemm_nt_mod_kernel(const int8_t* __re
   const int l16 = lane & 15, lq = lane >> 4;
   const int64_t kslabs = K / IBK;
   const int8_t* Ap = A + (int64_t)bi * kslabs * I_OP;   // this row block's slab tiles
+  const bool alias = bj >= alias_rb;
   const int8_t* Bp = B + (int64_t)bj * kslabs * I_OP;
+  const int8_t* Bq = B + ((int64_t)(alias ? bj - alias_rb : 0) * kslabs + alias_ks) * I_OP;
 
   i4v acc[8][4];
 #pragma unroll
@@ -293,7 +299,7 @@ __global__ __launch_bounds__(512, 1) void igemm_nt_mod_kernel(const int8_t* __re
     int8_t* As = smem + st * I_STAGE;
     int8_t* Bs = As + I_OP;
     const int8_t* Ag = Ap + (int64_t)s * I_OP;
-    const int8_t* Bg = Bp + (int64_t)s * I_OP;
+    const int8_t* Bg = ((alias && s < alias_ks) ? Bq : Bp) + (int64_t)s * I_OP;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int row = wid * 32 + h * 16 + drow;

@@ -5,6 +5,7 @@
 #include <cstdio>
 #include <random>
 #include <vector>
+#include <climits>
 namespace gp2d { void set_error(const std::string&) {} }
 using namespace gp2d;
 int main() {
@@ -24,7 +25,7 @@ int main() {
   (void)hipMemcpy(dB, Bb.data(), B.size(), hipMemcpyHostToDevice);
   hipEvent_t e0, e1; (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
   const dim3 g(nc / IBN, n / IBM);
-  auto launch = [&]() { igemm_nt_mod_kernel<<<g, 512>>>(dA, dB, dC, n, n, nc, n, 1, mod, 1.0 / mod); };
+  auto launch = [&]() { igemm_nt_mod_kernel<<<g, 512>>>(dA, dB, dC, n, n, nc, n, 1, mod, 1.0 / mod, 1 << 30, 0); };
   for (int w = 0; w < 3; ++w) launch();
   (void)hipDeviceSynchronize();
   (void)hipEventRecord(e0);
