@@ -44,6 +44,7 @@ struct GemmParams {
   int c_lower;   // enumerate lower tiles of a square C; diagonal tiles store i >= j
   int rev_rows;  // dispatch heavy (large i0) row blocks first (a_lower)
   int xcd_cols;  // 1-D grid: groups of 8 column tiles × all row blocks, column tile = XCD label
+  int cols_first;  // 1-D grid, column blocks slow and ascending: heavy-first order for b_lower
   double* P; int64_t ldp; int64_t sP;         // EPI_COLSQ partials [M/BM][N]
 };
 
@@ -73,6 +74,10 @@ __global__ __launch_bounds__(256, 2) void gemm_f64_kernel(GemmParams p) {
     const int g = q / nr, r = q - g * nr;
     bj = g * 8 + x;
     bi = nr - 1 - r;  // heavy (long-K) row blocks first
+  } else if (p.cols_first) {
+    const int nr = p.M / GBM;
+    bj = (int)blockIdx.x / nr;
+    bi = (int)blockIdx.x - bj * nr;
   } else {
     bj = blockIdx.x;
     bi = p.rev_rows ? (int)(gridDim.y - 1 - blockIdx.y) : (int)blockIdx.y;
@@ -222,6 +227,8 @@ inline int launch_gemm(const GemmParams& p, int batch, hipStream_t s) {
       set_error("gemm: xcd_cols needs a multiple of 8 column tiles");
       return -2;
     }
+    grid = dim3((p.N / GBN) * (p.M / GBM), 1, batch);
+  } else if (p.cols_first) {
     grid = dim3((p.N / GBN) * (p.M / GBM), 1, batch);
   } else {
     grid = dim3(p.N / GBN, p.M / GBM, batch);

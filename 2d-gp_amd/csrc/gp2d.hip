@@ -312,6 +312,7 @@ int gp2d_trtri(double* A, int64_t n, int64_t lda, const double* dinv, void* work
       p.B = A + Lo * lda + Lo; p.ldb = lda; p.sB = stride;
       p.C = T; p.ldc = bw; p.sC = (int64_t)rh * bw;
       p.M = rh; p.N = bw; p.K = bw; p.b_lower = 1;
+      p.cols_first = 1;   // column block j needs k ≥ j: long-K tiles first
       GP2D_CHECK((launch_gemm<false, EPI_STORE>(p, pr.count, s)));
       // A[R, L] = −WD · T     WD = A[R, R] (rh × rh lower)
       GemmParams q = gemm_params();
@@ -319,6 +320,7 @@ int gp2d_trtri(double* A, int64_t n, int64_t lda, const double* dinv, void* work
       q.B = T; q.ldb = bw; q.sB = (int64_t)rh * bw;
       q.C = A + Ro * lda + Lo; q.ldc = lda; q.sC = stride;
       q.M = rh; q.N = bw; q.K = rh; q.a_lower = 1; q.alpha = -1.0;
+      q.rev_rows = 1;     // row block i needs k ≤ i: long-K tiles first
       GP2D_CHECK((launch_gemm<false, EPI_STORE>(q, pr.count, s)));
     }
   }
