@@ -507,12 +507,14 @@ int gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int nmod, int
   const double add = (var_mode == GP2D_VAR_LATENT) ? 0.0 : noise;
   const int clip = (var_mode == GP2D_VAR_CLIPPED);
   const VecParams vp = make_vec_params(k);
+  OzakiConsts oc_mean_only = oc;
+  oc_mean_only.nmod = 0;   // mean only: K*·α without the residue planes
   for (int64_t c0 = 0; c0 < m; c0 += chunk) {
     const int64_t cv = std::min<int64_t>(chunk, m - c0);
     const int64_t cp = round_up(cv, IBN);   // whole 256-row tiles per component half (B aliasing)
     const int64_t ncols = 2 * cp;
     ozaki_kstar_kernel<<<dim3((unsigned)nmseg, (unsigned)(cp / OZ_KS_P)), 256, 0, s>>>(
-        xtr, ntr, ntr_pad, xg + 2 * c0, cv, cp, vp, alpha, oc, bres, pm);
+        xtr, ntr, ntr_pad, xg + 2 * c0, cv, cp, vp, alpha, compute_var ? oc : oc_mean_only, bres, pm);
     GP2D_CHECK(check_launch("ozaki_kstar_kernel"));
     if (compute_var) {
       hipEvent_t e0 = nullptr, e1 = nullptr;
