@@ -9,6 +9,7 @@
 #include "factor.hpp"
 #include "predict.hpp"
 #include "ozaki.hpp"
+#include "lml.hpp"
 #include "../../include/gp2d.h"
 
 #include <algorithm>
@@ -545,6 +546,127 @@ int gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int nmod, int
     GP2D_CHECK(check_launch("predict_finalize_kernel"));
   }
   return 0;
+}
+
+// ------------------------------------------------- LOG MARGINAL LIKELIHOOD (§8f.1)
+int gp2d_lml(const double* W, int64_t n, int64_t ldw, const double* alpha, const double* y, int64_t nobs,
+             double* lml_dev, void* stream) {
+  GP2D_REQUIRE(W && alpha && y && lml_dev, "lml: NULL argument");
+  GP2D_REQUIRE(n > 0 && ldw >= n && nobs >= 0 && nobs <= n, "lml: bad sizes");
+  hipStream_t s = S(stream);
+  lml_terms_kernel<<<1, 256, 0, s>>>(W, n, ldw, alpha, y, nobs, lml_dev);
+  return check_launch("lml_terms_kernel");
+}
+
+int gp2d_lml_grad_count(const gp2d_kernel_t* k) {
+  if (validate_kernel(k) != 0) return -2;
+  if (k->family == GP2D_FAMILY_VECTOR2D) return 4;
+  return k->nterms * (1 + k->dim) + 1;
+}
+
+int gp2d_kernel_grad_count(const gp2d_kernel_t* k) {
+  const int n = gp2d_lml_grad_count(k);
+  return n < 0 ? n : n - 1;
+}
+
+}  // extern "C"
+
+namespace {
+// Output order → accumulator slots (lml.hpp): GPy param_array order, noise last.
+SlotMap grad_slots(const gp2d_kernel_t* k, bool with_noise) {
+  SlotMap m{};
+  m.ng = 0;
+  if (k->family == GP2D_FAMILY_VECTOR2D) {
+    for (int a = 0; a < 3; ++a) m.slot[m.ng++] = a;
+    if (with_noise) m.slot[m.ng++] = 3;
+  } else {
+    for (int t = 0; t < k->nterms; ++t) {
+      m.slot[m.ng++] = t * 4;
+      for (int d = 0; d < k->dim; ++d) m.slot[m.ng++] = t * 4 + 1 + d;
+    }
+    if (with_noise) m.slot[m.ng++] = 8;
+  }
+  return m;
+}
+}  // namespace
+
+extern "C" {
+
+static int64_t grad_blocks(int64_t ncols_pad, int64_t nrows) {
+  return (ncols_pad / PT_TILE) * ((nrows + LML_ROWS - 1) / LML_ROWS);
+}
+
+size_t gp2d_lml_grad_workspace(int64_t n) {
+  const int64_t nblk = (n / PT_TILE + 1) * (n / LML_ROWS + 1);
+  return sizeof(double) * (2 * (size_t)n * (size_t)n + (size_t)nblk * LML_MAXG);
+}
+
+int gp2d_lml_grad(const double* W, int64_t n, int64_t ldw, const double* alpha, const double* xtr, int64_t ntr,
+                  int64_t ntr_pad, const gp2d_kernel_t* k, double* grad_dev, void* work, size_t work_bytes,
+                  void* stream) {
+  GP2D_CHECK(validate_kernel(k));
+  GP2D_REQUIRE(W && alpha && xtr && grad_dev, "lml_grad: NULL argument");
+  const int bd = gp2d_block_dim(k);
+  GP2D_REQUIRE(n == bd * ntr_pad && ntr_pad % PT_TILE == 0, "lml_grad: n must equal block_dim × ntr_pad");
+  GP2D_REQUIRE(n % NB == 0, "lml_grad: n must be a multiple of 128");
+  GP2D_REQUIRE(ntr >= 1 && ntr <= ntr_pad && ldw >= n, "lml_grad: bad sizes");
+  GP2D_REQUIRE(work != nullptr && work_bytes >= gp2d_lml_grad_workspace(n), "lml_grad: workspace too small");
+  hipStream_t s = S(stream);
+  double* V = reinterpret_cast<double*>(work);
+  double* C = V + (size_t)n * n;
+  double* partial = C + (size_t)n * n;
+  // V = J Wᵀ J (lower), C = V Vᵀ = J K_y⁻¹ J, lower tiles only
+  rev_transpose_kernel<<<dim3((unsigned)(n / 64), (unsigned)(n / 64)), 256, 0, s>>>(W, n, ldw, V);
+  GP2D_CHECK(check_launch("rev_transpose_kernel"));
+  GemmParams p = gemm_params();
+  p.A = V; p.lda = n;
+  p.B = V; p.ldb = n;
+  p.C = C; p.ldc = n;
+  p.M = (int)n; p.N = (int)n; p.K = (int)n;
+  p.a_lower = 1; p.c_lower = 1;
+  GP2D_CHECK((launch_gemm<true, EPI_STORE>(p, 1, s)));
+  const dim3 grid((unsigned)(ntr_pad / PT_TILE), (unsigned)((ntr + LML_ROWS - 1) / LML_ROWS));
+  if (k->family == GP2D_FAMILY_VECTOR2D) {
+    VecGradParams gp{make_vec_params(k), k->l_df, k->l_cf};
+    lml_grad_vec_kernel<<<grid, 256, 0, s>>>(C, n, alpha, xtr, ntr, ntr_pad, gp, partial);
+    GP2D_CHECK(check_launch("lml_grad_vec_kernel"));
+  } else {
+    lml_grad_ard_kernel<<<grid, 256, 0, s>>>(C, n, alpha, xtr, ntr, make_ard_params(k), partial);
+    GP2D_CHECK(check_launch("lml_grad_ard_kernel"));
+  }
+  const SlotMap sm = grad_slots(k, true);
+  grad_sum_kernel<<<sm.ng, 64, 0, s>>>(partial, grad_blocks(ntr_pad, ntr), sm, 0.5, grad_dev);
+  return check_launch("grad_sum_kernel");
+}
+
+size_t gp2d_kernel_grad_workspace(int64_t na, int64_t nb) {
+  return sizeof(double) * (size_t)grad_blocks(round_up(nb < 1 ? 1 : nb, PT_TILE), na < 1 ? 1 : na) * LML_MAXG;
+}
+
+int gp2d_kernel_grad(const double* xa, int64_t na, const double* xb, int64_t nb, const gp2d_kernel_t* k,
+                     const double* dL_dK, int64_t ld, double* grad_dev, void* work, size_t work_bytes,
+                     void* stream) {
+  GP2D_CHECK(validate_kernel(k));
+  GP2D_REQUIRE(xa && xb && dL_dK && grad_dev, "kernel_grad: NULL argument");
+  GP2D_REQUIRE(na >= 1 && nb >= 1, "kernel_grad: empty point set");
+  const int bd = gp2d_block_dim(k);
+  GP2D_REQUIRE(ld >= bd * nb, "kernel_grad: ld too small");
+  GP2D_REQUIRE(work != nullptr && work_bytes >= gp2d_kernel_grad_workspace(na, nb), "kernel_grad: workspace too small");
+  hipStream_t s = S(stream);
+  double* partial = reinterpret_cast<double*>(work);
+  const int64_t nbp = round_up(nb, PT_TILE);
+  const dim3 grid((unsigned)(nbp / PT_TILE), (unsigned)((na + LML_ROWS - 1) / LML_ROWS));
+  if (k->family == GP2D_FAMILY_VECTOR2D) {
+    VecGradParams gp{make_vec_params(k), k->l_df, k->l_cf};
+    kgrad_vec_kernel<<<grid, 256, 0, s>>>(xa, na, xb, nb, gp, dL_dK, ld, partial);
+    GP2D_CHECK(check_launch("kgrad_vec_kernel"));
+  } else {
+    kgrad_ard_kernel<<<grid, 256, 0, s>>>(xa, na, xb, nb, make_ard_params(k), dL_dK, ld, partial);
+    GP2D_CHECK(check_launch("kgrad_ard_kernel"));
+  }
+  const SlotMap sm = grad_slots(k, false);
+  grad_sum_kernel<<<sm.ng, 64, 0, s>>>(partial, grad_blocks(nbp, na), sm, 1.0, grad_dev);
+  return check_launch("grad_sum_kernel");
 }
 
 // ------------------------------------------------------------------ instrumentation

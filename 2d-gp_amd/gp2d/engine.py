@@ -125,6 +125,7 @@ class GPFit:
     device: torch.device
     info: int = 0
     extra: dict = field(default_factory=dict)
+    y: torch.Tensor = None   # (n,) padded observations (LML)
 
     @property
     def n(self) -> int:
@@ -197,7 +198,8 @@ def fit(kernel: KernelSpec, x, y, noise: float, jitter: float = 0.0, device=None
     pbytes = int(L.gp2d_potrs_workspace(n))
     pwork = torch.empty(pbytes // 8 + 1, dtype=torch.float64, device=dev)
     N.check(L.gp2d_potrs_inv(_ptr(A), n, n, _ptr(Y), _ptr(alpha), _ptr(pwork), pbytes, s), "gp2d_potrs_inv")
-    gp = GPFit(kernel=kernel, noise=float(noise), x=X, n_train=ntr, n_pad=npad, W=A, alpha=alpha, device=dev)
+    gp = GPFit(kernel=kernel, noise=float(noise), x=X, n_train=ntr, n_pad=npad, W=A, alpha=alpha, device=dev,
+               y=Y)
     if variance == "ozaki":
         ozaki_prepare(gp)
     return gp
@@ -265,6 +267,70 @@ class Predictor:
 
 def predict(gp: GPFit, xg, var_mode: str = "latent", compute_var: bool = True, chunk: int = 8192):
     return Predictor(gp, chunk)(xg, var_mode=var_mode, compute_var=compute_var)
+
+
+# ------------------------------------------------------------------ hyperparameters
+def param_names(kernel: KernelSpec) -> tuple:
+    """Gradient / parameter order of log_marginal_likelihood: vector2d (l_df, l_cf, ratio, noise);
+    ARD per term (variance, lengthscale_0..D−1), then noise (GPy param_array order, krig.py:459-466)."""
+    if kernel.family == "vector2d":
+        return ("l_df", "l_cf", "ratio", "noise")
+    names = []
+    for t, ls in enumerate(kernel.lengthscales):
+        names += [f"variance_{t}"] + [f"lengthscale_{t}_{d}" for d in range(len(ls))]
+    return tuple(names + ["noise"])
+
+
+def log_marginal_likelihood(gp: GPFit, eval_gradient: bool = False):
+    """log p(y | X, θ) of a fit, and optionally ∂/∂θ in natural units (param_names order).
+
+    Replaces the objective of GPy model.optimize (krig.py:450; GP_plots.py:673-765) and
+    sklearn log_marginal_likelihood(theta, eval_gradient=True) (_gpr.py:584-650); the
+    gradient is the exact one (the reference's myKernel.update_gradients_full is not,
+    SURVEY.md §0.2).  Both run in HIP kernels (gp2d_lml, gp2d_lml_grad)."""
+    if gp.y is None:
+        raise ValueError("this fit carries no observations (it was not made by engine.fit)")
+    L = N.lib()
+    s = _stream_handle(gp.device)
+    bd = gp.kernel.block_dim
+    out = torch.empty(1, dtype=torch.float64, device=gp.device)
+    N.check(L.gp2d_lml(_ptr(gp.W), gp.n, gp.n, _ptr(gp.alpha), _ptr(gp.y), bd * gp.n_train, _ptr(out), s),
+            "gp2d_lml")
+    if not eval_gradient:
+        return float(out.item())
+    desc = gp.kernel.desc()
+    ng = int(L.gp2d_lml_grad_count(ctypes.byref(desc)))
+    wbytes = int(L.gp2d_lml_grad_workspace(gp.n))
+    work = torch.empty(wbytes // 8 + 1, dtype=torch.float64, device=gp.device)
+    g = torch.empty(ng, dtype=torch.float64, device=gp.device)
+    N.check(L.gp2d_lml_grad(_ptr(gp.W), gp.n, gp.n, _ptr(gp.alpha), _ptr(gp.x), gp.n_train, gp.n_pad,
+                            ctypes.byref(desc), _ptr(g), _ptr(work), wbytes, s), "gp2d_lml_grad")
+    return float(out.item()), g.cpu().numpy()
+
+
+def kernel_grad(kernel: KernelSpec, xa, dL_dK, xb=None, device=None) -> np.ndarray:
+    """Σ dL_dK ⊙ ∂K(xa, xb)/∂θ for θ = param_names(kernel) without the noise — the contraction
+    GPy's Kern.update_gradients_full performs (myKernel.py:59-105; the exact derivative, not the
+    reference's formula).  dL_dK: (bd·Na, bd·Nb) in the reference's component-major layout."""
+    dev = _require_device(device)
+    L = N.lib()
+    d = kernel.input_dim
+    A = _as_points(xa, d, dev)
+    B = A if xb is None else _as_points(xb, d, dev)
+    G = dL_dK.to(device=dev, dtype=torch.float64) if isinstance(dL_dK, torch.Tensor) else \
+        torch.as_tensor(np.ascontiguousarray(np.asarray(dL_dK, dtype=np.float64)), device=dev)
+    G = G.contiguous()
+    bd = kernel.block_dim
+    if tuple(G.shape) != (bd * A.shape[0], bd * B.shape[0]):
+        raise ValueError(f"dL_dK has shape {tuple(G.shape)}, expected {(bd * A.shape[0], bd * B.shape[0])}")
+    desc = kernel.desc()
+    ng = int(L.gp2d_kernel_grad_count(ctypes.byref(desc)))
+    wbytes = int(L.gp2d_kernel_grad_workspace(A.shape[0], B.shape[0]))
+    work = torch.empty(wbytes // 8 + 1, dtype=torch.float64, device=dev)
+    g = torch.empty(ng, dtype=torch.float64, device=dev)
+    N.check(L.gp2d_kernel_grad(_ptr(A), A.shape[0], _ptr(B), B.shape[0], ctypes.byref(desc), _ptr(G), G.shape[1],
+                               _ptr(g), _ptr(work), wbytes, _stream_handle(dev)), "gp2d_kernel_grad")
+    return g.cpu().numpy()
 
 
 def timing_enable(on: bool = True):

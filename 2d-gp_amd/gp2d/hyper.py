@@ -1,0 +1,230 @@
+"""Hyperparameter fitting on the GPU.
+
+Replaces GPy's model.optimize / optimize_restarts (krig.py:430-468 runRestarts;
+GP_plots.py:673-765; laser_io_methods.py:496-676) and sklearn's internal
+L-BFGS-B restarts (_gpr.py:298-333).  Every objective evaluation is one HIP fit
+(assemble → POTRF → TRTRI → α) plus gp2d_lml / gp2d_lml_grad; only the optimiser
+state (a handful of scalars) lives on the host.
+
+Free parameters are optimised in an unconstrained space, as GPy does through its
+constraints (myKernel.py:19-21): length scales, variances and the noise variance
+through log (GPy: constrain_positive), the div-free weight `ratio` through the
+logistic map (GPy: constrain_bounded(0, 1)).  Restarts draw the starting point
+uniformly within ±`spread` of the current point in that space (GPy's randomize()
+draws from the parameters' priors; the reference sets none, so the spread is ours).
+
+Config E (64 hyperparameter settings × N=4096, BASELINE.json) is `sweep`: the
+settings are dealt round-robin to ranks (one GP per GPU at a time), each rank
+evaluates its own, and one all-reduce of a zero-padded vector assembles the
+results — every entry has exactly one non-zero contributor, so the result is
+bit-identical for any world size.
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import engine as E
+
+_BAD = 1e25  # objective for a non-positive-definite K_y (rejected by the line search)
+
+
+def free_names(kernel: E.KernelSpec, fix=()) -> tuple:
+    """Names (engine.param_names order) of the parameters the optimiser moves."""
+    if kernel.family == "vector2d":
+        used = {"df": ("l_df",), "scalar": ("l_df",), "cf": ("l_cf",),
+                "mixed": ("l_df", "l_cf", "ratio")}[_kind_name(kernel.kind)]
+        names = used + ("noise",)
+    else:
+        names = E.param_names(kernel)
+    return tuple(n for n in names if n not in set(fix))
+
+
+def _kind_name(kind):
+    return {0: "scalar", 1: "df", 2: "cf", 3: "mixed"}.get(kind, kind)
+
+
+def get_params(kernel: E.KernelSpec, noise: float) -> dict:
+    names = E.param_names(kernel)
+    if kernel.family == "vector2d":
+        vals = (kernel.l_df, kernel.l_cf, kernel.ratio, noise)
+    else:
+        vals = []
+        for v, ls in zip(kernel.variances, kernel.lengthscales):
+            vals += [v, *ls]
+        vals.append(noise)
+    return dict(zip(names, (float(v) for v in vals)))
+
+
+def set_params(kernel: E.KernelSpec, params: dict):
+    """(KernelSpec, noise) with `params` (a get_params-style dict) applied."""
+    if kernel.family == "vector2d":
+        k = dataclasses.replace(kernel, l_df=params["l_df"], l_cf=params["l_cf"], ratio=params["ratio"])
+        return k, params["noise"]
+    var, ls = [], []
+    for t, l in enumerate(kernel.lengthscales):
+        var.append(params[f"variance_{t}"])
+        ls.append(tuple(params[f"lengthscale_{t}_{d}"] for d in range(len(l))))
+    return dataclasses.replace(kernel, variances=tuple(var), lengthscales=tuple(ls)), params["noise"]
+
+
+def _to_free(name, v):
+    if name == "ratio":
+        v = min(max(v, 1e-12), 1 - 1e-12)
+        return math.log(v / (1 - v))
+    return math.log(v)
+
+
+def _from_free(name, z):
+    if name == "ratio":
+        return 1.0 / (1.0 + math.exp(-z))
+    return math.exp(z)
+
+
+def _dfree(name, v):
+    """d(value)/d(free coordinate)."""
+    return v * (1 - v) if name == "ratio" else v
+
+
+@dataclass
+class OptResult:
+    kernel: E.KernelSpec
+    noise: float
+    lml: float
+    nit: int = 0
+    nfev: int = 0
+    success: bool = True
+    message: str = ""
+    runs: list = field(default_factory=list)   # per-restart (params dict, lml), GPy optimization_runs
+
+
+class Objective:
+    """−LML and its gradient in the free coordinates, one HIP fit per evaluation."""
+
+    def __init__(self, kernel, x, y, noise, names, jitter=0.0, device=None):
+        self.kernel, self.noise = kernel, float(noise)
+        self.x, self.y = x, y
+        self.names = tuple(names)
+        self.jitter = float(jitter)
+        self.device = device
+        self.base = get_params(kernel, noise)
+        self.order = E.param_names(kernel)
+        self.nfev = 0
+
+    def params(self, z) -> dict:
+        p = dict(self.base)
+        for n, zi in zip(self.names, z):
+            p[n] = _from_free(n, float(zi))
+        return p
+
+    def __call__(self, z):
+        self.nfev += 1
+        p = self.params(z)
+        k, noise = set_params(self.kernel, p)
+        try:
+            gp = E.fit(k, self.x, self.y, noise, jitter=self.jitter, device=self.device)
+        except np.linalg.LinAlgError:
+            return _BAD, np.zeros(len(z))
+        val, g = E.log_marginal_likelihood(gp, eval_gradient=True)
+        del gp
+        gd = dict(zip(self.order, g))
+        gz = np.array([gd[n] * _dfree(n, p[n]) for n in self.names])
+        if not np.isfinite(val) or not np.all(np.isfinite(gz)):
+            return _BAD, np.zeros(len(z))
+        return -val, -gz
+
+
+def optimize(kernel: E.KernelSpec, x, y, noise: float, fix=(), jitter: float = 0.0, device=None,
+             maxiter: int = 200, start: dict = None, messages: bool = False) -> OptResult:
+    """Maximise the LML over the free hyperparameters with L-BFGS-B (GPy model.optimize,
+    krig.py:450 / laser_io_methods.py:496).  `fix` names parameters to hold (GPy
+    constrain_fixed, GP_plots.py:761-762)."""
+    from scipy.optimize import minimize
+    names = free_names(kernel, fix)
+    obj = Objective(kernel, x, y, noise, names, jitter=jitter, device=device)
+    p0 = dict(obj.base)
+    if start:
+        p0.update(start)
+    z0 = np.array([_to_free(n, p0[n]) for n in names])
+    if len(names) == 0:
+        val = -obj(z0)[0]
+        return OptResult(kernel, float(noise), val, nfev=1)
+    res = minimize(obj, z0, jac=True, method="L-BFGS-B", options=dict(maxiter=maxiter, disp=bool(messages)))
+    p = obj.params(res.x)
+    k, nz = set_params(kernel, p)
+    return OptResult(k, nz, float(-res.fun), nit=int(res.nit), nfev=obj.nfev, success=bool(res.success),
+                     message=str(res.message))
+
+
+def optimize_restarts(kernel: E.KernelSpec, x, y, noise: float, num_restarts: int = 10, fix=(),
+                      jitter: float = 0.0, device=None, seed: int = 0, spread: float = 1.0,
+                      maxiter: int = 200, messages: bool = False) -> OptResult:
+    """GPy model.optimize_restarts (krig.py:450): the first run starts at the current
+    hyperparameters, the others at random points within ±spread (free coordinates);
+    the best run is returned, all runs are listed in .runs."""
+    rng = np.random.default_rng(seed)
+    names = free_names(kernel, fix)
+    base = get_params(kernel, noise)
+    best = None
+    runs = []
+    for r in range(max(1, int(num_restarts))):
+        start = None
+        if r > 0:
+            start = {n: _from_free(n, _to_free(n, base[n]) + rng.uniform(-spread, spread)) for n in names}
+        res = optimize(kernel, x, y, noise, fix=fix, jitter=jitter, device=device, maxiter=maxiter, start=start,
+                       messages=messages)
+        runs.append((get_params(res.kernel, res.noise), res.lml))
+        if best is None or res.lml > best.lml:
+            best = res
+    best.runs = runs
+    return best
+
+
+def sweep(kernel: E.KernelSpec, x, y, settings, noise: float = None, jitter: float = 0.0, device=None,
+          eval_gradient: bool = False):
+    """LML (and gradient) for each hyperparameter setting (a list of get_params-style dicts,
+    missing keys taken from kernel/noise) — BASELINE config E.  Under torch.distributed the
+    settings are dealt round-robin over ranks and the results all-reduced (bit-identical to
+    one rank).  Returns (lml[S], grad[S, P] or None); a non-PD setting gives -inf."""
+    ws, rank = (dist.get_world_size(), dist.get_rank()) if dist.is_available() and dist.is_initialized() else (1, 0)
+    base = get_params(kernel, noise if noise is not None else 0.0)
+    S = len(settings)
+    P = len(base)
+    vals = np.zeros(S)
+    grads = np.zeros((S, P))
+    for i in range(rank, S, ws):
+        p = dict(base)
+        p.update(settings[i])
+        k, nz = set_params(kernel, p)
+        try:
+            gp = E.fit(k, x, y, nz, jitter=jitter, device=device)
+        except np.linalg.LinAlgError:
+            vals[i] = -np.inf
+            continue
+        if eval_gradient:
+            vals[i], grads[i] = E.log_marginal_likelihood(gp, eval_gradient=True)
+        else:
+            vals[i] = E.log_marginal_likelihood(gp)
+        del gp
+    if ws > 1:
+        vals, grads = allreduce_disjoint(vals, grads, device)
+    return vals, (grads if eval_gradient else None)
+
+
+def allreduce_disjoint(vals: np.ndarray, grads: np.ndarray, device=None):
+    """Combine per-rank results whose non-zero entries are disjoint (sum of x and exact zeros:
+    bit-exact).  -inf entries travel as a separate mask."""
+    bad = np.isneginf(vals)
+    v = np.where(bad, 0.0, vals)
+    dev = device if (device is not None and torch.cuda.is_available() and dist.get_backend() == "nccl") else "cpu"
+    buf = torch.as_tensor(np.concatenate([v, bad.astype(np.float64), grads.reshape(-1)]), device=dev)
+    dist.all_reduce(buf)
+    out = buf.cpu().numpy()
+    S = vals.size
+    v, bad = out[:S], out[S:2 * S] > 0
+    return np.where(bad, -np.inf, v), out[2 * S:].reshape(grads.shape)

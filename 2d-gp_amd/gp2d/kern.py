@@ -11,8 +11,11 @@ Mirrors
     K* generation, variance from the inverse Cholesky factor).
 
 GPy itself is not a dependency: the classes expose the same methods and
-parameters without the paramz machinery.  Gradient methods are out of scope for
-this round (the reference's are broken); calling them raises.
+parameters without the paramz machinery.  Parameters are floats carrying a
+``.gradient`` attribute, which ``update_gradients_full`` fills with the EXACT
+derivative contraction (HIP kernel gp2d_kernel_grad) — the reference's own
+formula is not a derivative of its kernel.
+``gradients_X`` raises, as the reference's does (NameError, myKernel.py:123).
 Outputs are numpy arrays, as in the reference; ``*_device`` variants return the
 torch tensor resident in HBM.
 """
@@ -23,8 +26,18 @@ import numpy as np
 from . import engine as E
 
 
+class Param(float):
+    """A float hyperparameter with a GPy-style ``.gradient`` slot."""
+
+    def __new__(cls, value):
+        obj = super().__new__(cls, value)
+        obj.gradient = 0.0
+        return obj
+
+
 class _VectorKern:
     input_dim = 2
+    _grad_index = (0, 1, 2)   # engine.kernel_grad entries for parameter_names()
 
     def __init__(self, input_dim=2, active_dim=(0, 1), name="kern"):
         assert input_dim == 2, "For this kernel we assume input_dim=2"
@@ -55,9 +68,20 @@ class _VectorKern:
         return np.full(2 * n, self._spec().kdiag())
 
     def update_gradients_full(self, dL_dK, X, X2=None):
-        raise NotImplementedError("kernel gradients are SURVEY.md §8f item 1 (next round)")
+        """Set each parameter's .gradient to Σ dL_dK ⊙ ∂K(X, X2)/∂θ (myKernel.py:59-105)."""
+        g = E.kernel_grad(self._spec(), self._cols(X), dL_dK, None if X2 is None else self._cols(X2))
+        for name, i in zip(self.parameter_names(), self._grad_index):
+            p = Param(getattr(self, name))
+            p.gradient = float(g[i])
+            setattr(self, name, p)
 
-    gradients_X = update_gradients_full
+    def update_gradients_diag(self, dL_dKdiag, X):
+        """Kdiag depends on the length scales only through 1/ℓ²; the reference leaves this a
+        no-op (myKernel.py:107-108), and so does this mirror."""
+
+    def gradients_X(self, dL_dK, X, X2=None):
+        raise NotImplementedError("gradients_X is broken in the reference (NameError, myKernel.py:123); "
+                                  "not provided")
 
     @property
     def param_array(self):
@@ -73,9 +97,9 @@ class myKernel(_VectorKern):
             raise ValueError("length scales must be positive")
         if not 0.0 <= ratio <= 1.0:
             raise ValueError("ratio is bounded to [0, 1] (myKernel.py:21)")
-        self.length_df = float(l_df)
-        self.length_cf = float(l_cf)
-        self.ratio = float(ratio)
+        self.length_df = Param(l_df)
+        self.length_cf = Param(l_cf)
+        self.ratio = Param(ratio)
 
     def parameter_names(self):
         return ["length_df", "length_cf", "ratio"]
@@ -86,12 +110,13 @@ class myKernel(_VectorKern):
 
 class nonDivK(_VectorKern):
     """Divergence-free SE kernel (myKernel.py:148-180)."""
+    _grad_index = (0,)
 
     def __init__(self, input_dim=2, active_dim=(0, 1), length=1.0):
         super().__init__(input_dim, active_dim, "nonDivK")
         if length <= 0:
             raise ValueError("length must be positive")
-        self.length = float(length)
+        self.length = Param(length)
 
     def parameter_names(self):
         return ["length"]
@@ -102,12 +127,13 @@ class nonDivK(_VectorKern):
 
 class nonRotK(_VectorKern):
     """Curl-free SE kernel (myKernel.py:244-275)."""
+    _grad_index = (1,)
 
     def __init__(self, input_dim=2, active_dim=(0, 1), l=1.0):  # noqa: E741 (reference name)
         super().__init__(input_dim, active_dim, "nonRotK")
         if l <= 0:
             raise ValueError("length must be positive")
-        self.length = float(l)
+        self.length = Param(l)
 
     def parameter_names(self):
         return ["length"]

@@ -12,8 +12,8 @@ Differences forced by the environment (documented in DESIGN.md):
   * pyproj / NAD83 is absent: ``project`` is a signed local equirectangular
     projection in km about (lat0, lon0);
   * NetCDF output is SURVEY.md §8f item 3 (next): outputs are ``.npz``;
-  * hyperparameter optimisation (GPy optimize_restarts) is §8f item 1 (next):
-    ``runRestarts`` raises NotImplementedError;
+  * hyperparameter optimisation (GPy optimize / optimize_restarts) runs on the GPU
+    (``gp2d.hyper``: HIP LML + exact gradient, scipy L-BFGS-B on the host);
   * kernelType 2/3/4 use the 2-D spatial div-free / curl-free / mixed kernels on
     the (Y, X) columns — the reference's spatio-temporal myKernel2 is missing from
     the reference itself (krig.py:9).
@@ -29,6 +29,7 @@ import torch
 
 from . import data as D
 from . import engine as E
+from . import hyper as H
 
 lat0 = 28.8
 lon0 = -88.6
@@ -130,6 +131,32 @@ class Krig:
         M = pts.shape[0]
         shp = [np.size(y), -1]
         return (mu[:M].reshape(shp), mu[M:].reshape(shp), var[:M].reshape(shp), var[M:].reshape(shp))
+
+    # ------------------------------------------------------------------ hyperparameters
+    def log_likelihood(self, eval_gradient: bool = False):
+        """GPy model.log_likelihood() / sklearn log_marginal_likelihood() of the current fit;
+        with eval_gradient also ∂/∂θ in param_array order (engine.param_names)."""
+        self._check()
+        return E.log_marginal_likelihood(self.gp, eval_gradient=eval_gradient)
+
+    def _apply(self, res: "H.OptResult"):
+        self.spec, self.noise = res.kernel, float(res.noise)
+        self.fit(self._X, self._y)
+        return res
+
+    def optimize(self, fix=(), messages: bool = False, maxiter: int = 200):
+        """GPy model.optimize (laser_io_methods.py:496): L-BFGS-B on the LML, refit at the optimum."""
+        self._check()
+        return self._apply(H.optimize(self.spec, self._X, self._y, self.noise, fix=fix, jitter=self.jitter,
+                                      device=self.device, maxiter=maxiter, messages=messages))
+
+    def optimize_restarts(self, num_restarts: int = 10, fix=(), seed: int = 0, messages: bool = False,
+                          maxiter: int = 200):
+        """GPy model.optimize_restarts (krig.py:450): best of num_restarts L-BFGS-B runs."""
+        self._check()
+        return self._apply(H.optimize_restarts(self.spec, self._X, self._y, self.noise, num_restarts=num_restarts,
+                                               fix=fix, jitter=self.jitter, device=self.device, seed=seed,
+                                               maxiter=maxiter, messages=messages))
 
     # ------------------------------------------------------------------ state
     @property
@@ -320,9 +347,25 @@ def kriging(st, et, lalim=(0, 0), lolim=(0, 0), sample_step=5, skip=5, nKernels=
     return models
 
 
-def runRestarts(fname, nres=10, nKernels=2):
-    """krig.runRestarts (krig.py:430-468): GPy optimize_restarts of the hyperparameters."""
-    raise NotImplementedError("hyperparameter optimisation is SURVEY.md §8f item 1 (next round)")
+def runRestarts(fname, nres=10, nKernels=2, device=None, seed=0):
+    """krig.runRestarts (krig.py:430-468): load a saved model, optimize_restarts its
+    hyperparameters (nres runs), save it back and print old : new values.  Model files are
+    .npz (Krig.save) instead of GPy pickles; the restart history is kept in the model file
+    (the reference's fname_dict.pkl workaround, krig.py:439-457, is not needed)."""
+    t0 = time.time()
+    filename = fname if fname.endswith(".npz") else fname + ".npz"
+    model = Krig.load(filename, device=device)
+    hyp_old = model.param_array.copy()
+    res = model.optimize_restarts(num_restarts=nres, seed=seed)
+    hyp = model.param_array
+    model.save(filename)
+    print("Optimized Hyperparameters =================================================")
+    names = E.param_names(model.spec)
+    for nm, a, b in zip(names, hyp_old, hyp):
+        print(f"{nm} = {a}   :   {b}")
+    print("===========================================================================")
+    print("End of script, time : " + str(time.time() - t0))
+    return res
 
 
 def predict(filename, tlim=(0, 0), ylim=(0, 0), xlim=(0, 0), dt=0.5, dx=0.5, xL=40, yL=40, Simul=0,

@@ -142,6 +142,39 @@ int    gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int nmod, 
                           double* mean, double* var, int64_t chunk,
                           void* work, size_t work_bytes, void* stream);
 
+/* ---- hyperparameters: log marginal likelihood and its gradient -----
+ * Replaces the objective of GPy model.optimize / optimize_restarts (krig.py:450,
+ * GP_plots.py:673-765) and sklearn log_marginal_likelihood(theta, eval_gradient=True)
+ * (_gpr.py:584-650), evaluated from a fit (W = L⁻¹, alpha = K_y⁻¹y, y the padded
+ * observations of gp2d_potrs_inv):
+ * gp2d_lml: *lml_dev (device double) = −½ yᵀα + Σ log W_ii − (nobs/2) log 2π,
+ *   nobs = observed entries (bd·N).
+ * gp2d_lml_grad: grad_dev (device, gp2d_lml_grad_count(k) doubles) = ½ tr((ααᵀ − K_y⁻¹) ∂K_y/∂θ)
+ *   in natural units, θ = vector2d: (l_df, l_cf, ratio, noise) — entries a kind does not
+ *   use are 0, KIND_SCALAR's σ is l_df; ARD, per term t: (var[t], ls[t][0..D)), then noise —
+ *   GPy's param_array order (krig.py:459-466).
+ *   K_y⁻¹ = WᵀW is formed in the workspace (gp2d_lml_grad_workspace(n) bytes, ≈ 2n² doubles).
+ *   The reference's myKernel.update_gradients_full (myKernel.py:59-105) is not the
+ *   derivative of its kernel; this is the exact one.                  */
+int    gp2d_lml(const double* W, int64_t n, int64_t ldw, const double* alpha, const double* y,
+                int64_t nobs, double* lml_dev, void* stream);
+int    gp2d_lml_grad_count(const gp2d_kernel_t* k);
+size_t gp2d_lml_grad_workspace(int64_t n);
+int    gp2d_lml_grad(const double* W, int64_t n, int64_t ldw, const double* alpha,
+                     const double* xtr, int64_t ntr, int64_t ntr_pad, const gp2d_kernel_t* k,
+                     double* grad_dev, void* work, size_t work_bytes, void* stream);
+
+/* gp2d_kernel_grad: the GPy Kern.update_gradients_full contraction (myKernel.py:59-105,
+ * exact derivative): grad_dev[g] = Σ_ab dL_dK[a][b] · ∂K(xa, xb)_ab/∂θ_g for a caller-supplied
+ * dL_dK (device, (bd·na) × (bd·nb) component-major WITHOUT padding — the reference layout —
+ * leading dim ld).  θ as gp2d_lml_grad without the noise entry
+ * (gp2d_kernel_grad_count(k) = gp2d_lml_grad_count(k) − 1 values).                      */
+int    gp2d_kernel_grad_count(const gp2d_kernel_t* k);
+size_t gp2d_kernel_grad_workspace(int64_t na, int64_t nb);
+int    gp2d_kernel_grad(const double* xa, int64_t na, const double* xb, int64_t nb,
+                        const gp2d_kernel_t* k, const double* dL_dK, int64_t ld,
+                        double* grad_dev, void* work, size_t work_bytes, void* stream);
+
 /* ---- instrumentation ------------------------------------------------------------
  * When enabled, every launch of the predict variance kernel (the dominant
  * kernel) is bracketed by hipEvents on its stream; gp2d_timing_read()

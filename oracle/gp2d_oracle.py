@@ -215,6 +215,115 @@ def ard_fit_predict(X, y, Xg, variances, lengthscales, noise, jitter=1e-10):
 
 
 # --------------------------------------------------------------------------------------
+# Log marginal likelihood and its gradient
+# --------------------------------------------------------------------------------------
+def lml_from_K(K, y):
+    """−½ yᵀK⁻¹y − Σ log L_ii − (n/2) log 2π via Cholesky (sklearn _gpr.py:612-628; GPy
+    ExactGaussianInference, the objective of model.optimize at krig.py:450)."""
+    import scipy.linalg as sla
+    y = np.asarray(y, dtype=np.float64).reshape(-1)
+    L = np.linalg.cholesky(K)
+    alpha = sla.cho_solve((L, True), y)
+    return -0.5 * y @ alpha - np.sum(np.log(np.diag(L))) - 0.5 * y.size * np.log(2 * np.pi), L, alpha
+
+
+def _trace_grad(L, alpha, dK):
+    """½ tr((ααᵀ − K⁻¹) dK) (sklearn _gpr.py:631-642)."""
+    import scipy.linalg as sla
+    Ki = sla.cho_solve((L, True), np.eye(L.shape[0]))
+    return 0.5 * np.einsum("ij,ji->", np.outer(alpha, alpha) - Ki, dK)
+
+
+VECTOR_PARAMS = ("l_df", "l_cf", "ratio", "noise")
+
+
+def vector_lml(x, y, kind="df", l_df=5.0, l_cf=5.0, ratio=1.0, noise=0.0025, jitter=0.0,
+               eval_gradient=False, rel_step=1e-4):
+    """LML of the vector-kernel GP (K_y = vector_kernel + (noise+jitter)·I).
+
+    The gradient (l_df, l_cf, ratio, noise) differentiates the kernel MATRIX numerically —
+    a 4-point central stencil on vector_kernel, independent of the HIP kernel's closed-form
+    derivative — and contracts it as ½ tr((ααᵀ − K_y⁻¹) ∂K). Parameters a kind does not use
+    get 0 (scalar kind: σ = l_df).  ∂K_y/∂noise = I."""
+    x = np.asarray(x, dtype=np.float64).reshape(-1, 2)
+    kw = dict(kind=kind, l_df=l_df, l_cf=l_cf, ratio=ratio)
+    K = vector_kernel(x, x, **kw)
+    K[np.diag_indices_from(K)] += noise + jitter
+    val, L, alpha = lml_from_K(K, y)
+    if not eval_gradient:
+        return val
+    code = kind_code(kind)
+    uses = {KIND_SCALAR: ("l_df",), KIND_DIVFREE: ("l_df",), KIND_CURLFREE: ("l_cf",),
+            KIND_MIXED: ("l_df", "l_cf", "ratio")}[code]
+    g = np.zeros(4)
+    for i, name in enumerate(VECTOR_PARAMS[:3]):
+        if name not in uses:
+            continue
+        h = rel_step * (abs(kw[name]) if name != "ratio" else 1.0)
+        Ks = []
+        for t in (-2, -1, 1, 2):
+            k2 = dict(kw)
+            k2[name] = kw[name] + t * h
+            Ks.append(vector_kernel(x, x, **k2))
+        dK = (Ks[0] - 8 * Ks[1] + 8 * Ks[2] - Ks[3]) / (12 * h)
+        g[i] = _trace_grad(L, alpha, dK)
+    g[3] = _trace_grad(L, alpha, np.eye(K.shape[0]))
+    return val, g
+
+
+def ard_lml(X, y, variances, lengthscales, noise, jitter=0.0, eval_gradient=False):
+    """LML of Σ_t var_t·RBF(ls_t) + White(noise) (the krig.scikit_prior model, krig.py:174-180)
+    with the analytic gradient in GPy's param_array order: per term (var_t, ls_t[0..D)), then
+    noise.  ∂k/∂var_t = e_t, ∂k/∂ls_td = var_t·e_t·Δ_d²/ls_td³ (sklearn kernels.RBF.__call__
+    gradient, divided by ls to leave log-space)."""
+    X = np.atleast_2d(np.asarray(X, dtype=np.float64))
+    K = ard_rbf_exact(X, X, variances, lengthscales)
+    K[np.diag_indices_from(K)] += noise + jitter
+    val, L, alpha = lml_from_K(K, y)
+    if not eval_gradient:
+        return val
+    g = []
+    for v, ls in zip(variances, lengthscales):
+        e = ard_rbf_exact(X, X, [1.0], [ls])
+        g.append(_trace_grad(L, alpha, e))
+        for d in range(X.shape[1]):
+            D2 = np.square(X[:, d][:, None] - X[:, d][None, :])
+            g.append(_trace_grad(L, alpha, v * e * D2 / ls[d] ** 3))
+    g.append(_trace_grad(L, alpha, np.eye(K.shape[0])))
+    return val, np.array(g)
+
+
+def reference_mykernel_gradient(x, dL_dK, l_df, l_cf, ratio):
+    """The reference's myKernel.update_gradients_full (myKernel.py:59-105), restated to document
+    SURVEY.md §0.2's quirk: its l_df / l_cf entries are NOT the derivative of myKernel.K
+    (myKernel.py:27-53) — the A·(2ℓ²−Cℓ²)/ℓ⁵ term has the opposite sign and dA/dℓ lacks
+    the 1/ℓ² factor.  Its ratio entry is right.  Returns (g_ldf, g_lcf, g_ratio)."""
+    x = np.asarray(x, dtype=np.float64).reshape(-1, 2)
+    d1 = x[:, 0][:, None] - x[:, 0]
+    d2 = x[:, 1][:, None] - x[:, 1]
+    B11, B12, B22 = d1 * d1, d1 * d2, d2 * d2
+    r2 = B11 + B22
+
+    def blk(a, b, c):
+        return np.block([[a, b], [b, c]])
+
+    ld2 = l_df ** 2
+    Cd = r2 / ld2
+    Ad = blk(B11 / ld2 + 1 - Cd, B12 / ld2, B22 / ld2 + 1 - Cd)
+    dAd = (2 / l_df ** 3) * blk(r2 - B11, -B12, r2 - B22)
+    Cd4 = blk(Cd, Cd, Cd)
+    g_df = ratio * np.exp(-Cd4 / 2) * (dAd + Ad * (2 * ld2 - Cd4 * ld2) / l_df ** 5)
+    lc2 = l_cf ** 2
+    Cc = r2 / lc2
+    Ac = blk(1 - B11 / lc2, -B12 / lc2, 1 - B22 / lc2)
+    dAc = (2 / l_cf ** 3) * blk(B11, B12, B22)
+    Cc4 = blk(Cc, Cc, Cc)
+    g_cf = (1 - ratio) * np.exp(-Cc4 / 2) * (dAc + Ac * (2 * lc2 - Cc4 * lc2) / l_cf ** 5)
+    dr = np.exp(-Cd4 / 2) * Ad / ld2 - np.exp(-Cc4 / 2) * Ac / lc2
+    return np.sum(g_df * dL_dK), np.sum(g_cf * dL_dK), np.sum(dr * dL_dK)
+
+
+# --------------------------------------------------------------------------------------
 # Index / grid work (bit-exact)
 # --------------------------------------------------------------------------------------
 def split_indices(n, step):

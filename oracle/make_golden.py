@@ -256,6 +256,69 @@ def gen_sklearn(out):
                         mean=np.asarray(U).reshape(-1), std=np.asarray(Ustd).reshape(-1))
 
 
+def gen_lml(gs, out):
+    """Log marginal likelihood + gradient fixtures.
+
+    vector kernels: K from the reference's own myKernel (GP_scripts.py:6-42) at N=300
+    synthetic tracks; LML by Cholesky; the gradient by a 4-point central difference of that
+    LML in each hyperparameter (l_df, l_cf, rate) — the reference's analytic gradient
+    (myKernel.py:59-105) is not a derivative — and ∂/∂noise exactly.
+    ARD: scikit-learn's log_marginal_likelihood(theta, eval_gradient=True) for the
+    krig.scikit_prior model (krig.py:174-180) at N=128, gradient mapped from log-space."""
+    import scipy.linalg as sla
+    from sklearn.gaussian_process import GaussianProcessRegressor, kernels
+    x, y, u, v = synthetic_tracks(300, seed=7)
+    xa = np.stack([x, y], 1)
+    obs = np.concatenate([u, v])
+    d = dict(x=x, y=y, u=u, v=v)
+
+    def lml(p):
+        K = gs["myKernel"](xa, xa, p[0], p[1], p[2]) + np.identity(2 * xa.shape[0]) * p[3]
+        L = np.linalg.cholesky(K)
+        a = sla.cho_solve((L, True), obs)
+        return -0.5 * obs @ a - np.sum(np.log(np.diag(L))) - 0.5 * obs.size * np.log(2 * np.pi), L, a
+
+    cases = [("df", [4.0, 5.0, 1.0, 0.0025]), ("cf", [5.0, 3.5, 0.0, 0.0025]),
+             ("mixed", [6.0, 4.0, 0.4, 0.01])]
+    for name, p in cases:
+        val, L, a = lml(p)
+        g = np.zeros(4)
+        for i in range(3):
+            if (name == "df" and i != 0) or (name == "cf" and i != 1):
+                continue
+            h = 1e-4 * (p[i] if i < 2 else 1.0)
+            f = []
+            for t in (-2, -1, 1, 2):
+                q = list(p)
+                q[i] += t * h
+                f.append(lml(q)[0])
+            g[i] = (f[0] - 8 * f[1] + 8 * f[2] - f[3]) / (12 * h)
+        Ki = sla.cho_solve((L, True), np.identity(L.shape[0]))
+        g[3] = 0.5 * (a @ a - np.trace(Ki))
+        d[f"{name}_params"] = np.array(p)
+        d[f"{name}_lml"] = np.array(val)
+        d[f"{name}_grad"] = g
+    np.savez_compressed(os.path.join(out, "lml_vector_N300.npz"), **d)
+
+    rng = np.random.default_rng(12)
+    N = 128
+    X = np.stack([rng.uniform(0, 6, N), rng.uniform(0, 20, N), rng.uniform(-5, 15, N)], 1)
+    uu = np.sin(X[:, 1] / 4) * np.cos(X[:, 2] / 5) + 0.1 * X[:, 0] / 6 + rng.normal(0, 0.05, N)
+    e = dict(X=X, u=uu)
+    for T, HP in ((1, np.array([0.8, 3.0, 4.0, 5.0, 0.004])),
+                  (2, np.array([0.8, 3.0, 4.0, 5.0, 0.2, 10.0, 1.5, 2.0, 0.004]))):
+        k = HP[0] * kernels.RBF(length_scale=list(HP[1:4]))
+        if T == 2:
+            k = k + HP[4] * kernels.RBF(length_scale=list(HP[5:8]))
+        k = k + kernels.WhiteKernel(noise_level=HP[-1])
+        model = GaussianProcessRegressor(kernel=k, optimizer=None).fit(X, uu)
+        val, glog = model.log_marginal_likelihood(model.kernel_.theta, eval_gradient=True)
+        e[f"T{T}_HP"] = HP
+        e[f"T{T}_lml"] = np.array(val)
+        e[f"T{T}_grad"] = np.asarray(glog) / HP   # ∂/∂x = ∂/∂log x ÷ x
+    np.savez_compressed(os.path.join(out, "lml_sklearn_ard_N128.npz"), **e)
+
+
 def gen_indices(out):
     """Split index arrays, verbatim reference expression (GP_laser.py:81-83, krig.py:335-337)."""
     sizes = list(range(30, 40)) + list(range(128, 140)) + [257, 1000, 1031, 3000, 12288]
@@ -298,7 +361,8 @@ def main():
     gs = load_gp_scripts()
     jobs = dict(small=lambda: gen_small(gs, a.out), laser=lambda: gen_laser(gs, a.out),
                 mykernel=lambda: gen_mykernel(gs, a.out), sklearn=lambda: gen_sklearn(a.out),
-                indices=lambda: gen_indices(a.out), grids=lambda: gen_grids(a.out))
+                indices=lambda: gen_indices(a.out), grids=lambda: gen_grids(a.out),
+                lml=lambda: gen_lml(gs, a.out))
     for name, fn in jobs.items():
         if a.only and name not in a.only.split(","):
             continue

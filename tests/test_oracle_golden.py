@@ -132,3 +132,52 @@ def test_known_answers():
                                 method="inv")
         assert np.allclose(mu, [1.0, 0.0], atol=1e-12)
         assert np.allclose(var, 0.0, atol=1e-9)
+
+
+# ------------------------------------------------------------------ LML
+@pytest.mark.parametrize("name,kind", [("df", "df"), ("cf", "cf"), ("mixed", "mixed")])
+def test_vector_lml_golden(golden, name, kind):
+    """Oracle LML / gradient vs the fixture built on the reference's own myKernel
+    (GP_scripts.py:6-42): value 1e-10 relative; gradient (both finite-difference based,
+    4-point stencils) 1e-6 relative to the largest entry."""
+    g = golden("lml_vector_N300.npz")
+    x = np.stack([g["x"], g["y"]], 1)
+    y = np.concatenate([g["u"], g["v"]])
+    l_df, l_cf, rate, noise = g[f"{name}_params"]
+    val, grad = O.vector_lml(x, y, kind=kind, l_df=l_df, l_cf=l_cf, ratio=rate, noise=noise, eval_gradient=True)
+    assert abs(val - float(g[f"{name}_lml"])) <= 1e-10 * abs(float(g[f"{name}_lml"]))
+    assert rel_err(grad, g[f"{name}_grad"]) < 1e-6
+
+
+@pytest.mark.parametrize("T", [1, 2])
+def test_ard_lml_sklearn(golden, T):
+    """Oracle ARD LML / analytic gradient vs scikit-learn's log_marginal_likelihood
+    (_gpr.py:584-650, alpha=1e-10 jitter) — value and gradient 1e-10 relative."""
+    g = golden("lml_sklearn_ard_N128.npz")
+    HP = g[f"T{T}_HP"]
+    var = [HP[0]] + ([HP[4]] if T == 2 else [])
+    ls = [tuple(HP[1:4])] + ([tuple(HP[5:8])] if T == 2 else [])
+    val, grad = O.ard_lml(g["X"], g["u"], var, ls, HP[-1], jitter=1e-10, eval_gradient=True)
+    assert abs(val - float(g[f"T{T}_lml"])) <= 1e-10 * abs(float(g[f"T{T}_lml"]))
+    assert rel_err(grad, g[f"T{T}_grad"]) < 1e-10
+
+
+def test_reference_gradient_quirk():
+    """the reference's myKernel.update_gradients_full (myKernel.py:59-105) is not
+    the derivative of myKernel.K — its length-scale entries disagree with finite differences,
+    while its ratio entry agrees.  The build implements the exact derivative."""
+    import scipy.linalg as sla
+    rng = np.random.default_rng(5)
+    n = 80
+    x = np.stack([rng.uniform(0, 30, n), rng.uniform(0, 20, n)], 1)
+    y = rng.normal(0, 1, 2 * n)
+    kw = dict(kind="mixed", l_df=4.0, l_cf=6.0, ratio=0.3, noise=0.01)
+    _, g = O.vector_lml(x, y, eval_gradient=True, **kw)
+    K = O.vector_kernel(x, x, kind="mixed", l_df=4.0, l_cf=6.0, ratio=0.3) + 0.01 * np.eye(2 * n)
+    L = np.linalg.cholesky(K)
+    a = sla.cho_solve((L, True), y)
+    dL_dK = 0.5 * (np.outer(a, a) - sla.cho_solve((L, True), np.eye(2 * n)))
+    r_df, r_cf, r_ratio = O.reference_mykernel_gradient(x, dL_dK, 4.0, 6.0, 0.3)
+    assert abs(r_ratio - g[2]) < 1e-6 * abs(g[2])
+    assert abs(r_df - g[0]) > 1e-2 * abs(g[0])
+    assert abs(r_cf - g[1]) > 1e-2 * abs(g[1])
