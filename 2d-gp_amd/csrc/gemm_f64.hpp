@@ -41,6 +41,7 @@ struct GemmParams {
   double alpha, beta;
   int a_lower;   // A lower-triangular: row block i0 only needs k < i0+BM
   int b_lower;   // (NN) B lower-triangular: column block j0 only needs k >= j0
+  int a_upper;   // A upper-triangular: row block i0 only needs k >= i0
   int c_lower;   // enumerate lower tiles of a square C; diagonal tiles store i >= j
   int rev_rows;  // dispatch heavy (large i0) row blocks first (a_lower)
   int xcd_cols;  // 1-D grid: groups of 8 column tiles × all row blocks, column tile = XCD label
@@ -62,7 +63,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f64_kernel(GemmParams p) {
 
   int bi, bj;
   if (p.c_lower) {
-    tri_tile(blockIdx.x, bi, bj);
+    tri_tile(blockIdx.x, bi, bj);  // top rows first: the heavy ones under a_upper
   } else if (p.xcd_cols) {
     // Blocks b and b+8 share an XCD (round-robin dispatch).  Give every XCD one column
     // tile of the current group of 8 and all row blocks: the K*ᵀ column panel slabs are
@@ -87,7 +88,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f64_kernel(GemmParams p) {
   const double* __restrict__ A = p.A + z * p.sA;
   const double* __restrict__ B = p.B + z * p.sB;
 
-  const int kb = p.b_lower ? j0 : 0;
+  const int kb = max(p.b_lower ? j0 : 0, p.a_upper ? i0 : 0);
   const int ke = p.a_lower ? min(p.K, i0 + GBM) : p.K;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;

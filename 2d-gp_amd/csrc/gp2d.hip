@@ -615,16 +615,16 @@ int gp2d_lml_grad(const double* W, int64_t n, int64_t ldw, const double* alpha, 
   double* V = reinterpret_cast<double*>(work);
   double* C = V + (size_t)n * n;
   double* partial = C + (size_t)n * n;
-  // V = J Wᵀ J (lower), C = V Vᵀ = J K_y⁻¹ J, lower tiles only
-  rev_transpose_kernel<<<dim3((unsigned)(n / 64), (unsigned)(n / 64)), 256, 0, s>>>(W, n, ldw, V);
-  GP2D_CHECK(check_launch("rev_transpose_kernel"));
+  // Wt = Wᵀ (upper), C = Wt·W = K_y⁻¹, lower tiles only
+  transpose_kernel<<<dim3((unsigned)(n / 64), (unsigned)(n / 64)), 256, 0, s>>>(W, n, ldw, V);
+  GP2D_CHECK(check_launch("transpose_kernel"));
   GemmParams p = gemm_params();
   p.A = V; p.lda = n;
-  p.B = V; p.ldb = n;
+  p.B = W; p.ldb = ldw;
   p.C = C; p.ldc = n;
   p.M = (int)n; p.N = (int)n; p.K = (int)n;
-  p.a_lower = 1; p.c_lower = 1;
-  GP2D_CHECK((launch_gemm<true, EPI_STORE>(p, 1, s)));
+  p.a_upper = 1; p.c_lower = 1;
+  GP2D_CHECK((launch_gemm<false, EPI_STORE>(p, 1, s)));
   const dim3 grid((unsigned)(ntr_pad / PT_TILE), (unsigned)((ntr + LML_ROWS - 1) / LML_ROWS));
   if (k->family == GP2D_FAMILY_VECTOR2D) {
     VecGradParams gp{make_vec_params(k), k->l_df, k->l_cf};
@@ -635,7 +635,7 @@ int gp2d_lml_grad(const double* W, int64_t n, int64_t ldw, const double* alpha, 
     GP2D_CHECK(check_launch("lml_grad_ard_kernel"));
   }
   const SlotMap sm = grad_slots(k, true);
-  grad_sum_kernel<<<sm.ng, 64, 0, s>>>(partial, grad_blocks(ntr_pad, ntr), sm, 0.5, grad_dev);
+  grad_sum_kernel<<<sm.ng, 256, 0, s>>>(partial, grad_blocks(ntr_pad, ntr), sm, 0.5, grad_dev);
   return check_launch("grad_sum_kernel");
 }
 
@@ -665,7 +665,7 @@ int gp2d_kernel_grad(const double* xa, int64_t na, const double* xb, int64_t nb,
     GP2D_CHECK(check_launch("kgrad_ard_kernel"));
   }
   const SlotMap sm = grad_slots(k, false);
-  grad_sum_kernel<<<sm.ng, 64, 0, s>>>(partial, grad_blocks(nbp, na), sm, 1.0, grad_dev);
+  grad_sum_kernel<<<sm.ng, 256, 0, s>>>(partial, grad_blocks(nbp, na), sm, 1.0, grad_dev);
   return check_launch("grad_sum_kernel");
 }
 

@@ -7,18 +7,15 @@
 //   LML      = −½ yᵀα − Σ_i log L_ii − (n_obs/2) log 2π          α = K_y⁻¹ y
 //   ∂LML/∂θ  = ½ tr((ααᵀ − K_y⁻¹) ∂K_y/∂θ)
 //
-// From the fitted W = L⁻¹: log L_ii = −log W_ii, and K_y⁻¹ = WᵀW.  K_y⁻¹ is formed
-// as C = V·Vᵀ with V = J·Wᵀ·J (J reverses the index order), which makes V lower
-// triangular, so the existing lower-tile FP64 MFMA GEMM (c_lower + a_lower,
-// n³/3 flops) applies: C[n−1−a][n−1−b] = (K_y⁻¹)_ab, lower triangle only.
+// From the fitted W = L⁻¹: log L_ii = −log W_ii, and K_y⁻¹ = WᵀW, formed as the
+// lower tiles of the NN product Wᵀ·W on the FP64 MFMA GEMM (c_lower; Wᵀ upper
+// triangular, so row block i only needs k ≥ i: a_upper; n³/3 flops).
 //
 // The trace is one fused pass: a thread per training-point pair (p, q) regenerates
 // the 2×2 block ∂K/∂θ on the fly (no n×n derivative matrices are stored) and
-// contracts it with the stored entries of ααᵀ − K_y⁻¹:
-//   uv block: every pair, weight 2 (the vu block is its transpose);
-//   uu, vv blocks: pairs p ≤ q, weight 2 off the diagonal, 1 on it.
-// Reading only (n−1−a ≥ n−1−b) entries keeps every access inside C's stored
-// lower triangle.  Per-block partial sums are reduced in a fixed order, so the
+// contracts it with the stored (row ≥ column) entries of ααᵀ − K_y⁻¹:
+//   vu block (np+p, q): every pair, weight 2 (the uv block is its transpose);
+//   uu, vv blocks: pairs p ≥ q, weight 2 off the diagonal, 1 on it.  Per-block partial sums are reduced in a fixed order, so the
 // result is deterministic.
 //
 // The reference's own gradient (myKernel.update_gradients_full, myKernel.py:59-105)
@@ -34,18 +31,17 @@ namespace gp2d {
 constexpr int LML_MAXG = 9;   // ARD: 2 variances + 2×3 length scales + noise
 constexpr int LML_ROWS = 16;  // row points per block (4 per thread row)
 
-// V[i][k] = W[n−1−k][n−1−i]: reversed transpose through a 64×65 LDS tile.
-__global__ __launch_bounds__(256) void rev_transpose_kernel(const double* __restrict__ W, int64_t n, int64_t ldw,
-                                                            double* __restrict__ V) {
+// Wt = Wᵀ through a 64×65 LDS tile (both sides coalesced).
+__global__ __launch_bounds__(256) void transpose_kernel(const double* __restrict__ W, int64_t n, int64_t ldw,
+                                                        double* __restrict__ Wt) {
   __shared__ double t[64][65];
   const int64_t r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;  // source tile of W
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
 #pragma unroll 4
   for (int r = ty; r < 64; r += 4) t[r][tx] = W[(r0 + r) * ldw + c0 + tx];
   __syncthreads();
-  // W[r0+r][c0+c] goes to V[n−1−c0−c][n−1−r0−r]
 #pragma unroll 4
-  for (int c = ty; c < 64; c += 4) V[(n - 1 - c0 - c) * n + (n - 1 - r0 - tx)] = t[tx][c];
+  for (int c = ty; c < 64; c += 4) Wt[(c0 + c) * n + r0 + tx] = t[tx][c];
 }
 
 // LML = −½ Σ y_i α_i + Σ log W_ii − (n_obs/2) log 2π (padded rows: W_ii = 1, y_i = 0) — one block,
@@ -204,7 +200,7 @@ __device__ __forceinline__ void load_point(const double* x, int64_t i, int dim, 
 
 // Vector family: partial[block][slots 0..3] = Σ over the block's pairs of
 // (ααᵀ − K_y⁻¹) ⊙ ∂K/∂(ℓ_df, ℓ_cf, ratio) and the noise term Σ_diag (α_a² − K_y⁻¹_aa).
-// Grid (ntr_pad/64, ceil(ntr/16)); C = reversed K_y⁻¹ (lower triangle), n × n.
+// Grid (ntr_pad/64, ceil(ntr/16)); C = K_y⁻¹, lower triangle, n × n.
 __global__ __launch_bounds__(256) void lml_grad_vec_kernel(const double* __restrict__ C, int64_t n,
                                                            const double* __restrict__ alpha,
                                                            const double* __restrict__ x, int64_t ntr, int64_t np,
@@ -216,29 +212,29 @@ __global__ __launch_bounds__(256) void lml_grad_vec_kernel(const double* __restr
   if (q < ntr) {
     const double b1 = x[2 * q], b2 = x[2 * q + 1];
     const double aqu = alpha[q], aqv = alpha[np + q];
-    const int64_t cqu = n - 1 - q, cqv = n - 1 - (np + q);  // reversed column indices
 #pragma unroll 1
     for (int r = 0; r < LML_ROWS / 4; ++r) {
       const int64_t p = (int64_t)blockIdx.y * LML_ROWS + ty + 4 * r;
       if (p >= ntr) break;
       const double apu = alpha[p], apv = alpha[np + p];
-      const int64_t rpu = (n - 1 - p) * n, rpv = (n - 1 - (np + p)) * n;
-      // uv entry (p, np+q): stored at C[n−1−p][n−1−np−q]; weight 2 (vu is its transpose)
-      const double muv = apu * aqv - C[rpu + cqv];
+      const double* cu = C + p * n;          // row p (u)
+      const double* cv = C + (np + p) * n;   // row np+p (v)
+      // vu entry (np+p, q): always in the stored triangle; weight 2 (uv is its transpose)
+      const double mvu = apv * aqu - cv[q];
       double w11 = 0.0, w22 = 0.0;
-      if (p <= q) {
+      if (p >= q) {
         const double wt = (p == q) ? 1.0 : 2.0;
-        w11 = wt * (apu * aqu - C[rpu + cqu]);
-        w22 = wt * (apv * aqv - C[rpv + cqv]);
+        w11 = wt * (apu * aqu - cu[q]);
+        w22 = wt * (apv * aqv - cv[np + q]);
         if (p == q) acc[3] += w11 + w22;
       }
-      vec_grad_accum(gp, x[2 * p] - b1, x[2 * p + 1] - b2, w11, 2.0 * muv, w22, acc);
+      vec_grad_accum(gp, x[2 * p] - b1, x[2 * p + 1] - b2, w11, 2.0 * mvu, w22, acc);
     }
   }
   block_reduce_vec<4>(acc, red, partial + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * LML_MAXG);
 }
 
-// ARD family (slots t·4 + {0: var, 1+d: ls_d}, 8: noise); pairs p ≤ q of the stored triangle.
+// ARD family (slots t·4 + {0: var, 1+d: ls_d}, 8: noise); pairs p ≥ q of the stored triangle.
 __global__ __launch_bounds__(256) void lml_grad_ard_kernel(const double* __restrict__ C, int64_t n,
                                                            const double* __restrict__ alpha,
                                                            const double* __restrict__ x, int64_t ntr, ArdParams ap,
@@ -253,12 +249,12 @@ __global__ __launch_bounds__(256) void lml_grad_ard_kernel(const double* __restr
     double b[3], a[3];
     load_point(x, q, ap.dim, b);
     const double aq = alpha[q];
-    const int64_t cq = n - 1 - q;
 #pragma unroll 1
     for (int r = 0; r < LML_ROWS / 4; ++r) {
       const int64_t p = (int64_t)blockIdx.y * LML_ROWS + ty + 4 * r;
-      if (p >= ntr || p > q) break;
-      const double wt = ((p == q) ? 1.0 : 2.0) * (alpha[p] * aq - C[(n - 1 - p) * n + cq]);
+      if (p >= ntr) break;
+      if (p < q) continue;
+      const double wt = ((p == q) ? 1.0 : 2.0) * (alpha[p] * aq - C[p * n + q]);
       load_point(x, p, ap.dim, a);
       ard_grad_accum(ap, a, b, wt, acc);
       if (p == q) acc[8] += wt;
@@ -316,16 +312,16 @@ __global__ __launch_bounds__(256) void kgrad_ard_kernel(const double* __restrict
   block_reduce_vec<LML_MAXG>(acc, red, partial + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * LML_MAXG);
 }
 
-// out[g] = scale · Σ_blocks partial[block][slot[g]], fixed order (one wave per output entry).
-__global__ __launch_bounds__(64) void grad_sum_kernel(const double* __restrict__ partial, int64_t nblk, SlotMap sm,
-                                                      double scale, double* __restrict__ out) {
-  const int g = blockIdx.x, lane = threadIdx.x;
-  const int slot = sm.slot[g];
+// out[g] = scale · Σ_blocks partial[block][slot[g]], fixed order (one 256-thread block per entry).
+__global__ __launch_bounds__(256) void grad_sum_kernel(const double* __restrict__ partial, int64_t nblk, SlotMap sm,
+                                                       double scale, double* __restrict__ out) {
+  __shared__ double red[1][256];
+  const int slot = sm.slot[blockIdx.x];
   double s = 0.0;
-  for (int64_t b = lane; b < nblk; b += 64) s += partial[b * LML_MAXG + slot];
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-  if (lane == 0) out[g] = scale * s;
+  for (int64_t b = threadIdx.x; b < nblk; b += 256) s += partial[b * LML_MAXG + slot];
+  double tot = 0.0;
+  block_reduce_vec<1>(&s, red, &tot);  // thread 0 receives the total
+  if (threadIdx.x == 0) out[blockIdx.x] = scale * tot;
 }
 
 }  // namespace gp2d
