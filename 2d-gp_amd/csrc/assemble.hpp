@@ -19,6 +19,8 @@ namespace gp2d {
 
 struct VecParams {
   int kind;
+  int pdim;               // point stride: 2 (x1, x2), or 3 (t, x1, x2) for the spatio-temporal product
+  double var_t, ilt2;     // temporal factor var_t·exp(−Δt²·ilt2/2) (pdim = 3)
   double il_df2, il_cf2;  // 1/ℓ²
   double l_df2;           // ℓ² (scalar kind: the σ² factor of GP_scripts.py:68)
   double ratio, cratio;   // ratio, 1 − ratio
@@ -40,6 +42,9 @@ inline VecParams make_vec_params(const gp2d_kernel_t* k) {
   p.ratio = k->ratio;
   p.cratio = 1.0 - k->ratio;
   p.same_len = (k->l_df == k->l_cf);
+  p.pdim = (k->family == GP2D_FAMILY_VECTOR_ST) ? 3 : 2;
+  p.var_t = (p.pdim == 3) ? k->var[0] : 1.0;
+  p.ilt2 = (p.pdim == 3) ? 1.0 / (k->ls[0][0] * k->ls[0][0]) : 0.0;
   return p;
 }
 
@@ -89,6 +94,31 @@ __device__ __forceinline__ void vec_block(const VecParams& p, double d1, double 
   k22 = p.ratio * f22 + p.cratio * g22;
 }
 
+// Coordinates of vector-family point i: time (0 for the purely spatial family) and (x1, x2).
+__device__ __forceinline__ void vec_point(const VecParams& p, const double* __restrict__ x, int64_t i, double& t,
+                                          double& a, double& b) {
+  if (p.pdim == 3) {
+    t = x[3 * i]; a = x[3 * i + 1]; b = x[3 * i + 2];
+  } else {
+    t = 0.0; a = x[2 * i]; b = x[2 * i + 1];
+  }
+}
+
+// Temporal factor of the spatio-temporal product (GPy RBF on t, myKernel.py:349-352); 1 otherwise.
+__device__ __forceinline__ double time_factor(const VecParams& p, double dt) {
+  return (p.pdim == 3) ? p.var_t * exp(-0.5 * dt * dt * p.ilt2) : 1.0;
+}
+
+// Full 2×2 block of a vector-family kernel: spatial block × temporal factor.
+__device__ __forceinline__ void vec_block_st(const VecParams& p, double dt, double d1, double d2, double& k11,
+                                             double& k12, double& k22) {
+  vec_block(p, d1, d2, k11, k12, k22);
+  if (p.pdim == 3) {
+    const double f = time_factor(p, dt);
+    k11 *= f; k12 *= f; k22 *= f;
+  }
+}
+
 __device__ __forceinline__ double ard_value(const ArdParams& p, const double* a, const double* b) {
   double k = 0.0;
   for (int t = 0; t < p.nterms; ++t) {
@@ -113,15 +143,17 @@ __global__ __launch_bounds__(256) void assemble_vec_kernel(
   const int64_t j = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
   const int ty = threadIdx.x >> 6;
   const bool jv = j < nb;
-  const double b1 = jv ? xb[2 * j] : 0.0;
-  const double b2 = jv ? xb[2 * j + 1] : 0.0;
+  double b0 = 0.0, b1 = 0.0, b2 = 0.0;
+  if (jv) vec_point(p, xb, j, b0, b1, b2);
 #pragma unroll 1
   for (int q = 0; q < ASM_ROWS / 4; ++q) {
     const int64_t i = (int64_t)blockIdx.y * ASM_ROWS + ty + 4 * q;
     if (i >= na_pad) break;
     double k11, k12, k22;
     if (jv && i < na) {
-      vec_block(p, xa[2 * i] - b1, xa[2 * i + 1] - b2, k11, k12, k22);
+      double a0, a1, a2;
+      vec_point(p, xa, i, a0, a1, a2);
+      vec_block_st(p, a0 - b0, a1 - b1, a2 - b2, k11, k12, k22);
       if (symmetric && i == j) { k11 += diag_add; k22 += diag_add; }
     } else {
       const double dd = (symmetric && i == j) ? 1.0 : 0.0;  // padded points: identity rows

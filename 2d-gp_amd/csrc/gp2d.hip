@@ -40,12 +40,23 @@ struct Timing {
 };
 static Timing g_timing;
 
+static bool is_vector_family(const gp2d_kernel_t* k) {
+  return k->family == GP2D_FAMILY_VECTOR2D || k->family == GP2D_FAMILY_VECTOR_ST;
+}
+
+// coordinates per point: (x1, x2), (t, x1, x2), or the ARD dimension
+static int point_dim(const gp2d_kernel_t* k) {
+  return k->family == GP2D_FAMILY_VECTOR2D ? 2 : (k->family == GP2D_FAMILY_VECTOR_ST ? 3 : k->dim);
+}
+
 static int validate_kernel(const gp2d_kernel_t* k) {
   GP2D_REQUIRE(k != nullptr, "kernel descriptor is NULL");
-  if (k->family == GP2D_FAMILY_VECTOR2D) {
+  if (is_vector_family(k)) {
     GP2D_REQUIRE(k->kind >= 0 && k->kind <= 3, "vector2d kind must be 0..3");
     GP2D_REQUIRE(k->l_df > 0.0, "l_df must be > 0");
     if (k->kind == GP2D_KIND_CURLFREE || k->kind == GP2D_KIND_MIXED) GP2D_REQUIRE(k->l_cf > 0.0, "l_cf must be > 0");
+    if (k->family == GP2D_FAMILY_VECTOR_ST)
+      GP2D_REQUIRE(k->var[0] > 0.0 && k->ls[0][0] > 0.0, "spatio-temporal var_t and l_t must be > 0");
   } else if (k->family == GP2D_FAMILY_ARD_RBF) {
     GP2D_REQUIRE(k->dim >= 1 && k->dim <= 3, "ARD dim must be 1..3");
     GP2D_REQUIRE(k->nterms >= 1 && k->nterms <= 2, "ARD nterms must be 1..2");
@@ -65,7 +76,7 @@ static int assemble_impl(const double* xa, int64_t na, int64_t na_pad, const dou
   GP2D_REQUIRE(na_pad % PT_TILE == 0 && nb_pad % PT_TILE == 0, "padded point counts must be multiples of 64");
   GP2D_REQUIRE(na <= na_pad && nb <= nb_pad && na >= 0 && nb >= 0, "point counts exceed padded counts");
   if (na_pad == 0 || nb_pad == 0) return 0;
-  const int bd = (k->family == GP2D_FAMILY_VECTOR2D) ? 2 : 1;
+  const int bd = is_vector_family(k) ? 2 : 1;
   GP2D_REQUIRE(ld >= bd * nb_pad, "ld too small");
   dim3 grid(nb_pad / 64, (na_pad + ASM_ROWS - 1) / ASM_ROWS);
   if (bd == 2) {
@@ -106,12 +117,14 @@ static int64_t modinv(int64_t a, int64_t m) {  // a⁻¹ mod m (a, m coprime)
 }
 
 static double kstar_bound(const gp2d_kernel_t* k) {
-  // |K*| entries: div-free and curl-free parts are each bounded by 1/ℓ² (see ozaki.hpp)
+  // |K*| entries: div-free and curl-free parts are each bounded by 1/ℓ² (see ozaki.hpp);
+  // the temporal factor of the spatio-temporal product is ≤ var_t
+  const double vt = (k->family == GP2D_FAMILY_VECTOR_ST) ? k->var[0] : 1.0;
   switch (k->kind) {
-    case GP2D_KIND_SCALAR: return 1.0;
-    case GP2D_KIND_DIVFREE: return 1.0 / (k->l_df * k->l_df);
-    case GP2D_KIND_CURLFREE: return 1.0 / (k->l_cf * k->l_cf);
-    default: return std::max(1.0 / (k->l_df * k->l_df), 1.0 / (k->l_cf * k->l_cf));
+    case GP2D_KIND_SCALAR: return vt;
+    case GP2D_KIND_DIVFREE: return vt / (k->l_df * k->l_df);
+    case GP2D_KIND_CURLFREE: return vt / (k->l_cf * k->l_cf);
+    default: return vt * std::max(1.0 / (k->l_df * k->l_df), 1.0 / (k->l_cf * k->l_cf));
   }
 }
 
@@ -160,11 +173,12 @@ double gp2d_kernel_diag(const gp2d_kernel_t* k) {
     for (int t = 0; t < k->nterms; ++t) s += k->var[t];
     return s;
   }
+  const double vt = (k->family == GP2D_FAMILY_VECTOR_ST) ? k->var[0] : 1.0;  // Kt.Kdiag, myKernel.py:362-363
   switch (k->kind) {
-    case GP2D_KIND_SCALAR: return (1.0 / k->l_df) * (1.0 / k->l_df) * (k->l_df * k->l_df);
-    case GP2D_KIND_DIVFREE: return 1.0 / (k->l_df * k->l_df);
-    case GP2D_KIND_CURLFREE: return 1.0 / (k->l_cf * k->l_cf);
-    default: return k->ratio * (1.0 / (k->l_df * k->l_df)) + (1.0 - k->ratio) * (1.0 / (k->l_cf * k->l_cf));
+    case GP2D_KIND_SCALAR: return vt * ((1.0 / k->l_df) * (1.0 / k->l_df) * (k->l_df * k->l_df));
+    case GP2D_KIND_DIVFREE: return vt * (1.0 / (k->l_df * k->l_df));
+    case GP2D_KIND_CURLFREE: return vt * (1.0 / (k->l_cf * k->l_cf));
+    default: return vt * (k->ratio * (1.0 / (k->l_df * k->l_df)) + (1.0 - k->ratio) * (1.0 / (k->l_cf * k->l_cf)));
   }
 }
 
@@ -376,7 +390,7 @@ int gp2d_predict(const double* W, int64_t n, int64_t ldw, const double* alpha, c
   const double kss = gp2d_kernel_diag(k);
   const double add = (var_mode == GP2D_VAR_LATENT) ? 0.0 : noise;
   const int clip = (var_mode == GP2D_VAR_CLIPPED);
-  const int dim = (k->family == GP2D_FAMILY_VECTOR2D) ? 2 : k->dim;
+  const int dim = point_dim(k);
 
   for (int64_t c0 = 0; c0 < m; c0 += chunk) {
     const int64_t cv = std::min<int64_t>(chunk, m - c0);
@@ -428,7 +442,7 @@ size_t gp2d_ozaki_wres_bytes(int64_t n) {
 int gp2d_ozaki_prepare(const double* W, int64_t n, int64_t ldw, const gp2d_kernel_t* k, int8_t* wres,
                        double* rowscale, int* nmod_out, void* stream) {
   GP2D_CHECK(validate_kernel(k));
-  GP2D_REQUIRE(k->family == GP2D_FAMILY_VECTOR2D, "ozaki: vector2d family only");
+  GP2D_REQUIRE(is_vector_family(k), "ozaki: vector families only");
   GP2D_REQUIRE(n % IBM == 0 && n > 0, "ozaki: n must be a positive multiple of 256");
   GP2D_REQUIRE(nmod_out != nullptr, "ozaki: nmod_out is NULL");
   hipStream_t s = S(stream);
@@ -486,7 +500,7 @@ int gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int nmod, int
                        int var_mode, double noise, int compute_var, double* mean, double* var, int64_t chunk,
                        void* work, size_t work_bytes, void* stream) {
   GP2D_CHECK(validate_kernel(k));
-  GP2D_REQUIRE(k->family == GP2D_FAMILY_VECTOR2D, "ozaki: vector2d family only");
+  GP2D_REQUIRE(is_vector_family(k), "ozaki: vector families only");
   GP2D_REQUIRE(n == 2 * ntr_pad && n % IBM == 0, "ozaki: n must equal 2·ntr_pad and be a multiple of 256");
   GP2D_REQUIRE(chunk > 0 && chunk % (IBN / 2) == 0, "ozaki: chunk must be a positive multiple of 128");
   GP2D_REQUIRE(work != nullptr && work_bytes >= gp2d_predict_ozaki_workspace(n, chunk), "ozaki: workspace too small");
@@ -515,7 +529,7 @@ int gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int nmod, int
     const int64_t cp = round_up(cv, IBN);   // whole 256-row tiles per component half (B aliasing)
     const int64_t ncols = 2 * cp;
     ozaki_kstar_kernel<<<dim3((unsigned)nmseg, (unsigned)(cp / OZ_KS_P)), 256, 0, s>>>(
-        xtr, ntr, ntr_pad, xg + 2 * c0, cv, cp, vp, alpha, compute_var ? oc : oc_mean_only, bres, pm);
+        xtr, ntr, ntr_pad, xg + point_dim(k) * c0, cv, cp, vp, alpha, compute_var ? oc : oc_mean_only, bres, pm);
     GP2D_CHECK(check_launch("ozaki_kstar_kernel"));
     if (compute_var) {
       hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -561,6 +575,7 @@ int gp2d_lml(const double* W, int64_t n, int64_t ldw, const double* alpha, const
 int gp2d_lml_grad_count(const gp2d_kernel_t* k) {
   if (validate_kernel(k) != 0) return -2;
   if (k->family == GP2D_FAMILY_VECTOR2D) return 4;
+  if (k->family == GP2D_FAMILY_VECTOR_ST) return 6;
   return k->nterms * (1 + k->dim) + 1;
 }
 
@@ -576,8 +591,9 @@ namespace {
 SlotMap grad_slots(const gp2d_kernel_t* k, bool with_noise) {
   SlotMap m{};
   m.ng = 0;
-  if (k->family == GP2D_FAMILY_VECTOR2D) {
+  if (k->family == GP2D_FAMILY_VECTOR2D || k->family == GP2D_FAMILY_VECTOR_ST) {
     for (int a = 0; a < 3; ++a) m.slot[m.ng++] = a;
+    if (k->family == GP2D_FAMILY_VECTOR_ST) { m.slot[m.ng++] = 4; m.slot[m.ng++] = 5; }
     if (with_noise) m.slot[m.ng++] = 3;
   } else {
     for (int t = 0; t < k->nterms; ++t) {
@@ -626,8 +642,8 @@ int gp2d_lml_grad(const double* W, int64_t n, int64_t ldw, const double* alpha, 
   p.a_upper = 1; p.c_lower = 1;
   GP2D_CHECK((launch_gemm<false, EPI_STORE>(p, 1, s)));
   const dim3 grid((unsigned)(ntr_pad / PT_TILE), (unsigned)((ntr + LML_ROWS - 1) / LML_ROWS));
-  if (k->family == GP2D_FAMILY_VECTOR2D) {
-    VecGradParams gp{make_vec_params(k), k->l_df, k->l_cf};
+  if (is_vector_family(k)) {
+    VecGradParams gp{make_vec_params(k), k->l_df, k->l_cf, k->ls[0][0]};
     lml_grad_vec_kernel<<<grid, 256, 0, s>>>(C, n, alpha, xtr, ntr, ntr_pad, gp, partial);
     GP2D_CHECK(check_launch("lml_grad_vec_kernel"));
   } else {
@@ -656,8 +672,8 @@ int gp2d_kernel_grad(const double* xa, int64_t na, const double* xb, int64_t nb,
   double* partial = reinterpret_cast<double*>(work);
   const int64_t nbp = round_up(nb, PT_TILE);
   const dim3 grid((unsigned)(nbp / PT_TILE), (unsigned)((na + LML_ROWS - 1) / LML_ROWS));
-  if (k->family == GP2D_FAMILY_VECTOR2D) {
-    VecGradParams gp{make_vec_params(k), k->l_df, k->l_cf};
+  if (is_vector_family(k)) {
+    VecGradParams gp{make_vec_params(k), k->l_df, k->l_cf, k->ls[0][0]};
     kgrad_vec_kernel<<<grid, 256, 0, s>>>(xa, na, xb, nb, gp, dL_dK, ld, partial);
     GP2D_CHECK(check_launch("kgrad_vec_kernel"));
   } else {

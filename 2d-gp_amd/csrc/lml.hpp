@@ -78,7 +78,7 @@ __global__ __launch_bounds__(256) void lml_terms_kernel(const double* __restrict
 // Scalar kind (σ = ℓ_df): K = exp(−r²/(2σ²)), ∂K/∂σ = K r²/σ³ (all four entries).
 struct VecGradParams {
   VecParams p;
-  double l_df, l_cf;
+  double l_df, l_cf, l_t;
 };
 
 __device__ __forceinline__ void vec_block_grad(const VecGradParams& gp, double d1, double d2, double g[3][3]) {
@@ -153,19 +153,32 @@ __device__ __forceinline__ void block_reduce_vec(const double* v, double (*red)[
 }
 
 // Gradient accumulators live in fixed slots so that every index is a compile-time constant
-// (no scratch): vector2d 0 = l_df, 1 = l_cf, 2 = ratio, 3 = noise; ARD t·4 = var_t,
-// t·4+1+d = ls_td, 8 = noise.  SlotMap lists the slots in the output order.
+// (no scratch): vector families 0 = l_df, 1 = l_cf, 2 = ratio, 3 = noise, 4 = var_t, 5 = l_t
+// (spatio-temporal product); ARD t·4 = var_t, t·4+1+d = ls_td, 8 = noise.  SlotMap lists the
+// slots in the output order.
 struct SlotMap {
   int ng;
   int slot[LML_MAXG];
 };
 
-__device__ __forceinline__ void vec_grad_accum(const VecGradParams& gp, double d1, double d2, double w11, double w12,
-                                               double w22, double* acc) {
+// Spatio-temporal product K = c_t(Δt)·K_s with c_t = var_t·exp(−Δt²/(2ℓ_t²)):
+//   ∂K/∂θ_s = c_t ∂K_s/∂θ_s,  ∂K/∂var_t = exp(·)·K_s,  ∂K/∂ℓ_t = c_t·Δt²/ℓ_t³·K_s.
+__device__ __forceinline__ void vec_grad_accum(const VecGradParams& gp, double dt, double d1, double d2, double w11,
+                                               double w12, double w22, double* acc) {
   double g[3][3];
   vec_block_grad(gp, d1, d2, g);
+  double ct = 1.0;
+  if (gp.p.pdim == 3) {
+    const double e = exp(-0.5 * dt * dt * gp.p.ilt2);
+    ct = gp.p.var_t * e;
+    double k11, k12, k22;
+    vec_block(gp.p, d1, d2, k11, k12, k22);
+    const double ws = w11 * k11 + w12 * k12 + w22 * k22;
+    acc[4] += e * ws;
+    acc[5] += ct * dt * dt * gp.p.ilt2 / gp.l_t * ws;
+  }
 #pragma unroll
-  for (int a = 0; a < 3; ++a) acc[a] += w11 * g[a][0] + w12 * g[a][1] + w22 * g[a][2];
+  for (int a = 0; a < 3; ++a) acc[a] += ct * (w11 * g[a][0] + w12 * g[a][1] + w22 * g[a][2]);
 }
 
 // ∂k/∂var_t = e_t, ∂k/∂ls_td = var_t·e_t·z_d²/ls_td (z_d = Δ_d/ls_td), weighted by w.
@@ -205,12 +218,13 @@ __global__ __launch_bounds__(256) void lml_grad_vec_kernel(const double* __restr
                                                            const double* __restrict__ alpha,
                                                            const double* __restrict__ x, int64_t ntr, int64_t np,
                                                            VecGradParams gp, double* __restrict__ partial) {
-  __shared__ double red[4][256];
+  __shared__ double red[6][256];
   const int64_t q = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
   const int ty = threadIdx.x >> 6;
-  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
   if (q < ntr) {
-    const double b1 = x[2 * q], b2 = x[2 * q + 1];
+    double b0, b1, b2;
+    vec_point(gp.p, x, q, b0, b1, b2);
     const double aqu = alpha[q], aqv = alpha[np + q];
 #pragma unroll 1
     for (int r = 0; r < LML_ROWS / 4; ++r) {
@@ -228,10 +242,12 @@ __global__ __launch_bounds__(256) void lml_grad_vec_kernel(const double* __restr
         w22 = wt * (apv * aqv - cv[np + q]);
         if (p == q) acc[3] += w11 + w22;
       }
-      vec_grad_accum(gp, x[2 * p] - b1, x[2 * p + 1] - b2, w11, 2.0 * mvu, w22, acc);
+      double a0, a1, a2;
+      vec_point(gp.p, x, p, a0, a1, a2);
+      vec_grad_accum(gp, a0 - b0, a1 - b1, a2 - b2, w11, 2.0 * mvu, w22, acc);
     }
   }
-  block_reduce_vec<4>(acc, red, partial + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * LML_MAXG);
+  block_reduce_vec<6>(acc, red, partial + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * LML_MAXG);
 }
 
 // ARD family (slots t·4 + {0: var, 1+d: ls_d}, 8: noise); pairs p ≥ q of the stored triangle.
@@ -270,22 +286,25 @@ __global__ __launch_bounds__(256) void kgrad_vec_kernel(const double* __restrict
                                                         const double* __restrict__ xb, int64_t nb, VecGradParams gp,
                                                         const double* __restrict__ G, int64_t ld,
                                                         double* __restrict__ partial) {
-  __shared__ double red[4][256];
+  __shared__ double red[6][256];
   const int64_t q = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
   const int ty = threadIdx.x >> 6;
-  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
   if (q < nb) {
-    const double b1 = xb[2 * q], b2 = xb[2 * q + 1];
+    double b0, b1, b2;
+    vec_point(gp.p, xb, q, b0, b1, b2);
 #pragma unroll 1
     for (int r = 0; r < LML_ROWS / 4; ++r) {
       const int64_t p = (int64_t)blockIdx.y * LML_ROWS + ty + 4 * r;
       if (p >= na) break;
       const double* g0 = G + p * ld;
       const double* g1 = G + (na + p) * ld;
-      vec_grad_accum(gp, xa[2 * p] - b1, xa[2 * p + 1] - b2, g0[q], g0[nb + q] + g1[q], g1[nb + q], acc);
+      double a0, a1, a2;
+      vec_point(gp.p, xa, p, a0, a1, a2);
+      vec_grad_accum(gp, a0 - b0, a1 - b1, a2 - b2, g0[q], g0[nb + q] + g1[q], g1[nb + q], acc);
     }
   }
-  block_reduce_vec<4>(acc, red, partial + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * LML_MAXG);
+  block_reduce_vec<6>(acc, red, partial + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * LML_MAXG);
 }
 
 __global__ __launch_bounds__(256) void kgrad_ard_kernel(const double* __restrict__ xa, int64_t na,

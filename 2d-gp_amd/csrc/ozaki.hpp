@@ -136,14 +136,14 @@ __global__ __launch_bounds__(256) void ozaki_kstar_kernel(
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int64_t t0 = (int64_t)blockIdx.x * OZ_KS_T + 4 * tx;
   const int64_t n = 2 * npad, ncols = 2 * cp;
-  double a1[4], a2[4], x1[4], x2[4];
+  double a1[4], a2[4], x0[4], x1[4], x2[4];
   bool tv[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int64_t t = t0 + u;
     tv[u] = t < ntr;
-    x1[u] = tv[u] ? xtr[2 * t] : 0.0;
-    x2[u] = tv[u] ? xtr[2 * t + 1] : 0.0;
+    x0[u] = x1[u] = x2[u] = 0.0;
+    if (tv[u]) vec_point(vp, xtr, t, x0[u], x1[u], x2[u]);
     a1[u] = (t < npad) ? alpha[t] : 0.0;
     a2[u] = (t < npad) ? alpha[npad + t] : 0.0;
   }
@@ -152,13 +152,14 @@ __global__ __launch_bounds__(256) void ozaki_kstar_kernel(
   for (int q = 0; q < OZ_KS_P / 4; ++q) {
     const int64_t p = (int64_t)blockIdx.y * OZ_KS_P + ty + 4 * q;
     const bool pv = p < cv;
-    const double g1 = pv ? xg[2 * p] : 0.0, g2 = pv ? xg[2 * p + 1] : 0.0;
+    double g0 = 0.0, g1 = 0.0, g2 = 0.0;
+    if (pv) vec_point(vp, xg, p, g0, g1, g2);
     double k11[4], k12[4], k22[4];
     double mu = 0.0, mv = 0.0;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (pv && tv[u]) {
-        vec_block(vp, x1[u] - g1, x2[u] - g2, k11[u], k12[u], k22[u]);
+        vec_block_st(vp, x0[u] - g0, x1[u] - g1, x2[u] - g2, k11[u], k12[u], k22[u]);
       } else {
         k11[u] = k12[u] = k22[u] = 0.0;
       }

@@ -13,7 +13,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GP2D_LIB", os.path.join(_HERE, "libgp2d.so"))
 
-FAMILY_VECTOR2D, FAMILY_ARD_RBF = 0, 1
+FAMILY_VECTOR2D, FAMILY_ARD_RBF, FAMILY_VECTOR_ST = 0, 1, 2
 KIND_SCALAR, KIND_DIVFREE, KIND_CURLFREE, KIND_MIXED = 0, 1, 2, 3
 VAR_LATENT, VAR_NOISY, VAR_CLIPPED = 0, 1, 2
 
@@ -132,6 +132,16 @@ def vector_kernel_desc(kind: int, l_df: float, l_cf: float = 1.0, ratio: float =
     k.l_df = float(l_df)
     k.l_cf = float(l_cf)
     k.ratio = float(ratio)
+    return k
+
+
+def vector_st_kernel_desc(kind: int, l_df: float, l_cf: float, ratio: float, var_t: float, l_t: float) -> KernelDesc:
+    """Spatio-temporal product Kt(var_t, l_t) × vector kernel on (T, Y, X) points."""
+    k = vector_kernel_desc(kind, l_df, l_cf, ratio)
+    k.family = FAMILY_VECTOR_ST
+    k.dim = 3
+    k.var[0] = float(var_t)
+    k.ls[0][0] = float(l_t)
     return k
 
 

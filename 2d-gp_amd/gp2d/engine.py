@@ -55,6 +55,10 @@ class KernelSpec:
         l_df, l_cf, ratio  (myKernel.py:13-22; GP_laser.py:16 `l_df, l_cf, rate`)
     family 'ard' (the sklearn model of krig.scikit_prior, krig.py:174-180):
         variances (1-2 terms), lengthscales (per term, 1-3 dims)
+    family 'vector_st' (SURVEY.md §8f item 2): the spatio-temporal product
+        Kt(var_t, l_t) × (the vector2d kernel of `kind`) on (T, Y, X) points — GPy
+        `Kt(...) * nonDivK(2, [1, 2], ℓ)` (scratch.py:506-508; Kt myKernel.py:337-363),
+        standing in for the reference's missing myKernel2 (krig.py:397-404)
     """
     family: str = "vector2d"
     kind: str = "df"
@@ -63,6 +67,8 @@ class KernelSpec:
     ratio: float = 1.0
     variances: tuple = ()
     lengthscales: tuple = ()
+    var_t: float = 1.0
+    l_t: float = 1.0
 
     _KINDS = {"scalar": N.KIND_SCALAR, "df": N.KIND_DIVFREE, "cf": N.KIND_CURLFREE, "mixed": N.KIND_MIXED,
               0: N.KIND_SCALAR, 1: N.KIND_DIVFREE, 2: N.KIND_CURLFREE, 3: N.KIND_MIXED}
@@ -72,15 +78,24 @@ class KernelSpec:
             return N.vector_kernel_desc(self._KINDS[self.kind], self.l_df, self.l_cf, self.ratio)
         if self.family == "ard":
             return N.ard_kernel_desc(self.variances, self.lengthscales)
+        if self.family == "vector_st":
+            return N.vector_st_kernel_desc(self._KINDS[self.kind], self.l_df, self.l_cf, self.ratio, self.var_t,
+                                           self.l_t)
         raise ValueError(f"unknown kernel family {self.family!r}")
 
     @property
+    def is_vector(self) -> bool:
+        return self.family in ("vector2d", "vector_st")
+
+    @property
     def block_dim(self) -> int:
-        return 2 if self.family == "vector2d" else 1
+        return 2 if self.is_vector else 1
 
     @property
     def input_dim(self) -> int:
-        return 2 if self.family == "vector2d" else len(self.lengthscales[0])
+        if self.family == "vector2d":
+            return 2
+        return 3 if self.family == "vector_st" else len(self.lengthscales[0])
 
     def kdiag(self) -> float:
         return float(N.lib().gp2d_kernel_diag(ctypes.byref(self.desc())))
@@ -159,8 +174,8 @@ def fit(kernel: KernelSpec, x, y, noise: float, jitter: float = 0.0, device=None
     """
     if variance not in VARIANCE_ENGINES:
         raise ValueError(f"variance must be one of {VARIANCE_ENGINES}")
-    if variance == "ozaki" and kernel.family != "vector2d":
-        raise ValueError("the ozaki variance engine supports the vector2d family only")
+    if variance == "ozaki" and not kernel.is_vector:
+        raise ValueError("the ozaki variance engine supports the vector families only")
     dev = _require_device(device)
     L = N.lib()
     d, bd = kernel.input_dim, kernel.block_dim
@@ -272,9 +287,12 @@ def predict(gp: GPFit, xg, var_mode: str = "latent", compute_var: bool = True, c
 # ------------------------------------------------------------------ hyperparameters
 def param_names(kernel: KernelSpec) -> tuple:
     """Gradient / parameter order of log_marginal_likelihood: vector2d (l_df, l_cf, ratio, noise);
-    ARD per term (variance, lengthscale_0..D−1), then noise (GPy param_array order, krig.py:459-466)."""
+    vector_st (l_df, l_cf, ratio, var_t, l_t, noise); ARD per term (variance, lengthscale_0..D−1),
+    then noise (GPy param_array order, krig.py:459-466)."""
     if kernel.family == "vector2d":
         return ("l_df", "l_cf", "ratio", "noise")
+    if kernel.family == "vector_st":
+        return ("l_df", "l_cf", "ratio", "var_t", "l_t", "noise")
     names = []
     for t, ls in enumerate(kernel.lengthscales):
         names += [f"variance_{t}"] + [f"lengthscale_{t}_{d}" for d in range(len(ls))]

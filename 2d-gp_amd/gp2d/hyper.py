@@ -36,9 +36,11 @@ _BAD = 1e25  # objective for a non-positive-definite K_y (rejected by the line s
 
 def free_names(kernel: E.KernelSpec, fix=()) -> tuple:
     """Names (engine.param_names order) of the parameters the optimiser moves."""
-    if kernel.family == "vector2d":
+    if kernel.is_vector:
         used = {"df": ("l_df",), "scalar": ("l_df",), "cf": ("l_cf",),
                 "mixed": ("l_df", "l_cf", "ratio")}[_kind_name(kernel.kind)]
+        if kernel.family == "vector_st":
+            used = used + ("var_t", "l_t")
         names = used + ("noise",)
     else:
         names = E.param_names(kernel)
@@ -53,6 +55,8 @@ def get_params(kernel: E.KernelSpec, noise: float) -> dict:
     names = E.param_names(kernel)
     if kernel.family == "vector2d":
         vals = (kernel.l_df, kernel.l_cf, kernel.ratio, noise)
+    elif kernel.family == "vector_st":
+        vals = (kernel.l_df, kernel.l_cf, kernel.ratio, kernel.var_t, kernel.l_t, noise)
     else:
         vals = []
         for v, ls in zip(kernel.variances, kernel.lengthscales):
@@ -65,6 +69,10 @@ def set_params(kernel: E.KernelSpec, params: dict):
     """(KernelSpec, noise) with `params` (a get_params-style dict) applied."""
     if kernel.family == "vector2d":
         k = dataclasses.replace(kernel, l_df=params["l_df"], l_cf=params["l_cf"], ratio=params["ratio"])
+        return k, params["noise"]
+    if kernel.family == "vector_st":
+        k = dataclasses.replace(kernel, l_df=params["l_df"], l_cf=params["l_cf"], ratio=params["ratio"],
+                                var_t=params["var_t"], l_t=params["l_t"])
         return k, params["noise"]
     var, ls = [], []
     for t, l in enumerate(kernel.lengthscales):

@@ -14,9 +14,11 @@ Differences forced by the environment (documented in DESIGN.md):
   * NetCDF output is SURVEY.md §8f item 3 (next): outputs are ``.npz``;
   * hyperparameter optimisation (GPy optimize / optimize_restarts) runs on the GPU
     (``gp2d.hyper``: HIP LML + exact gradient, scipy L-BFGS-B on the host);
-  * kernelType 2/3/4 use the 2-D spatial div-free / curl-free / mixed kernels on
-    the (Y, X) columns — the reference's spatio-temporal myKernel2 is missing from
-    the reference itself (krig.py:9).
+  * kernelType 2/3/4 use the spatio-temporal product Kt(var_t, l_t) × div-free /
+    curl-free / mixed kernel on (T, Y, X) (engine family 'vector_st', the form of
+    scratch.py:506-508) — the reference's myKernel2 (var, lt, ly, lx) is missing from
+    the reference itself (krig.py:9, SURVEY.md §0.2), so ly = lx = ℓ here;
+    hyper={'temporal': False} gives the purely spatial kernel on (Y, X).
 """
 from __future__ import annotations
 
@@ -167,6 +169,8 @@ class Krig:
             for v, ls in zip(s.variances, s.lengthscales):
                 hp += [v, *ls]
             return np.array(hp + [self.noise])
+        if s.family == "vector_st":
+            return np.array([s.l_df, s.l_cf, s.ratio, s.var_t, s.l_t, self.noise])
         return np.array([s.l_df, s.l_cf, s.ratio, self.noise])
 
     def save(self, path: str, with_factor: bool = False):
@@ -176,7 +180,8 @@ class Krig:
         s = self.spec
         d = dict(X=_to_numpy(self._X), y=_to_numpy(self._y), family=s.family, kind=str(s.kind), l_df=s.l_df,
                  l_cf=s.l_cf, ratio=s.ratio, variances=np.asarray(s.variances, dtype=np.float64),
-                 lengthscales=np.asarray(s.lengthscales, dtype=np.float64), noise=self.noise, jitter=self.jitter,
+                 lengthscales=np.asarray(s.lengthscales, dtype=np.float64), var_t=s.var_t, l_t=s.l_t,
+                 noise=self.noise, jitter=self.jitter,
                  var_mode=self.var_mode)
         if with_factor:
             d["W"] = _to_numpy(self.gp.W)
@@ -191,8 +196,9 @@ class Krig:
             spec = E.KernelSpec(family="ard", variances=tuple(z["variances"].tolist()),
                                 lengthscales=tuple(tuple(r) for r in z["lengthscales"].tolist()))
         else:
-            spec = E.KernelSpec(kind=str(z["kind"]), l_df=float(z["l_df"]), l_cf=float(z["l_cf"]),
-                                ratio=float(z["ratio"]))
+            st = dict(var_t=float(z["var_t"]), l_t=float(z["l_t"])) if "var_t" in z.files else {}
+            spec = E.KernelSpec(family=fam, kind=str(z["kind"]), l_df=float(z["l_df"]), l_cf=float(z["l_cf"]),
+                                ratio=float(z["ratio"]), **st)
         k = cls(spec, noise=float(z["noise"]), jitter=float(z["jitter"]), var_mode=str(z["var_mode"]),
                 device=device)
         if refit:
@@ -309,15 +315,16 @@ def kriging(st, et, lalim=(0, 0), lolim=(0, 0), sample_step=5, skip=5, nKernels=
     """krig.kriging (krig.py:259-418): build the GP model(s) for a drifter data window.
 
     kernelType 1: scalar ARD RBF on (T, Y, X), one model per component (v, u);
-    2 / 3 / 4: div-free / curl-free / mixed vector kernel on (Y, X) with obs = [v; u]
-    (krig.py:392-404).  nKernels > 1 sums nKernels identical ARD terms (krig.py:405-407;
+    2 / 3 / 4: Kt(var_t, l_t) × div-free / curl-free / mixed vector kernel on (T, Y, X) with
+    obs = [v; u] (krig.py:392-404; hyper 'temporal': False → spatial kernel on (Y, X)).  nKernels > 1 sums nKernels identical ARD terms (krig.py:405-407;
     ≤ 2 supported).  Hyperparameters come from `hyper` (no optimisation here).
     Writes output+'.npz' (the .mat of krig.py:417) and the model files; returns the models.
     """
     if tracks is None:
         raise ValueError("tracks= is required (the reference's Filtered_2016_2_7.pkl is not available)")
     t0 = time.time()
-    h = dict(l_df=5.0, l_cf=5.0, ratio=None, noise=0.0025, variance=1.0, lengthscale=(1.0, 1.0, 1.0))
+    h = dict(l_df=5.0, l_cf=5.0, ratio=None, noise=0.0025, variance=1.0, lengthscale=(1.0, 1.0, 1.0),
+             var_t=1.0, l_t=1.0, temporal=True)
     h.update(hyper or {})
     d = _prepare(tracks, st, et, lalim, lolim, sample_step, skip)
     X, Xt = d["X"], d["Xt"]
@@ -336,8 +343,14 @@ def kriging(st, et, lalim=(0, 0), lolim=(0, 0), sample_step=5, skip=5, nKernels=
         kind = {2: "df", 3: "cf", 4: "mixed"}[int(kernelType)]
         obs_all = np.concatenate([d["vo"], d["uo"]], 0)
         obst = np.concatenate([d["vt"], d["ut"]], 0)
-        k = Krig(kind, l_df=h["l_df"], l_cf=h["l_cf"], ratio=h["ratio"], noise=h["noise"], var_mode="gpy",
-                 device=device).fit(X[:, 1:3], obs_all[:, 0])
+        ratio = h["ratio"] if h["ratio"] is not None else {"df": 1.0, "cf": 0.0, "mixed": 0.5}[kind]
+        if h["temporal"]:
+            spec = E.KernelSpec(family="vector_st", kind=kind, l_df=h["l_df"], l_cf=h["l_cf"], ratio=ratio,
+                                var_t=h["var_t"], l_t=h["l_t"])
+            k = Krig(spec, noise=h["noise"], var_mode="gpy", device=device).fit(X, obs_all[:, 0])
+        else:
+            k = Krig(kind, l_df=h["l_df"], l_cf=h["l_cf"], ratio=ratio, noise=h["noise"], var_mode="gpy",
+                     device=device).fit(X[:, 1:3], obs_all[:, 0])
         tag = {2: "_divFree", 3: "_curlFree", 4: "_combined"}[int(kernelType)]
         k.save(output + tag + ".npz")
         models[tag] = k
@@ -368,6 +381,11 @@ def runRestarts(fname, nres=10, nKernels=2, device=None, seed=0):
     return res
 
 
+def _vec_cols(model, X):
+    """(T, Y, X) rows for the spatio-temporal kernel, (Y, X) for the spatial one."""
+    return X if model.spec.input_dim == 3 else X[:, 1:3]
+
+
 def predict(filename, tlim=(0, 0), ylim=(0, 0), xlim=(0, 0), dt=0.5, dx=0.5, xL=40, yL=40, Simul=0,
             device=None):
     """krig.predict (krig.py:471-574): grid posterior per time slice for the u and v
@@ -395,7 +413,7 @@ def predict(filename, tlim=(0, 0), ylim=(0, 0), xlim=(0, 0), dt=0.5, dx=0.5, xL=
             v2, vv2 = mv.predict(Xp2)
             u2, uv2 = mu_.predict(Xp2)
         else:
-            f2, fv2 = mvec.predict(Xp2[:, 1:3])
+            f2, fv2 = mvec.predict(_vec_cols(mvec, Xp2))
             v2, u2 = f2[:inc], f2[inc:]
             vv2, uv2 = fv2[:inc], fv2[inc:]
         V.append(v2)
@@ -432,7 +450,7 @@ def predictTest(filename, device=None):
             u2, uv2 = mu_.predict(Xt2)
         else:
             m = Xt2.shape[0]
-            f2, fv2 = mvec.predict(Xt2[:, 1:3])
+            f2, fv2 = mvec.predict(_vec_cols(mvec, Xt2))
             v2, u2, vv2, uv2 = f2[:m], f2[m:], fv2[:m], fv2[m:]
         V.append(v2)
         U.append(u2)

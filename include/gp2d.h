@@ -16,7 +16,7 @@
  *
  * Layouts:
  *   points          (N, dim) row-major; dim = 2 for the vector kernels (x1, x2),
- *                   dim = 1..3 for the scalar ARD family (T, Y, X order);
+ *                   3 for VECTOR_ST (t, x1, x2), 1..3 for the scalar ARD family (T, Y, X order);
  *   vector kernels  component-major 2Np × 2Np: [[K_uu, K_uv], [K_vu, K_vv]]
  *                   (GP_scripts.py:89-95), Np = gp2d_padded_points(N);
  *   observations    y = [u_1..u_N, 0.., v_1..v_N, 0..] (2Np; GP_laser.py:98-99);
@@ -39,6 +39,9 @@ extern "C" {
 /* kernel families */
 #define GP2D_FAMILY_VECTOR2D 0   /* 2×2 matrix-valued SE kernels on (x1, x2)          */
 #define GP2D_FAMILY_ARD_RBF  1   /* scalar Σ var·exp(−½Σ_d (Δ_d/ls_d)²) (krig.py:174-180) */
+#define GP2D_FAMILY_VECTOR_ST 2  /* spatio-temporal product Kt(t) × vector2d(y, x) on (T, Y, X) points:
+                                    var[0]·exp(−Δt²/(2·ls[0][0]²)) times the 2×2 block of `kind`
+                                    (scratch.py:506-508 kt * nonDivK; myKernel.py:337-360 Kt)    */
 
 /* vector2d kinds — the reference's divFree flag (GP_scripts.py:57-69) */
 #define GP2D_KIND_SCALAR   0     /* divFree=0: scalar SE broadcast into the 2×2 block  */
@@ -59,8 +62,8 @@ typedef struct gp2d_kernel {
     double  ratio;       /* weight of the div-free part (myKernel `ratio`, GP_laser `rate`) */
     int32_t dim;         /* ARD: input dimension, 1..3                                 */
     int32_t nterms;      /* ARD: number of RBF terms, 1..2                             */
-    double  var[2];      /* ARD: term variances                                        */
-    double  ls[2][3];    /* ARD: term length scales per dimension                      */
+    double  var[2];      /* ARD: term variances; VECTOR_ST: var[0] = temporal variance */
+    double  ls[2][3];    /* ARD: term length scales per dimension; VECTOR_ST: ls[0][0] = ℓ_t */
 } gp2d_kernel_t;
 
 /* ---- sizes ------------------------------------------------------------------- */
@@ -151,7 +154,7 @@ int    gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int nmod, 
  *   nobs = observed entries (bd·N).
  * gp2d_lml_grad: grad_dev (device, gp2d_lml_grad_count(k) doubles) = ½ tr((ααᵀ − K_y⁻¹) ∂K_y/∂θ)
  *   in natural units, θ = vector2d: (l_df, l_cf, ratio, noise) — entries a kind does not
- *   use are 0, KIND_SCALAR's σ is l_df; ARD, per term t: (var[t], ls[t][0..D)), then noise —
+ *   use are 0, KIND_SCALAR's σ is l_df; VECTOR_ST: (l_df, l_cf, ratio, var_t, l_t, noise); ARD, per term t: (var[t], ls[t][0..D)), then noise —
  *   GPy's param_array order (krig.py:459-466).
  *   K_y⁻¹ = WᵀW is formed in the workspace (gp2d_lml_grad_workspace(n) bytes, ≈ 2n² doubles).
  *   The reference's myKernel.update_gradients_full (myKernel.py:59-105) is not the

@@ -215,6 +215,73 @@ def ard_fit_predict(X, y, Xg, variances, lengthscales, noise, jitter=1e-10):
 
 
 # --------------------------------------------------------------------------------------
+# Spatio-temporal product kernel
+# --------------------------------------------------------------------------------------
+def vector_st_kernel(xa, xb, kind=KIND_DIVFREE, l_df=1.0, l_cf=1.0, ratio=1.0, var_t=1.0, l_t=1.0):
+    """Kt(var_t, l_t) × vector kernel on (T, Y, X) rows: GPy's product `kt * nonDivK(2, [1, 2], ℓ)`
+    (scratch.py:506-508) with Kt.K = the GPy RBF on t broadcast into all four blocks
+    (myKernel.py:347-355); the product is elementwise (GPy Prod).  Components follow the
+    spatial coordinate order (Y, X), i.e. obs = [v; u] (krig.py:390)."""
+    xa = np.asarray(xa, dtype=np.float64).reshape(-1, 3)
+    xb = np.asarray(xb, dtype=np.float64).reshape(-1, 3)
+    C = var_t * np.exp(-0.5 * np.square(xa[:, 0][:, None] - xb[:, 0][None, :]) / l_t ** 2)
+    K = vector_kernel(xa[:, 1:], xb[:, 1:], kind=kind, l_df=l_df, l_cf=l_cf, ratio=ratio)
+    return K * np.block([[C, C], [C, C]])
+
+
+def st_fit_predict(x, y, xg, kind="df", l_df=5.0, l_cf=5.0, ratio=1.0, var_t=1.0, l_t=1.0, noise=0.0025,
+                   var_mode="latent"):
+    """Posterior mean / variance of the spatio-temporal GP (Cholesky; GP_laser.py:113-131 recipe)."""
+    import scipy.linalg as sla
+    kw = dict(kind=kind_code(kind), l_df=l_df, l_cf=l_cf, ratio=ratio, var_t=var_t, l_t=l_t)
+    K = vector_st_kernel(x, x, **kw)
+    K[np.diag_indices_from(K)] += noise
+    L = np.linalg.cholesky(K)
+    alpha = sla.cho_solve((L, True), np.asarray(y, dtype=np.float64).reshape(-1))
+    xg = np.asarray(xg, dtype=np.float64).reshape(-1, 3)
+    M = xg.shape[0]
+    Ks = vector_st_kernel(xg, x, **kw)
+    f = Ks @ alpha
+    V = sla.solve_triangular(L, Ks.T, lower=True)
+    kss = var_t * kernel_diag(kind_code(kind), l_df=l_df, l_cf=l_cf, ratio=ratio)
+    v = kss - np.einsum("ij,ij->j", V, V)
+    if var_mode in ("gpy", "sklearn"):
+        v = v + noise
+    if var_mode == "sklearn":
+        v = np.where(v < 0, 0.0, v)
+    return f, v
+
+
+def vector_st_lml(x, y, kind="df", l_df=5.0, l_cf=5.0, ratio=1.0, var_t=1.0, l_t=1.0, noise=0.0025,
+                  eval_gradient=False, rel_step=1e-4):
+    """LML of the spatio-temporal GP; gradient (l_df, l_cf, ratio, var_t, l_t, noise) as in
+    vector_lml (4-point stencil on the kernel matrix, ∂/∂noise = I)."""
+    kw = dict(kind=kind, l_df=l_df, l_cf=l_cf, ratio=ratio, var_t=var_t, l_t=l_t)
+    K = vector_st_kernel(x, x, **kw)
+    K[np.diag_indices_from(K)] += noise
+    val, L, alpha = lml_from_K(K, y)
+    if not eval_gradient:
+        return val
+    code = kind_code(kind)
+    uses = {KIND_SCALAR: ("l_df",), KIND_DIVFREE: ("l_df",), KIND_CURLFREE: ("l_cf",),
+            KIND_MIXED: ("l_df", "l_cf", "ratio")}[code] + ("var_t", "l_t")
+    names = ("l_df", "l_cf", "ratio", "var_t", "l_t")
+    g = np.zeros(6)
+    for i, name in enumerate(names):
+        if name not in uses:
+            continue
+        h = rel_step * (abs(kw[name]) if name != "ratio" else 1.0)
+        Ks = []
+        for t in (-2, -1, 1, 2):
+            k2 = dict(kw)
+            k2[name] = kw[name] + t * h
+            Ks.append(vector_st_kernel(x, x, **k2))
+        g[i] = _trace_grad(L, alpha, (Ks[0] - 8 * Ks[1] + 8 * Ks[2] - Ks[3]) / (12 * h))
+    g[5] = _trace_grad(L, alpha, np.eye(K.shape[0]))
+    return val, g
+
+
+# --------------------------------------------------------------------------------------
 # Log marginal likelihood and its gradient (SURVEY.md §8f item 1)
 # --------------------------------------------------------------------------------------
 def lml_from_K(K, y):

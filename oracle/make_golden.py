@@ -319,6 +319,45 @@ def gen_lml(gs, out):
     np.savez_compressed(os.path.join(out, "lml_sklearn_ard_N128.npz"), **e)
 
 
+def gen_st(gs, out):
+    """Spatio-temporal product kernel: Kt(var_t, l_t) × vector kernel on
+    (T, Y, X), the GPy product of scratch.py:506-508.  The spatial factor is the reference's own
+    myKernel (GP_scripts.py:6-42) on (Y, X); the temporal factor is the GPy RBF of Kt.K
+    (myKernel.py:347-355) = var·exp(−Δt²/2ℓ²), evaluated by scikit-learn's RBF (GPy is absent).
+    N=150 tracks over 6 days, 2 time slices × 10×10 grid; posterior by the GP_laser.py:113-131
+    recipe (np.linalg.inv)."""
+    from sklearn.gaussian_process import kernels
+    rng = np.random.default_rng(31)
+    N = 150
+    t = rng.uniform(0, 6, N)
+    yy = rng.uniform(0, 45, N)
+    xx = rng.uniform(0, 60, N)
+    v = np.cos(xx / 9) + 0.1 * t + rng.normal(0, 0.05, N)
+    u = np.sin(yy / 7) - 0.05 * t + rng.normal(0, 0.05, N)
+    obs = np.concatenate([v, u])        # components follow (Y, X): [v; u] (krig.py:390)
+    gy, gx = np.meshgrid(np.linspace(0, 45, 10), np.linspace(0, 60, 10), indexing="ij")
+    G = np.concatenate([np.stack([np.full(100, tt), gy.reshape(-1), gx.reshape(-1)], 1) for tt in (2.0, 4.5)])
+    d = dict(t=t, y=yy, x=xx, obs=obs, G=G)
+    for name, (ldf, lcf, rate, var_t, l_t, noise) in (("df", (5.0, 5.0, 1.0, 5.0, 1.0, 0.0025)),
+                                                     ("mixed", (6.0, 4.0, 0.4, 2.0, 1.5, 0.01))):
+        def K_st(A, B):
+            C = var_t * kernels.RBF(length_scale=l_t)(A[:, :1], B[:, :1])
+            S = gs["myKernel"](A[:, 1:], B[:, 1:], ldf, lcf, rate)
+            return S * np.block([[C, C], [C, C]])
+        X = np.stack([t, yy, xx], 1)
+        K = K_st(X, X) + np.identity(2 * N) * noise
+        Ki = np.linalg.inv(K)
+        Ks = K_st(G, X)
+        f = gs["getMean"](Ks, Ki, obs[:, None])
+        kss = np.diag(K_st(G, G))
+        var = kss - np.einsum("ij,ij->i", Ks, Ks @ Ki)
+        d[f"{name}_params"] = np.array([ldf, lcf, rate, var_t, l_t, noise])
+        d[f"{name}_K_rows"] = K[[0, 1, N, 2 * N - 1]]
+        d[f"{name}_mean"] = np.asarray(f).reshape(-1)
+        d[f"{name}_var"] = var
+    np.savez_compressed(os.path.join(out, "st_product_N150.npz"), **d)
+
+
 def gen_indices(out):
     """Split index arrays, verbatim reference expression (GP_laser.py:81-83, krig.py:335-337)."""
     sizes = list(range(30, 40)) + list(range(128, 140)) + [257, 1000, 1031, 3000, 12288]
@@ -362,7 +401,7 @@ def main():
     jobs = dict(small=lambda: gen_small(gs, a.out), laser=lambda: gen_laser(gs, a.out),
                 mykernel=lambda: gen_mykernel(gs, a.out), sklearn=lambda: gen_sklearn(a.out),
                 indices=lambda: gen_indices(a.out), grids=lambda: gen_grids(a.out),
-                lml=lambda: gen_lml(gs, a.out))
+                lml=lambda: gen_lml(gs, a.out), st=lambda: gen_st(gs, a.out))
     for name, fn in jobs.items():
         if a.only and name not in a.only.split(","):
             continue

@@ -96,20 +96,32 @@ def test_var_modes_and_save_load(tmp_path):
 
 
 def test_kriging_predict_pipeline(tmp_path):
-    """kriging → predict → predictTest on synthetic drifters (kernelType 2 and 1)."""
+    """kriging → predict → predictTest on synthetic drifters: kernelType 2 (the spatio-temporal
+    product Kt × div-free on (T, Y, X), and the spatial kernel with hyper temporal=False) and 1."""
     tr = krig.Tracks.synthetic(n_time=24, n_drifters=40)
     out = str(tmp_path / "model")
-    models = krig.kriging(0, 24, sample_step=-2, skip=2, nKernels=1, output=out, kernelType=2, tracks=tr)
+    models = krig.kriging(0, 24, sample_step=-2, skip=2, nKernels=1, output=out, kernelType=2, tracks=tr,
+                          hyper=dict(var_t=1.5, l_t=4.0))
     k = models["_divFree"]
+    assert k.spec.family == "vector_st" and k.spec.input_dim == 3
     f = np.load(out + ".npz")
     assert f["Xo"].shape[1] == 3 and f["obs"].shape[0] == 2 * f["Xo"].shape[0]
     Xp, V, U, VV, UV = krig.predict(out, tlim=[0, 2], ylim=[-5, 40], xlim=[-5, 50], dt=1.0, dx=2.0)
     assert V.shape == U.shape == VV.shape == UV.shape and V.shape[0] == 2
-    # same posterior as the oracle with obs=[v; u] on the (Y, X) columns
+    # same posterior as the oracle with obs=[v; u] on (T, Y, X), first time slice
+    pts = Xp[:V.shape[1] * V.shape[2], :]
+    mo, vo = O.st_fit_predict(f["Xo"], f["obs"][:, 0], pts, kind="df", l_df=5.0, var_t=1.5, l_t=4.0,
+                              noise=0.0025, var_mode="gpy")
+    M = pts.shape[0]
+    assert rel(V[0].reshape(-1), mo[:M]) < 1e-10 and rel(U[0].reshape(-1), mo[M:]) < 1e-10
+    assert rel(VV[0].reshape(-1), vo[:M]) < 1e-10
+    # purely spatial variant on the (Y, X) columns
+    krig.kriging(0, 24, sample_step=-2, skip=2, nKernels=1, output=out + "_xy", kernelType=2, tracks=tr,
+                 hyper=dict(temporal=False))
+    Xp, V, U, VV, UV = krig.predict(out + "_xy", tlim=[0, 2], ylim=[-5, 40], xlim=[-5, 50], dt=1.0, dx=2.0)
     pts = Xp[:V.shape[1] * V.shape[2], 1:3]
     mo, vo = O.fit_predict(f["Xo"][:, 1:3], f["obs"][:, 0], pts, kind="df", l_df=5.0, noise=0.0025,
                            var_mode="gpy")
-    M = pts.shape[0]
     assert rel(V[0].reshape(-1), mo[:M]) < 1e-10 and rel(U[0].reshape(-1), mo[M:]) < 1e-10
     assert rel(VV[0].reshape(-1), vo[:M]) < 1e-10
     V2, U2, VV2, UV2 = krig.predictTest(out)

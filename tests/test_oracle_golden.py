@@ -181,3 +181,20 @@ def test_reference_gradient_quirk():
     assert abs(r_ratio - g[2]) < 1e-6 * abs(g[2])
     assert abs(r_df - g[0]) > 1e-2 * abs(g[0])
     assert abs(r_cf - g[1]) > 1e-2 * abs(g[1])
+
+
+# ------------------------------------------------------ spatio-temporal product (§8f.2)
+@pytest.mark.parametrize("name,kind", [("df", "df"), ("mixed", "mixed")])
+def test_st_product_golden(golden, name, kind):
+    """Oracle Kt × vector kernel and its posterior vs the fixture built from the reference's
+    myKernel (GP_scripts.py:6-42) times the GPy-RBF temporal factor (myKernel.py:347-355)."""
+    g = golden("st_product_N150.npz")
+    X = np.stack([g["t"], g["y"], g["x"]], 1)
+    ldf, lcf, rate, var_t, l_t, noise = g[f"{name}_params"]
+    kw = dict(kind=kind, l_df=ldf, l_cf=lcf, ratio=rate, var_t=var_t, l_t=l_t)
+    K = O.vector_st_kernel(X, X, **kw) + noise * np.eye(2 * X.shape[0])
+    N = X.shape[0]
+    assert rel_err(K[[0, 1, N, 2 * N - 1]], g[f"{name}_K_rows"]) < 1e-13
+    mean, var = O.st_fit_predict(X, g["obs"], g["G"], noise=noise, **kw)
+    assert rel_err(mean, g[f"{name}_mean"]) < 1e-10
+    assert rel_err(var, g[f"{name}_var"]) < 1e-10
