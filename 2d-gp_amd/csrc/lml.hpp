@@ -21,7 +21,7 @@
 // The reference's own gradient (myKernel.update_gradients_full, myKernel.py:59-105)
 // is not a derivative of its kernel (the (2ℓ²−Cℓ²)/ℓ⁵ term has the wrong sign and
 // dA/dℓ lacks the 1/ℓ² factor; SURVEY.md §0.2 lists the gradient paths as broken).
-// This file implements the exact derivative; DESIGN.md §3.5 documents the quirk.
+// This file implements the exact derivative; DESIGN.md §3.2 documents the quirk.
 #pragma once
 #include "common.hpp"
 #include "assemble.hpp"

@@ -14,7 +14,7 @@ GPy itself is not a dependency: the classes expose the same methods and
 parameters without the paramz machinery.  Parameters are floats carrying a
 ``.gradient`` attribute, which ``update_gradients_full`` fills with the EXACT
 derivative contraction (HIP kernel gp2d_kernel_grad) — the reference's own
-formula is not a derivative of its kernel (SURVEY.md §0.2, DESIGN.md §3.5).
+formula is not a derivative of its kernel (SURVEY.md §0.2, DESIGN.md §3.2).
 ``gradients_X`` raises, as the reference's does (NameError, myKernel.py:123).
 Outputs are numpy arrays, as in the reference; ``*_device`` variants return the
 torch tensor resident in HBM.

@@ -158,7 +158,7 @@ int    gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int nmod, 
  *   GPy's param_array order (krig.py:459-466).
  *   K_y⁻¹ = WᵀW is formed in the workspace (gp2d_lml_grad_workspace(n) bytes, ≈ 2n² doubles).
  *   The reference's myKernel.update_gradients_full (myKernel.py:59-105) is not the
- *   derivative of its kernel; this is the exact one (DESIGN.md §3.5).                  */
+ *   derivative of its kernel; this is the exact one (DESIGN.md §3.2).                  */
 int    gp2d_lml(const double* W, int64_t n, int64_t ldw, const double* alpha, const double* y,
                 int64_t nobs, double* lml_dev, void* stream);
 int    gp2d_lml_grad_count(const gp2d_kernel_t* k);
