@@ -11,7 +11,9 @@ Differences forced by the environment (documented in DESIGN.md):
     are ``.npz`` (inputs + hyperparameters, optionally the factor);
   * pyproj / NAD83 is absent: ``project`` is a signed local equirectangular
     projection in km about (lat0, lon0);
-  * NetCDF output is SURVEY.md §8f item 3 (next): outputs are ``.npz``;
+  * NetCDF: krig.predict writes filename+'.nc' (CDF-2, printNCFiles layout) through
+    ``gp2d.ncio`` (netCDF4 is absent; a self-contained classic-format writer), plus the
+    ``.npz`` of the same arrays;
   * hyperparameter optimisation (GPy optimize / optimize_restarts) runs on the GPU
     (``gp2d.hyper``: HIP LML + exact gradient, scipy L-BFGS-B on the host);
   * kernelType 2/3/4 use the spatio-temporal product Kt(var_t, l_t) × div-free /
@@ -32,6 +34,7 @@ import torch
 from . import data as D
 from . import engine as E
 from . import hyper as H
+from . import ncio as NC
 
 lat0 = 28.8
 lon0 = -88.6
@@ -389,7 +392,7 @@ def _vec_cols(model, X):
 def predict(filename, tlim=(0, 0), ylim=(0, 0), xlim=(0, 0), dt=0.5, dx=0.5, xL=40, yL=40, Simul=0,
             device=None):
     """krig.predict (krig.py:471-574): grid posterior per time slice for the u and v
-    models saved by kriging(); writes filename+'_pred.npz' and returns
+    models saved by kriging(); writes filename+'.nc' (krig.py:559-570) and filename+'_pred.npz', returns
     (Xp, V, U, VVar, UVar) reshaped [tp, yp, xp]."""
     t0 = time.time()
     f = np.load(filename + ".npz", allow_pickle=False)
@@ -423,6 +426,10 @@ def predict(filename, tlim=(0, 0), ylim=(0, 0), xlim=(0, 0), dt=0.5, dx=0.5, xL=
     shp = [tp.size, yp.size, xp.size]
     V, U, VV, UV = (np.reshape(np.concatenate(a, 0), shp) for a in (V, U, VV, UV))
     np.savez(filename + "_pred.npz", time=tp, y=yp, x=xp, v=V, u=U, vvar=VV, uvar=UV)
+    # NetCDF-3 product, krig.py:559-570 (createNC + writeNC of v, u, vvar, uvar, hyperparams)
+    hyp_v = (mv if kt == 1 else mvec).param_array
+    hyp_u = (mu_ if kt == 1 else mvec).param_array
+    NC.write_prediction(filename + ".nc", tp, yp, xp, V, U, VV, UV, hyp_v, hyp_u)
     print("End of script, time : " + str(time.time() - t0))
     return Xp, V, U, VV, UV
 
@@ -465,19 +472,34 @@ def scikit_prior(filename0, varname="v", dt=0, tlim=6, radar="", xlim=(0, 0), yl
                  HP=None, device=None):
     """krig.scikit_prior (krig.py:88-207): fixed-hyperparameter scalar GP
     HP0·RBF([lt,ly,lx]) (+ HP4·RBF) + White(noise) on the windowed observations,
-    predicted on the getGrid window at time dt.  Model inputs come from
+    predicted at time dt on the getGrid window (xlim/ylim given) or on the grid of a
+    pre-existing filename0+'.nc' (krig.py:123-141).  Model inputs come from
     filename0+'.npz' (written by kriging); HP = [var1, lt, ly, lx, (var2, lt, ly, lx,) noise]
     (the GPy param_array the reference loads at krig.py:159-161).
-    Returns (U, Ustd²) reshaped [1, yg, xg] and writes the .npz output."""
+    Writes <filename>_<t>h_scikit_<ind>.nc (createNC if absent, then varname, varname+'var',
+    hyperparam_<varname>, krig.py:197-206) and returns (U, Ustd²) reshaped [1, yg, xg]."""
     if radar:
-        raise NotImplementedError("radar grids need NetCDF input (SURVEY.md §8f item 3)")
+        raise NotImplementedError("radar grids need the radar NetCDF files and the NAD83 projection "
+                                  "(pyproj), neither of which exists here")
     fm = np.load(filename0 + ".npz", allow_pickle=False)
     if HP is None:
         raise ValueError("HP (hyperparameters) is required: the reference reads them from a GPy pickle")
     HP = np.asarray(HP, dtype=np.float64)
-    if not ((xlim[1] > xlim[0]) and (ylim[1] > ylim[0])):
-        raise ValueError("scikit_prior needs an explicit xlim/ylim window (pre-existing NetCDF grids are next)")
-    X, tcenter, yg, xg = getGrid([dt, dt + 1], ylim, xlim, 1, dx)   # krig.py:121
+    if (xlim[1] > xlim[0]) and (ylim[1] > ylim[0]):
+        X, tcenter, yg, xg = getGrid([dt, dt + 1], ylim, xlim, 1, dx)   # krig.py:121
+        filename = filename0 + "_cyc"
+    else:                                                             # krig.py:123-141
+        g = NC.readNC(filename0 + ".nc")
+        xg, yg, tg = (np.asarray(g[k], dtype=np.float64) for k in ("x", "y", "time"))
+        it = int(dt)
+        tcenter = np.array([tg[it]])
+        Yg, Tg, Xg = np.meshgrid(yg, tg, xg)
+        X = np.concatenate([Tg.reshape(-1, 1), Yg.reshape(-1, 1), Xg.reshape(-1, 1)], 1)
+        filename = filename0
+        inc = yg.size * xg.size
+        X = X[inc * it:inc * it + inc, :]
+    filename = filename + "_" + str(np.round(tcenter[0], decimals=2)) + "h_scikit_"
+    outFile = filename + str(ind) + ".nc"
     to, tt = fm["Xo"][:, 0], fm["Xt"][:, 0]
     xo, xt = fm["Xo"][:, 2], fm["Xt"][:, 2]
     ito = np.where((to >= tcenter - tlim) & (to <= tcenter + tlim) & (xo >= xlim[0] - xrange) & (xo <= xlim[1] + xrange))
@@ -501,8 +523,12 @@ def scikit_prior(filename0, varname="v", dt=0, tlim=6, radar="", xlim=(0, 0), yl
     Um, Uvar = k.predict(X)
     U = np.reshape(Um, [tcenter.size, yg.size, xg.size])
     Ustd2 = np.reshape(Uvar, [tcenter.size, yg.size, xg.size])
-    out = filename0 + "_cyc_" + str(np.round(tcenter[0], decimals=2)) + "h_scikit_" + str(ind) + ".npz"
-    np.savez(out, time=tcenter, y=yg, x=xg, **{varname: U, varname + "var": Ustd2, "hyperparam_" + varname: HP})
+    if not os.path.isfile(outFile):
+        NC.createNC(outFile, tcenter, yg, xg, HP)
+    with NC.openNC(outFile, "a") as fi:
+        NC.writeNC(fi, varname, U)
+        NC.writeNC(fi, varname + "var", Ustd2)
+        NC.writeNC(fi, "hyperparam_" + varname, HP)
     return U, Ustd2
 
 

@@ -8,6 +8,7 @@ if not torch.cuda.is_available():  # pragma: no cover
     pytest.skip("no HIP device", allow_module_level=True)
 
 import krig  # noqa: E402
+from gp2d import ncio  # noqa: E402
 from gp2d import engine as E  # noqa: E402
 from gp2d import kern  # noqa: E402
 from oracle import gp2d_oracle as O  # noqa: E402
@@ -115,6 +116,13 @@ def test_kriging_predict_pipeline(tmp_path):
     M = pts.shape[0]
     assert rel(V[0].reshape(-1), mo[:M]) < 1e-10 and rel(U[0].reshape(-1), mo[M:]) < 1e-10
     assert rel(VV[0].reshape(-1), vo[:M]) < 1e-10
+    # the NetCDF-3 product of krig.py:559-570 (read back through scipy's independent reader)
+    from scipy.io import netcdf_file
+    with netcdf_file(out + ".nc", "r", mmap=False) as nc:
+        assert nc.dimensions["time"] is None and nc.variables["v"].shape == V.shape
+        assert np.array_equal(nc.variables["v"][:], V.astype(np.float32))
+        assert np.array_equal(nc.variables["uvar"][:], UV.astype(np.float32))
+        assert np.array_equal(nc.variables["hyperparam_v"][:], k.param_array.astype(np.float32))
     # purely spatial variant on the (Y, X) columns
     krig.kriging(0, 24, sample_step=-2, skip=2, nKernels=1, output=out + "_xy", kernelType=2, tracks=tr,
                  hyper=dict(temporal=False))
@@ -131,3 +139,22 @@ def test_kriging_predict_pipeline(tmp_path):
     assert set(models) == {"u", "v"}
     Xp, V, U, VV, UV = krig.predict(out + "_rbf", tlim=[0, 2], ylim=[-5, 40], xlim=[-5, 50], dt=1.0, dx=3.0)
     assert np.all(np.isfinite(V)) and np.all(VV > 0)
+    # scikit_prior on the pre-existing grid of out_rbf.nc (krig.py:123-141), NetCDF output
+    HP = np.array([0.1, 5.0, 8.0, 8.0, 0.001])
+    U0, S0 = krig.scikit_prior(out + "_rbf", varname="v", dt=1, HP=HP, xrange=1000.0)
+    g = ncio.readNC(out + "_rbf.nc")
+    yg, tg, xg = (np.asarray(g[c], dtype=np.float64) for c in ("y", "time", "x"))
+    Yg, Tg, Xg = np.meshgrid(yg, tg, xg)
+    inc = yg.size * xg.size
+    Xq = np.stack([Tg.reshape(-1), Yg.reshape(-1), Xg.reshape(-1)], 1)[inc:2 * inc]
+    fm = np.load(out + "_rbf.npz")
+    tc = tg[1]
+    sel = lambda T: np.where((T[:, 0] >= tc - 6) & (T[:, 0] <= tc + 6))[0]   # tlim = 6, all x
+    XT = np.concatenate([fm["Xo"][sel(fm["Xo"])], fm["Xt"][sel(fm["Xt"])]])
+    u = np.concatenate([fm["obs"][sel(fm["Xo"]), 0], fm["test_points"][sel(fm["Xt"]), 0]])
+    mo, so = O.ard_fit_predict(XT, u, Xq, [0.1], [(5.0, 8.0, 8.0)], 0.001, jitter=1e-10)
+    assert rel(U0.reshape(-1), mo) < 1e-10 and rel(S0.reshape(-1), so ** 2) < 1e-10
+    outf = out + "_rbf_" + str(np.round(tc, decimals=2)) + "h_scikit_0.nc"
+    d = ncio.readNC(outf)
+    assert np.array_equal(d["v"], U0.astype(np.float32)) and np.array_equal(d["vvar"], S0.astype(np.float32))
+    assert np.array_equal(d["hyperparam_v"], HP.astype(np.float32))
