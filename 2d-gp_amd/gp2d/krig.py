@@ -45,13 +45,23 @@ KERNEL_NAMES = {"df": "df", "divfree": "df", "div-free": "df", 1: "df",
                 "scalar": "scalar", "isotropic": "scalar", 0: "scalar"}
 
 
-def project(lon, lat, lon_0: float = lon0, lat_0: float = lat0):
-    """Signed local equirectangular projection to km (stands in for the NAD83
-    projection of krig.py:19-20,291-298, which needs pyproj)."""
-    R = 6371.0
-    x = R * np.cos(np.deg2rad(lat_0)) * np.deg2rad(np.asarray(lon, dtype=np.float64) - lon_0)
-    y = R * np.deg2rad(np.asarray(lat, dtype=np.float64) - lat_0)
+def nad83(lon, lat):
+    """Stand-in for the reference's NAD83 / EPSG:3452 projection (krig.py:19; pyproj is absent):
+    a signed equirectangular projection in metres, scaled at lat0."""
+    R = 6371000.0
+    x = R * np.cos(np.deg2rad(lat0)) * np.deg2rad(np.asarray(lon, dtype=np.float64))
+    y = R * np.deg2rad(np.asarray(lat, dtype=np.float64))
     return x, y
+
+
+x_ori, y_ori = nad83(lon0, lat0)   # krig.py:20
+
+
+def project(lon, lat):
+    """Track coordinates to km about (lat0, lon0), with the reference's arithmetic
+    (krig.py:291-298): (NAD83(lon, lat) − origin) / 1000."""
+    x, y = nad83(lon, lat)
+    return (x - x_ori) / 1000.0, (y - y_ori) / 1000.0
 
 
 def _to_numpy(t):
@@ -265,32 +275,43 @@ class Tracks:
         return cls(np.arange(n_time) * dt_h * 3600.0, lat, lon, U, V)
 
 
-def getData(st, et, tracks: Tracks):
+def getData(st, et, tracks: Tracks, drop_drifters=()):
     """krig.getData (krig.py:42-77) on a track container: time in hours from the first
-    sample, columns ordered by decreasing number of valid points."""
+    sample, columns ordered by decreasing number of valid points.  drop_drifters are set to
+    NaN first — the reference hard-codes drifter 238 of Filtered_2016_2_7.pkl (krig.py:46-52);
+    pass (238,) for that file.  The caller's container is not modified."""
+    lat, lon, u, v = (np.array(a, dtype=np.float64) for a in (tracks.lat, tracks.lon, tracks.u, tracks.v))
+    for c in drop_drifters:
+        lat[:, c] = np.nan
+        lon[:, c] = np.nan
+        u[:, c] = np.nan
+        v[:, c] = np.nan
     time_h = (tracks.time[st:et] - tracks.time[0]) / 3600.0
-    latt = tracks.lat[st:et, :]
-    lont = tracks.lon[st:et, :]
-    uob = tracks.u[st:et, :]
-    vob = tracks.v[st:et, :]
+    latt = lat[st:et, :]
+    lont = lon[st:et, :]
+    uob = u[st:et, :]
+    vob = v[st:et, :]
     valid = np.array([np.size(np.where((~np.isnan(lont[:, i])) & (~np.isnan(latt[:, i])))[0])
                       for i in range(latt.shape[1])])
     order = np.squeeze(valid.argsort(axis=0))[::-1]
     return time_h, latt[:, order], lont[:, order], vob[:, order], uob[:, order], valid[order]
 
 
-def _prepare(tracks, st, et, lalim, lolim, sample_step, skip):
+def _prepare(tracks, st, et, lalim, lolim, sample_step, skip, drop_drifters=()):
     """Data selection of krig.kriging (krig.py:274-381): bounds, projection, split,
-    NaN filter, T,Y,X stacking.  Returns dict of observation / test arrays."""
-    time_h, latt, lont, vob, uob, _ = getData(st, et, tracks)
+    NaN filter, T,Y,X stacking.  Returns dict of observation / test arrays.
+    Bit-exact with the reference's code on the same tracks (tests/golden/prep_tracks.npz)."""
+    time_h, latt, lont, vob, uob, _ = getData(st, et, tracks, drop_drifters)
     if lolim[1] > lolim[0]:
         latt, lont, vob, uob = boundData(lont, lolim, latt, lont, vob, uob)
     if lalim[1] > lalim[0]:
         latt, lont, vob, uob = boundData(latt, lalim, latt, lont, vob, uob)
-    xob, yob = project(lont, latt)
+    xob, yob = nad83(lont, latt)
     tob = np.repeat(time_h[:, None], latt.shape[1], axis=1)
     yob[np.where(np.isnan(lont))] = np.nan
     xob[np.where(np.isnan(lont))] = np.nan
+    xob = (xob - x_ori) / 1000.0
+    yob = (yob - y_ori) / 1000.0
     if (sample_step < 0) or (skip > 1):
         samples, testt, testd = D.drifter_split(tob.shape[0], tob.shape[1], sample_step, skip)
 
@@ -314,7 +335,8 @@ def _prepare(tracks, st, et, lalim, lolim, sample_step, skip):
 
 
 def kriging(st, et, lalim=(0, 0), lolim=(0, 0), sample_step=5, skip=5, nKernels=1, output="rbfModel",
-            pkg="gp2d", kernelType=1, laser=1, tracks: Tracks = None, hyper: dict = None, device=None):
+            pkg="gp2d", kernelType=1, laser=1, tracks: Tracks = None, hyper: dict = None, device=None,
+            drop_drifters=()):
     """krig.kriging (krig.py:259-418): build the GP model(s) for a drifter data window.
 
     kernelType 1: scalar ARD RBF on (T, Y, X), one model per component (v, u);
@@ -329,7 +351,7 @@ def kriging(st, et, lalim=(0, 0), lolim=(0, 0), sample_step=5, skip=5, nKernels=
     h = dict(l_df=5.0, l_cf=5.0, ratio=None, noise=0.0025, variance=1.0, lengthscale=(1.0, 1.0, 1.0),
              var_t=1.0, l_t=1.0, temporal=True)
     h.update(hyper or {})
-    d = _prepare(tracks, st, et, lalim, lolim, sample_step, skip)
+    d = _prepare(tracks, st, et, lalim, lolim, sample_step, skip, drop_drifters)
     X, Xt = d["X"], d["Xt"]
     models = {}
     if kernelType == 1:
@@ -468,6 +490,24 @@ def predictTest(filename, device=None):
     return V, U, VV, UV
 
 
+def _prior_window(fm, tcenter, tlim, xlim, xrange, varname):
+    """scikit_prior's observation window (krig.py:146-167): observation and test points within
+    ±tlim of tcenter and within xrange of the x window, stacked [obs; test], and the chosen
+    velocity component.  Bit-exact with the reference (tests/golden/prior_window.npz); a
+    window holding a single point stays 2-D here (the reference's squeeze() would make it 1-D)."""
+    to, tt = fm["Xo"][:, 0], fm["Xt"][:, 0]
+    xo, xt = fm["Xo"][:, 2], fm["Xt"][:, 2]
+    ito = np.where((to >= tcenter - tlim) & (to <= tcenter + tlim) & (xo >= xlim[0] - xrange) & (xo <= xlim[1] + xrange))
+    itt = np.where((tt >= tcenter - tlim) & (tt <= tcenter + tlim) & (xt >= xlim[0] - xrange) & (xt <= xlim[1] + xrange))
+    Xo = fm["Xo"][ito, :].squeeze(0)
+    Xt = fm["Xt"][itt, :].squeeze(0)
+    XT = np.concatenate([Xo, Xt], axis=0)
+    obs = fm["obs"][ito, :].squeeze(0)
+    obst = fm["test_points"][itt, :].squeeze(0)
+    col = 1 if varname == "u" else 0
+    return XT, np.concatenate([obs[:, col], obst[:, col]])
+
+
 def scikit_prior(filename0, varname="v", dt=0, tlim=6, radar="", xlim=(0, 0), ylim=(0, 0), dx=0, ind=0, xrange=3,
                  HP=None, device=None):
     """krig.scikit_prior (krig.py:88-207): fixed-hyperparameter scalar GP
@@ -500,17 +540,7 @@ def scikit_prior(filename0, varname="v", dt=0, tlim=6, radar="", xlim=(0, 0), yl
         X = X[inc * it:inc * it + inc, :]
     filename = filename + "_" + str(np.round(tcenter[0], decimals=2)) + "h_scikit_"
     outFile = filename + str(ind) + ".nc"
-    to, tt = fm["Xo"][:, 0], fm["Xt"][:, 0]
-    xo, xt = fm["Xo"][:, 2], fm["Xt"][:, 2]
-    ito = np.where((to >= tcenter - tlim) & (to <= tcenter + tlim) & (xo >= xlim[0] - xrange) & (xo <= xlim[1] + xrange))
-    itt = np.where((tt >= tcenter - tlim) & (tt <= tcenter + tlim) & (xt >= xlim[0] - xrange) & (xt <= xlim[1] + xrange))
-    Xo = fm["Xo"][ito, :].squeeze(0)
-    Xt = fm["Xt"][itt, :].squeeze(0)
-    XT = np.concatenate([Xo, Xt], axis=0)
-    obs = fm["obs"][ito, :].squeeze(0)
-    obst = fm["test_points"][itt, :].squeeze(0)
-    col = 1 if varname == "u" else 0
-    u = np.concatenate([obs[:, col], obst[:, col]])
+    XT, u = _prior_window(fm, tcenter, tlim, xlim, xrange, varname)
     N = HP.size - 1
     variances = [HP[0]]
     lengths = [tuple(HP[1:4])]

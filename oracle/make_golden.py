@@ -358,6 +358,121 @@ def gen_st(gs, out):
     np.savez_compressed(os.path.join(out, "st_product_N150.npz"), **d)
 
 
+def gen_prep(out):
+    """Data-prep parity on real tracks: the reference's own getData
+    (krig.py:50-65 + its return expression, krig.py:77) and kriging selection block
+    (krig.py:274-381: boundData, projection, split, NaN filter, T,Y,X stacking) exec'd from
+    the file text (py2 `print` lines → `pass`), on simulTracks.pkl coordinates (transposed
+    to time × drifter, 12 steps × 240 drifters, with NaN tails injected so the filters act).
+    pyproj is absent: NAD83 is the build's documented stand-in (krig.nad83, restated here).
+    The outputs are large, so the fixture keeps SHA-256 digests of their bytes (bit-exact
+    check) plus shapes and a few rows."""
+    import hashlib
+    with open(os.path.join(REF, "krig.py")) as f:
+        lines = f.readlines()
+
+    def block(a, b, indent):
+        out = []
+        for ln in lines[a - 1:b]:
+            body = ln[indent:] if ln[:indent].strip() == "" else ln.lstrip()
+            if body.lstrip().startswith("print "):
+                out.append(body[:len(body) - len(body.lstrip())] + "pass\n")
+            else:
+                out.append(body)
+        return "".join(out)
+
+    getdata_body = block(50, 65, 6)                    # NaN-ing of drifter 238 … order[::-1]
+    ret = lines[76].strip()                            # krig.py:77
+    assert ret.startswith("return ")
+    ret = ret[len("return "):]
+    bound_src = block(79, 86, 0)                       # def boundData(...)
+    krig_body = block(274, 381, 3)                     # getData call … obst = …
+    tr = load_tracks()
+    rng = np.random.default_rng(41)
+    T, D = 12, 240
+    lat = np.array(tr.lat[:D, :T].T)
+    lon = np.array(tr.lon[:D, :T].T)
+    u = np.array(tr.u[:D, :T].T)
+    v = np.array(tr.v[:D, :T].T)
+    for c in rng.choice(D, 30, replace=False):         # drifters that stop reporting
+        k = int(rng.integers(1, T))
+        lat[k:, c] = np.nan
+        lon[k:, c] = np.nan
+    time = np.array(tr.time[:T])
+
+    class TR:
+        pass
+
+    R = 6371000.0
+    lat0, lon0 = 28.8, -88.6
+
+    def NAD83(lo, la):                                 # = krig.nad83
+        return (R * np.cos(np.deg2rad(lat0)) * np.deg2rad(np.asarray(lo, dtype=np.float64)),
+                R * np.deg2rad(np.asarray(la, dtype=np.float64)))
+
+    def getData(st, et, laser=1):
+        t = TR()
+        t.lat, t.lon, t.u, t.v, t.time = lat.copy(), lon.copy(), u.copy(), v.copy(), time.copy()
+        ns = {"np": np, "tr": t, "st": st, "et": et}
+        exec(compile(getdata_body, "krig.py[50:65]", "exec"), ns)
+        return eval(ret, ns)
+
+    bns = {"np": np}
+    exec(compile(bound_src, "krig.py[79:86]", "exec"), bns)
+    x_ori, y_ori = NAD83(lon0, lat0)
+    d = dict(time=time, lat=lat, lon=lon, u=u, v=v)
+    cases = [dict(st=0, et=12, sample_step=5, skip=1, lalim=[0, 0], lolim=[0, 0]),
+             dict(st=0, et=12, sample_step=-2, skip=1, lalim=[0, 0], lolim=[0, 0]),
+             dict(st=1, et=11, sample_step=-3, skip=3, lalim=[0, 0], lolim=[0, 0]),
+             dict(st=0, et=12, sample_step=-1, skip=2, lalim=[0, 0],
+                  lolim=[float(np.nanpercentile(lon[0], 20)), float(np.nanpercentile(lon[0], 80))]),
+             dict(st=2, et=12, sample_step=4, skip=1, lolim=[0, 0],
+                  lalim=[float(np.nanpercentile(lat[0], 10)), float(np.nanpercentile(lat[0], 70))])]
+    names = ("X", "LL_o", "obs", "Xt", "LL_t", "obst")
+    for i, c in enumerate(cases):
+        ns = {"np": np, "getData": getData, "boundData": bns["boundData"], "NAD83": NAD83, "x_ori": x_ori, "output": "m",
+              "y_ori": y_ori, "laser": 1, **c}
+        exec(compile(krig_body, "krig.py[274:381]", "exec"), ns)
+        d[f"c{i}_args"] = np.array([c["st"], c["et"], c["sample_step"], c["skip"], *c["lalim"], *c["lolim"]],
+                                   dtype=np.float64)
+        for nm in names:
+            a = np.ascontiguousarray(ns[nm], dtype=np.float64)
+            d[f"c{i}_{nm}_shape"] = np.array(a.shape)
+            d[f"c{i}_{nm}_sha256"] = np.frombuffer(hashlib.sha256(a.tobytes()).digest(), dtype=np.uint8)
+            d[f"c{i}_{nm}_rows"] = a[[0, -1]] if a.shape[0] else a
+    d["ncases"] = np.array(len(cases))
+    np.savez_compressed(os.path.join(out, "prep_tracks.npz"), **d)
+
+
+def gen_prior_window(out):
+    """scikit_prior's observation window (krig.py:146-157 and the component choice at
+    krig.py:164-167), exec'd from the file text on seeded (T, Y, X) observation / test arrays,
+    for several windows."""
+    with open(os.path.join(REF, "krig.py")) as f:
+        lines = f.readlines()
+    sel = "".join(("pass\n" if ln.strip().startswith("print ") else ln[3:]) for ln in lines[145:157])  # 146-157
+    comp = "".join(ln[3:] for ln in lines[163:167])          # krig.py:164-167
+    d = {}
+    rng = np.random.default_rng(9)
+    Xo = np.stack([rng.uniform(0, 6, 400), rng.uniform(-20, 20, 400), rng.uniform(-30, 30, 400)], 1)
+    Xt = np.stack([rng.uniform(0, 6, 300), rng.uniform(-20, 20, 300), rng.uniform(-30, 30, 300)], 1)
+    obs = rng.normal(size=(400, 2))
+    obst = rng.normal(size=(300, 2))
+    fm = {"Xo": Xo, "Xt": Xt, "obs": obs, "test_points": obst}
+    d.update(Xo=Xo, Xt=Xt, obs=obs, test_points=obst)
+    cases = [(3.0, 6, [-10.0, 10.0], 3, "v"), (1.0, 2, [0.0, 25.0], 0, "u"), (5.5, 1, [-40.0, 40.0], 10, "v")]
+    for i, (tc, tlim, xlim, xrange, varname) in enumerate(cases):
+        ns = {"np": np, "fm": fm, "tcenter": np.array([tc]), "tlim": tlim, "xlim": xlim, "xrange": xrange,
+              "varname": varname}
+        exec(compile(sel, "krig.py[146:157]", "exec"), ns)
+        exec(compile(comp, "krig.py[164:167]", "exec"), ns)
+        d[f"c{i}_args"] = np.array([tc, tlim, xlim[0], xlim[1], xrange, 1.0 if varname == "u" else 0.0])
+        d[f"c{i}_XT"] = np.concatenate([ns["Xo"], ns["Xt"]], axis=0)
+        d[f"c{i}_u"] = ns["u"][:, 0]
+    d["ncases"] = np.array(len(cases))
+    np.savez_compressed(os.path.join(out, "prior_window.npz"), **d)
+
+
 def gen_indices(out):
     """Split index arrays, verbatim reference expression (GP_laser.py:81-83, krig.py:335-337)."""
     sizes = list(range(30, 40)) + list(range(128, 140)) + [257, 1000, 1031, 3000, 12288]
@@ -401,7 +516,8 @@ def main():
     jobs = dict(small=lambda: gen_small(gs, a.out), laser=lambda: gen_laser(gs, a.out),
                 mykernel=lambda: gen_mykernel(gs, a.out), sklearn=lambda: gen_sklearn(a.out),
                 indices=lambda: gen_indices(a.out), grids=lambda: gen_grids(a.out),
-                lml=lambda: gen_lml(gs, a.out), st=lambda: gen_st(gs, a.out))
+                lml=lambda: gen_lml(gs, a.out), st=lambda: gen_st(gs, a.out),
+                prep=lambda: gen_prep(a.out), window=lambda: gen_prior_window(a.out))
     for name, fn in jobs.items():
         if a.only and name not in a.only.split(","):
             continue

@@ -116,3 +116,36 @@ def test_shard_ranges_cover_and_align():
             for (a, b), (c, d) in zip(parts, parts[1:]):
                 assert b == c
             assert all(a % 64 == 0 or a == m for a, _ in parts)
+
+
+@pytest.mark.parametrize("case", range(5))
+def test_data_prep_bit_exact_on_tracks(golden, case):
+    """krig's getData / boundData / projection / split / NaN filter / T,Y,X stacking vs the
+    reference's own code (krig.py:50-77, 79-86, 274-381 exec'd by oracle/make_golden.py) on
+    simulTracks coordinates with NaN tails and the hard-coded drifter-238 exclusion:
+    bit-exact (SHA-256 of every output array)."""
+    import hashlib
+    from gp2d import krig as K
+    g = golden("prep_tracks.npz")
+    tr = K.Tracks(g["time"], g["lat"], g["lon"], g["u"], g["v"])
+    st, et, ss, skip, la0, la1, lo0, lo1 = g[f"c{case}_args"]
+    d = K._prepare(tr, int(st), int(et), (la0, la1), (lo0, lo1), int(ss), int(skip), drop_drifters=(238,))
+    got = dict(X=d["X"], LL_o=d["LL_o"], obs=np.concatenate([d["vo"], d["uo"]], 1), Xt=d["Xt"], LL_t=d["LL_t"],
+               obst=np.concatenate([d["vt"], d["ut"]], 1))
+    for nm, a in got.items():
+        a = np.ascontiguousarray(a, dtype=np.float64)
+        assert tuple(a.shape) == tuple(g[f"c{case}_{nm}_shape"]), nm
+        if a.shape[0]:
+            assert np.array_equal(a[[0, -1]], g[f"c{case}_{nm}_rows"]), nm
+        assert hashlib.sha256(a.tobytes()).digest() == g[f"c{case}_{nm}_sha256"].tobytes(), nm
+
+
+@pytest.mark.parametrize("case", range(3))
+def test_prior_window_bit_exact(golden, case):
+    """scikit_prior's observation window (krig.py:146-167, exec'd by make_golden) — bit-exact."""
+    from gp2d import krig as K
+    g = golden("prior_window.npz")
+    tc, tlim, x0, x1, xrange, comp = g[f"c{case}_args"]
+    fm = {k: g[k] for k in ("Xo", "Xt", "obs", "test_points")}
+    XT, u = K._prior_window(fm, np.array([tc]), tlim, (x0, x1), xrange, "u" if comp else "v")
+    assert np.array_equal(XT, g[f"c{case}_XT"]) and np.array_equal(u, g[f"c{case}_u"])
