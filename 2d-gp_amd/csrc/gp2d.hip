@@ -13,6 +13,7 @@
 #include "../../include/gp2d.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <mutex>
 #include <string>
@@ -193,33 +194,56 @@ int gp2d_assemble(const double* xa, int64_t na, int64_t na_pad, const double* xb
 size_t gp2d_potrf_workspace(int64_t) { return 0; }
 
 namespace {
-// Side stream + event pool for the POTRF look-ahead (one per device, created lazily).
-struct SideStreams {
+// POTRF streams (one set per device, created lazily): `crit` carries the critical path
+// (block-column update, diagonal block, panel TRSM) at the highest priority, `bulk` the
+// trailing SYRK.  GP2D_CU_RESERVE=R (R > 0) gives `crit` CUs [0, R) and `bulk` the rest
+// through hardware CU masks, so the single-workgroup diagonal kernel never shares a CU with
+// SYRK tiles.
+struct FactorStreams {
   std::mutex mu;
-  std::vector<hipStream_t> side;   // indexed by device
+  std::vector<hipStream_t> crit, bulk;   // indexed by device
   std::vector<std::vector<hipEvent_t>> ev;
 };
-SideStreams g_side;
+FactorStreams g_fs;
 
-int side_stream(hipStream_t* out, std::vector<hipEvent_t>** evs) {
+static int cu_reserve() {
+  const char* e = std::getenv("GP2D_CU_RESERVE");
+  return e ? std::max(0, std::atoi(e)) : 0;
+}
+
+int factor_streams(hipStream_t* crit, hipStream_t* bulk, std::vector<hipEvent_t>** evs) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) { set_error("hipGetDevice failed"); return -1; }
-  std::lock_guard<std::mutex> lk(g_side.mu);
-  if ((int)g_side.side.size() <= dev) { g_side.side.resize(dev + 1, nullptr); g_side.ev.resize(dev + 1); }
-  if (!g_side.side[dev]) {
-    // highest priority: the side stream carries the POTRF critical path (diagonal block +
-    // panel), whose single-workgroup kernel must not queue behind the trailing SYRK tiles
-    int lo = 0, hi = 0;
-    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) { lo = 0; hi = 0; }
-    if (hipStreamCreateWithPriority(&g_side.side[dev], hipStreamNonBlocking, hi) != hipSuccess) {
-      set_error("hipStreamCreate failed"); return -1;
+  std::lock_guard<std::mutex> lk(g_fs.mu);
+  if ((int)g_fs.crit.size() <= dev) {
+    g_fs.crit.resize(dev + 1, nullptr); g_fs.bulk.resize(dev + 1, nullptr); g_fs.ev.resize(dev + 1);
+  }
+  if (!g_fs.crit[dev]) {
+    const int R = cu_reserve();
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) ncu = 0;
+    if (R > 0 && R < ncu) {
+      std::vector<uint32_t> mc((ncu + 31) / 32, 0u), mb((ncu + 31) / 32, 0u);
+      for (int c = 0; c < ncu; ++c) (c < R ? mc : mb)[c / 32] |= 1u << (c % 32);
+      if (hipExtStreamCreateWithCUMask(&g_fs.crit[dev], (uint32_t)mc.size(), mc.data()) != hipSuccess ||
+          hipExtStreamCreateWithCUMask(&g_fs.bulk[dev], (uint32_t)mb.size(), mb.data()) != hipSuccess) {
+        set_error("hipExtStreamCreateWithCUMask failed"); return -1;
+      }
+    } else {
+      int lo = 0, hi = 0;
+      if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) { lo = 0; hi = 0; }
+      if (hipStreamCreateWithPriority(&g_fs.crit[dev], hipStreamNonBlocking, hi) != hipSuccess ||
+          hipStreamCreateWithPriority(&g_fs.bulk[dev], hipStreamNonBlocking, lo) != hipSuccess) {
+        set_error("hipStreamCreate failed"); return -1;
+      }
     }
-    g_side.ev[dev].resize(2);
-    for (auto& e : g_side.ev[dev])
+    g_fs.ev[dev].resize(3);
+    for (auto& e : g_fs.ev[dev])
       if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) { set_error("hipEventCreate failed"); return -1; }
   }
-  *out = g_side.side[dev];
-  *evs = &g_side.ev[dev];
+  *crit = g_fs.crit[dev];
+  *bulk = g_fs.bulk[dev];
+  *evs = &g_fs.ev[dev];
   return 0;
 }
 
@@ -235,40 +259,35 @@ int launch_panel(double* A, int64_t lda, int k, int64_t n, const double* dinv, h
 }
 }  // namespace
 
-// Right-looking blocked Cholesky with one step of look-ahead: after step k's panel, the
-// update of block column k+1 runs first; block column k+1's diagonal factorisation and
-// panel then run on a side stream while the rest of step k's trailing SYRK (columns ≥ k+2)
-// runs on the caller's stream, so the single-workgroup diagonal kernel hides under the
-// chip-wide SYRK.  Data regions of the two streams are disjoint (column block k+1 vs ≥ k+2).
+// Right-looking blocked Cholesky with one step of look-ahead on two internal streams:
+//   crit: update of block column k+1 → its diagonal factorisation → its panel TRSM,
+//   bulk: the rest of step k's trailing SYRK (columns ≥ k+2),
+// so the single-workgroup diagonal kernel hides under the chip-wide SYRK.  Data regions are
+// disjoint (column block k+1 vs ≥ k+2); per step, bulk waits for panel k and crit waits for
+// SYRK k before it updates block column k+2.  The caller's stream is joined at both ends.
+#define GP2D_EV(call) do { if ((call) != hipSuccess) { set_error(#call " failed"); return -1; } } while (0)
 int gp2d_potrf(double* A, int64_t n, int64_t lda, double* dinv, int* info_dev, void*, size_t, void* stream) {
   GP2D_REQUIRE(n % NB == 0 && n > 0, "potrf: n must be a positive multiple of 128");
   GP2D_REQUIRE(lda >= n && lda % 2 == 0, "potrf: lda must be >= n and even");
   GP2D_REQUIRE(dinv != nullptr, "potrf: dinv buffer is required");
   hipStream_t s = S(stream);
   const int nb = (int)(n / NB);
-  hipStream_t s2;
+  hipStream_t sc, sb;
   std::vector<hipEvent_t>* ev;
-  GP2D_CHECK(side_stream(&s2, &ev));
-  hipEvent_t e_col = (*ev)[0], e_pan = (*ev)[1];
-  potrf_diag_kernel<<<1, 256, 0, s>>>(A, lda, 0, dinv, info_dev);
+  GP2D_CHECK(factor_streams(&sc, &sb, &ev));
+  hipEvent_t e_pan = (*ev)[0], e_syrk = (*ev)[1], e_join = (*ev)[2];
+  GP2D_EV(hipEventRecord(e_join, s));
+  GP2D_EV(hipStreamWaitEvent(sc, e_join, 0));
+  GP2D_EV(hipStreamWaitEvent(sb, e_join, 0));
+  potrf_diag_kernel<<<1, 256, 0, sc>>>(A, lda, 0, dinv, info_dev);
   GP2D_CHECK(check_launch("potrf_diag_kernel"));
-  GP2D_CHECK(launch_panel(A, lda, 0, n, dinv, s));
+  GP2D_CHECK(launch_panel(A, lda, 0, n, dinv, sc));
+  GP2D_EV(hipEventRecord(e_pan, sc));
   for (int k = 0; k + 1 < nb; ++k) {
     const int k0 = k * NB, k1 = k0 + NB;
     const double* Lk = A + (int64_t)k1 * lda + k0;     // panel k, rows ≥ k+1
-    // (1) update block column k+1:  A[k+1.., k+1] −= L[k+1.., k] · L[k+1, k]ᵀ
-    //     (B = rows of block k+1 = the first NB rows of the panel)
-    gemm_f64_panel_kernel<<<(unsigned)((n - k1) / PNL_R), 256, 0, s>>>(Lk, lda, Lk, lda, A + (int64_t)k1 * lda + k1,
-                                                                       lda, -1.0, 1.0);
-    GP2D_CHECK(check_launch("gemm_f64_panel_kernel"));
-    if (hipEventRecord(e_col, s) != hipSuccess) { set_error("hipEventRecord failed"); return -1; }
-    // (2) side stream: factor diagonal block k+1 and its panel
-    if (hipStreamWaitEvent(s2, e_col, 0) != hipSuccess) { set_error("hipStreamWaitEvent failed"); return -1; }
-    potrf_diag_kernel<<<1, 256, 0, s2>>>(A, lda, k1, dinv, info_dev);
-    GP2D_CHECK(check_launch("potrf_diag_kernel"));
-    GP2D_CHECK(launch_panel(A, lda, k + 1, n, dinv, s2));
-    if (hipEventRecord(e_pan, s2) != hipSuccess) { set_error("hipEventRecord failed"); return -1; }
-    // (3) rest of the trailing update, columns ≥ k+2 (lower tiles)
+    // bulk: trailing update of columns ≥ k+2 (lower tiles) once panel k is done
+    GP2D_EV(hipStreamWaitEvent(sb, e_pan, 0));
     const int rest = (int)(n - k1 - NB);
     if (rest > 0) {
       GemmParams q = gemm_params();
@@ -277,11 +296,25 @@ int gp2d_potrf(double* A, int64_t n, int64_t lda, double* dinv, int* info_dev, v
       q.C = A + (int64_t)(k1 + NB) * lda + (k1 + NB); q.ldc = lda;
       q.M = rest; q.N = rest; q.K = NB;
       q.alpha = -1.0; q.beta = 1.0; q.c_lower = 1;
-      GP2D_CHECK((launch_gemm<true, EPI_STORE>(q, 1, s)));
+      GP2D_CHECK((launch_gemm<true, EPI_STORE>(q, 1, sb)));
     }
-    // next step needs panel k+1
-    if (hipStreamWaitEvent(s, e_pan, 0) != hipSuccess) { set_error("hipStreamWaitEvent failed"); return -1; }
+    GP2D_EV(hipEventRecord(e_syrk, sb));
+    // crit: A[k+1.., k+1] −= L[k+1.., k] · L[k+1, k]ᵀ (B = the first NB rows of the panel),
+    // then factor diagonal block k+1 and its panel
+    gemm_f64_panel_kernel<<<(unsigned)((n - k1) / PNL_R), 256, 0, sc>>>(Lk, lda, Lk, lda, A + (int64_t)k1 * lda + k1,
+                                                                        lda, -1.0, 1.0);
+    GP2D_CHECK(check_launch("gemm_f64_panel_kernel"));
+    potrf_diag_kernel<<<1, 256, 0, sc>>>(A, lda, k1, dinv, info_dev);
+    GP2D_CHECK(check_launch("potrf_diag_kernel"));
+    GP2D_CHECK(launch_panel(A, lda, k + 1, n, dinv, sc));
+    GP2D_EV(hipEventRecord(e_pan, sc));
+    // block column k+2 must have received SYRK k before crit updates it
+    GP2D_EV(hipStreamWaitEvent(sc, e_syrk, 0));
   }
+  GP2D_EV(hipEventRecord(e_join, sb));
+  GP2D_EV(hipStreamWaitEvent(sc, e_join, 0));
+  GP2D_EV(hipEventRecord(e_join, sc));
+  GP2D_EV(hipStreamWaitEvent(s, e_join, 0));
   dim3 zg((unsigned)((n / 2 + 255) / 256), (unsigned)n);
   zero_upper_kernel<<<zg, 256, 0, s>>>(A, n, lda);
   return check_launch("zero_upper_kernel");
@@ -494,6 +527,84 @@ size_t gp2d_predict_ozaki_workspace(int64_t n, int64_t chunk) {
          + sizeof(double) * ((size_t)(n / 2 / OZ_KS_T + 1) + (size_t)(n / OZ_CRT_ROWS + 1)) * ncols;
 }
 
+// One chunked predict over the m grid points.  K* residue planes come either from the
+// inline ozaki_kstar_kernel (pre == nullptr: planes in the workspace, mean partials Σ α·K*)
+// or from gp2d_ozaki_kstar run earlier (pre: nmod_pre planes per chunk, chunk c at
+// pre + c·pre_stride; the mean is then Σ_i V_ij·β_i from the CRT kernel, β = W·y).
+static int predict_ozaki_impl(const int8_t* wres, const double* rowscale, int nmod, int64_t n,
+                              const double* alpha, const double* beta, const double* xtr, int64_t ntr,
+                              int64_t ntr_pad, const double* xg, int64_t m, const gp2d_kernel_t* k, int var_mode,
+                              double noise, int compute_var, double* mean, double* var, int64_t chunk,
+                              int8_t* bres, uint8_t* cres, double* pm, double* P, const int8_t* pre,
+                              int nmod_pre, size_t pre_stride, hipStream_t s) {
+  OzakiConsts oc;
+  GP2D_CHECK(make_ozaki_consts(nmod, k, oc));
+  const int nm = oc.nmod;
+  const int64_t nmseg = (ntr_pad + OZ_KS_T - 1) / OZ_KS_T;
+  const int64_t npseg = (n + OZ_CRT_ROWS - 1) / OZ_CRT_ROWS;
+  const double kss = gp2d_kernel_diag(k);
+  const double add = (var_mode == GP2D_VAR_LATENT) ? 0.0 : noise;
+  const int clip = (var_mode == GP2D_VAR_CLIPPED);
+  const VecParams vp = make_vec_params(k);
+  OzakiConsts oc_mean_only = oc;
+  oc_mean_only.nmod = 0;   // mean only: K*·α without the residue planes
+  int64_t ci = 0;
+  for (int64_t c0 = 0; c0 < m; c0 += chunk, ++ci) {
+    const int64_t cv = std::min<int64_t>(chunk, m - c0);
+    const int64_t cp = round_up(cv, IBN);   // whole 256-row tiles per component half (B aliasing)
+    const int64_t ncols = 2 * cp;
+    const int8_t* B = bres;
+    size_t bplane = (size_t)ncols * n;
+    if (pre) {
+      B = pre + (size_t)ci * pre_stride;
+      bplane = (size_t)ncols * n;
+    } else {
+      ozaki_kstar_kernel<<<dim3((unsigned)nmseg, (unsigned)(cp / OZ_KS_P)), 256, 0, s>>>(
+          xtr, ntr, ntr_pad, xg + point_dim(k) * c0, cv, cp, vp, alpha, compute_var ? oc : oc_mean_only, bres, pm);
+      GP2D_CHECK(check_launch("ozaki_kstar_kernel"));
+    }
+    if (compute_var) {
+      hipEvent_t e0 = nullptr, e1 = nullptr;
+      {
+        std::lock_guard<std::mutex> lk(g_timing.mu);
+        if (g_timing.on) { e0 = g_timing.get(); e1 = g_timing.get(); hipEventRecord(e0, s); }
+      }
+      const dim3 ggrid((unsigned)(ncols / IBN), (unsigned)(n / IBM));
+      for (int l = 0; l < nm; ++l) {
+        igemm_nt_mod_kernel<<<ggrid, 512, 0, s>>>(wres + (size_t)l * n * n, B + (size_t)l * bplane,
+                                                  cres + (size_t)l * n * ncols, n, (int)n, (int)ncols, (int)n, 1,
+                                                  oc.m[l], oc.inv_m[l], (int)(cp / IBN), (int)(ntr_pad / IBK));
+        GP2D_CHECK(check_launch("igemm_nt_mod_kernel"));
+      }
+      if (e0) {
+        std::lock_guard<std::mutex> lk(g_timing.mu);
+        hipEventRecord(e1, s);
+        g_timing.ev.push_back({e0, e1});
+        const double nv = 2.0 * (double)ntr;
+        g_timing.flops.push_back(2.0 * (double)cv * nv * nv);  // FP64-equivalent algorithmic flop
+      }
+      const dim3 cgrid((unsigned)((ncols + OZ_CRT_BCOLS - 1) / OZ_CRT_BCOLS), (unsigned)npseg);
+      if (pre) {
+        ozaki_crt_colsq_kernel<true><<<cgrid, 256, 0, s>>>(cres, n, ncols, oc, rowscale, P, beta, pm);
+      } else {
+        ozaki_crt_colsq_kernel<false><<<cgrid, 256, 0, s>>>(cres, n, ncols, oc, rowscale, P, nullptr, nullptr);
+      }
+      GP2D_CHECK(check_launch("ozaki_crt_colsq_kernel"));
+    }
+    predict_finalize_kernel<<<(unsigned)((ncols + 255) / 256), 256, 0, s>>>(
+        pm, pre ? npseg : nmseg, P, npseg, ncols, cp, cv, c0, m, kss, add, clip, compute_var, mean, var);
+    GP2D_CHECK(check_launch("predict_finalize_kernel"));
+  }
+  (void)nmod_pre;
+  return 0;
+}
+
+// partial-sum doubles per chunk column: mean partials (max of the K*-segment and CRT-segment
+// counts) + variance partials
+static size_t ozaki_partials(int64_t n) {
+  return (size_t)std::max<int64_t>(n / 2 / OZ_KS_T + 1, n / OZ_CRT_ROWS + 1) + (size_t)(n / OZ_CRT_ROWS + 1);
+}
+
 int gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int nmod, int64_t n, const double* alpha,
                        const double* xtr,
                        int64_t ntr, int64_t ntr_pad, const double* xg, int64_t m, const gp2d_kernel_t* k,
@@ -506,60 +617,104 @@ int gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int nmod, int
   GP2D_REQUIRE(work != nullptr && work_bytes >= gp2d_predict_ozaki_workspace(n, chunk), "ozaki: workspace too small");
   GP2D_REQUIRE(var_mode >= 0 && var_mode <= 2, "predict: bad var_mode");
   if (m <= 0) return 0;
-  hipStream_t s = S(stream);
   GP2D_REQUIRE(nmod > 0 && nmod <= ozaki_nmod_for(n), "ozaki: nmod exceeds the worst-case count the workspace is sized for");
-  OzakiConsts oc;
-  GP2D_CHECK(make_ozaki_consts(nmod, k, oc));
-  const int nm = oc.nmod;
+  const int nm = nmod;
   const int64_t ncols_max = 2 * round_up(chunk, IBN);
   int8_t* bres = reinterpret_cast<int8_t*>(work);
   uint8_t* cres = reinterpret_cast<uint8_t*>(bres + (size_t)nm * n * ncols_max);
   double* pm = reinterpret_cast<double*>(cres + (size_t)nm * n * ncols_max);
-  const int64_t nmseg = (ntr_pad + OZ_KS_T - 1) / OZ_KS_T;
   double* P = pm + (size_t)(n / 2 / OZ_KS_T + 1) * ncols_max;
-  const int64_t npseg = (n + OZ_CRT_ROWS - 1) / OZ_CRT_ROWS;
+  return predict_ozaki_impl(wres, rowscale, nmod, n, alpha, nullptr, xtr, ntr, ntr_pad, xg, m, k, var_mode, noise,
+                            compute_var, mean, var, chunk, bres, cres, pm, P, nullptr, 0, 0, S(stream));
+}
+
+// ---- K* residue planes ahead of the fit (the planes need no α: see the CRT kernel)
+int gp2d_ozaki_nmod_apriori(int64_t n, const gp2d_kernel_t* k, double diag_add) {
+  // gp2d_ozaki_prepare's per-row bound (b) with the largest row exponent any fit can have:
+  // W_ii = 1/L_ii ≥ 1/√(K_y,ii) (L_ii² = K_y,ii − Σ L_ik²), so max_k |W_ik| ≥ 1/√(kss + diag_add)
+  // and s_i = p−1−⌊log2 max|W_i|⌋ ≤ s_max.  (1 − 2^-40) absorbs the rounding of L_ii; the
+  // identity rows of padded points take bound (a) = 1.01·2^{2p−2}.  prepare's data-driven
+  // count never exceeds this one.
+  if (validate_kernel(k) != 0 || !is_vector_family(k) || n <= 0) return -1;
   const double kss = gp2d_kernel_diag(k);
-  const double add = (var_mode == GP2D_VAR_LATENT) ? 0.0 : noise;
-  const int clip = (var_mode == GP2D_VAR_CLIPPED);
+  const double dmin = (1.0 - std::ldexp(1.0, -40)) / std::sqrt(kss + diag_add);
+  const int smax = OZ_P - 1 - (int)std::floor(std::log2(dmin));
+  OzakiConsts probe;
+  if (make_ozaki_consts(1, k, probe) != 0) return -1;
+  const double sq = 2.0 * std::sqrt(kss);
+  const double b = std::ldexp(sq, smax + probe.sB) + std::ldexp((double)n, OZ_P - 2) + std::ldexp((double)n, OZ_P) +
+                   (double)n;
+  const double a_id = 1.01 * std::ldexp(1.0, 2 * OZ_P - 2);
+  return ozaki_nmod_bits(std::log2(std::max(b, a_id)));
+}
+
+size_t gp2d_ozaki_kstar_bytes(int64_t n, int64_t m, int64_t chunk, int nmod) {
+  if (n <= 0 || m <= 0 || chunk <= 0 || nmod <= 0) return 0;
+  const int64_t nchunks = (m + chunk - 1) / chunk;
+  return (size_t)nchunks * (size_t)nmod * (size_t)n * (size_t)(2 * round_up(chunk, IBN));
+}
+
+int gp2d_ozaki_kstar(const double* xtr, int64_t ntr, int64_t ntr_pad, const double* xg, int64_t m,
+                     const gp2d_kernel_t* k, int nmod, int64_t chunk, int8_t* bres, size_t bres_bytes,
+                     void* stream) {
+  GP2D_CHECK(validate_kernel(k));
+  GP2D_REQUIRE(is_vector_family(k), "ozaki: vector families only");
+  const int64_t n = 2 * ntr_pad;
+  GP2D_REQUIRE(ntr_pad > 0 && n % IBM == 0 && ntr <= ntr_pad, "ozaki_kstar: 2·ntr_pad must be a multiple of 256");
+  GP2D_REQUIRE(chunk > 0 && chunk % (IBN / 2) == 0, "ozaki_kstar: chunk must be a positive multiple of 128");
+  GP2D_REQUIRE(nmod > 0 && nmod <= OZ_MAXMOD, "ozaki_kstar: bad number of moduli");
+  if (m <= 0) return 0;
+  GP2D_REQUIRE(bres != nullptr && bres_bytes >= gp2d_ozaki_kstar_bytes(n, m, chunk, nmod),
+               "ozaki_kstar: plane buffer too small");
+  OzakiConsts oc;
+  GP2D_CHECK(make_ozaki_consts(nmod, k, oc));
   const VecParams vp = make_vec_params(k);
-  OzakiConsts oc_mean_only = oc;
-  oc_mean_only.nmod = 0;   // mean only: K*·α without the residue planes
-  for (int64_t c0 = 0; c0 < m; c0 += chunk) {
+  const int64_t nmseg = (ntr_pad + OZ_KS_T - 1) / OZ_KS_T;
+  const size_t stride = (size_t)nmod * (size_t)n * (size_t)(2 * round_up(chunk, IBN));
+  hipStream_t s = S(stream);
+  int64_t ci = 0;
+  for (int64_t c0 = 0; c0 < m; c0 += chunk, ++ci) {
     const int64_t cv = std::min<int64_t>(chunk, m - c0);
-    const int64_t cp = round_up(cv, IBN);   // whole 256-row tiles per component half (B aliasing)
-    const int64_t ncols = 2 * cp;
+    const int64_t cp = round_up(cv, IBN);
     ozaki_kstar_kernel<<<dim3((unsigned)nmseg, (unsigned)(cp / OZ_KS_P)), 256, 0, s>>>(
-        xtr, ntr, ntr_pad, xg + point_dim(k) * c0, cv, cp, vp, alpha, compute_var ? oc : oc_mean_only, bres, pm);
+        xtr, ntr, ntr_pad, xg + point_dim(k) * c0, cv, cp, vp, nullptr, oc, bres + ci * stride, nullptr);
     GP2D_CHECK(check_launch("ozaki_kstar_kernel"));
-    if (compute_var) {
-      hipEvent_t e0 = nullptr, e1 = nullptr;
-      {
-        std::lock_guard<std::mutex> lk(g_timing.mu);
-        if (g_timing.on) { e0 = g_timing.get(); e1 = g_timing.get(); hipEventRecord(e0, s); }
-      }
-      const dim3 ggrid((unsigned)(ncols / IBN), (unsigned)(n / IBM));
-      for (int l = 0; l < nm; ++l) {
-        igemm_nt_mod_kernel<<<ggrid, 512, 0, s>>>(wres + (size_t)l * n * n, bres + (size_t)l * ncols * n,
-                                                  cres + (size_t)l * n * ncols, n, (int)n, (int)ncols, (int)n, 1,
-                                                  oc.m[l], oc.inv_m[l], (int)(cp / IBN), (int)(ntr_pad / IBK));
-        GP2D_CHECK(check_launch("igemm_nt_mod_kernel"));
-      }
-      if (e0) {
-        std::lock_guard<std::mutex> lk(g_timing.mu);
-        hipEventRecord(e1, s);
-        g_timing.ev.push_back({e0, e1});
-        const double nv = 2.0 * (double)ntr;
-        g_timing.flops.push_back(2.0 * (double)cv * nv * nv);  // FP64-equivalent algorithmic flop
-      }
-      ozaki_crt_colsq_kernel<<<dim3((unsigned)((ncols + 3) / 4), (unsigned)npseg), 256, 0, s>>>(
-          cres, n, ncols, oc, rowscale, P);
-      GP2D_CHECK(check_launch("ozaki_crt_colsq_kernel"));
-    }
-    predict_finalize_kernel<<<(unsigned)((ncols + 255) / 256), 256, 0, s>>>(
-        pm, nmseg, P, npseg, ncols, cp, cv, c0, m, kss, add, clip, compute_var, mean, var);
-    GP2D_CHECK(check_launch("predict_finalize_kernel"));
   }
   return 0;
+}
+
+size_t gp2d_predict_ozaki_planes_workspace(int64_t n, int64_t chunk) {
+  const int nm = ozaki_nmod_for(n);
+  if (nm <= 0 || n <= 0) return 0;
+  const int64_t ncols = 2 * round_up(chunk < 1 ? 1 : chunk, IBN);
+  return (size_t)nm * (size_t)n * (size_t)ncols + sizeof(double) * ozaki_partials(n) * (size_t)ncols;
+}
+
+int gp2d_predict_ozaki_planes(const int8_t* wres, const double* rowscale, int nmod, int64_t n, const double* beta,
+                              const int8_t* bres, int nmod_b, int64_t ntr, int64_t ntr_pad, int64_t m,
+                              const gp2d_kernel_t* k, int var_mode, double noise, double* mean, double* var,
+                              int64_t chunk, void* work, size_t work_bytes, void* stream) {
+  GP2D_CHECK(validate_kernel(k));
+  GP2D_REQUIRE(is_vector_family(k), "ozaki: vector families only");
+  GP2D_REQUIRE(n == 2 * ntr_pad && n % IBM == 0, "ozaki: n must equal 2·ntr_pad and be a multiple of 256");
+  GP2D_REQUIRE(chunk > 0 && chunk % (IBN / 2) == 0, "ozaki: chunk must be a positive multiple of 128");
+  GP2D_REQUIRE(work != nullptr && work_bytes >= gp2d_predict_ozaki_planes_workspace(n, chunk),
+               "ozaki: workspace too small");
+  GP2D_REQUIRE(var_mode >= 0 && var_mode <= 2, "predict: bad var_mode");
+  GP2D_REQUIRE(beta != nullptr && bres != nullptr, "ozaki_planes: beta and the K* planes are required");
+  if (m <= 0) return 0;
+  GP2D_REQUIRE(nmod > 0 && nmod <= ozaki_nmod_for(n), "ozaki: nmod exceeds the worst-case count");
+  if (nmod > nmod_b) {
+    set_error("ozaki_planes: the fit needs more moduli than the K* planes carry");
+    return -3;
+  }
+  const int64_t ncols_max = 2 * round_up(chunk, IBN);
+  uint8_t* cres = reinterpret_cast<uint8_t*>(work);
+  double* pm = reinterpret_cast<double*>(cres + (size_t)nmod * n * ncols_max);
+  double* P = pm + (size_t)std::max<int64_t>(n / 2 / OZ_KS_T + 1, n / OZ_CRT_ROWS + 1) * ncols_max;
+  const size_t stride = (size_t)nmod_b * (size_t)n * (size_t)ncols_max;
+  return predict_ozaki_impl(wres, rowscale, nmod, n, nullptr, beta, nullptr, ntr, ntr_pad, nullptr, m, k, var_mode,
+                            noise, 1, mean, var, chunk, nullptr, cres, pm, P, bres, nmod_b, stride, S(stream));
 }
 
 // ------------------------------------------------- LOG MARGINAL LIKELIHOOD (§8f.1)

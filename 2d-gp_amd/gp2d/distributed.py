@@ -24,29 +24,31 @@ def world():
 
 
 def broadcast_fit(gp: E.GPFit | None, spec: E.KernelSpec, noise: float, x, device, src: int = 0) -> E.GPFit:
-    """Broadcast W, α and the training points from `src` to every rank (RCCL
+    """Broadcast W, α (with β = W·y when the fit has it) and the training points from `src` to every rank (RCCL
     ncclBroadcast under the 'nccl' backend).  Ranks other than `src` pass gp=None."""
     ws, rank = world()
     if ws == 1:
         return gp
-    meta = torch.zeros(3, dtype=torch.int64, device=device)
+    meta = torch.zeros(4, dtype=torch.int64, device=device)
     if rank == src:
-        meta[0], meta[1], meta[2] = gp.n, gp.n_train, gp.n_pad
+        meta[0], meta[1], meta[2], meta[3] = gp.n, gp.n_train, gp.n_pad, int(gp.beta is not None)
     dist.broadcast(meta, src)
-    n, ntr, npad = (int(v) for v in meta.tolist())
+    n, ntr, npad, has_beta = (int(v) for v in meta.tolist())
+    nab = 2 * n if has_beta else n
     if rank != src:
         W = torch.empty((n, n), dtype=torch.float64, device=device)
-        alpha = torch.empty(n, dtype=torch.float64, device=device)
+        ab = torch.empty(nab, dtype=torch.float64, device=device)
         X = torch.empty((ntr, spec.input_dim), dtype=torch.float64, device=device)
     else:
-        W, alpha, X = gp.W, gp.alpha, gp.x
+        W, X = gp.W, gp.x
+        ab = torch.cat([gp.alpha, gp.beta]) if has_beta else gp.alpha
     dist.broadcast(W, src)
-    dist.broadcast(alpha, src)
+    dist.broadcast(ab, src)   # α and β = W·y (the mean from precomputed K* planes)
     dist.broadcast(X, src)
     if rank == src:
         return gp
-    return E.GPFit(kernel=spec, noise=float(noise), x=X, n_train=ntr, n_pad=npad, W=W, alpha=alpha,
-                   device=torch.device(device))
+    return E.GPFit(kernel=spec, noise=float(noise), x=X, n_train=ntr, n_pad=npad, W=W, alpha=ab[:n],
+                   device=torch.device(device), beta=ab[n:] if has_beta else None)
 
 
 def fit_sharded(spec: E.KernelSpec, x, y, noise: float, device, mode: str = "bcast", jitter: float = 0.0,

@@ -141,6 +141,7 @@ class GPFit:
     info: int = 0
     extra: dict = field(default_factory=dict)
     y: torch.Tensor = None   # (n,) padded observations (LML)
+    beta: torch.Tensor = None  # (n,) W·y (the mean from precomputed K* planes: K*α = (W K*ᵀ)ᵀβ)
 
     @property
     def n(self) -> int:
@@ -163,6 +164,21 @@ def _pad_obs(y, n_train: int, n_pad: int, bd: int, device) -> torch.Tensor:
 VARIANCE_ENGINES = ("f64", "ozaki")
 
 
+def fit_layout(kernel: KernelSpec, n_train: int, variance: str = "f64"):
+    """(padded point count, matrix order n) of a fit: points padded to 64, n a multiple of
+    128 (of 256 for the ozaki engine, whose int8 GEMM tiles are 256 wide)."""
+    bd = kernel.block_dim
+    npad = padded_points(n_train)
+    n = bd * npad
+    if n % NB:  # scalar (ARD) family: the matrix order itself must be a multiple of 128
+        npad = (npad + NB - 1) // NB * NB
+        n = bd * npad
+    if variance == "ozaki" and n % 256:
+        npad = (npad + 127) // 128 * 128
+        n = bd * npad
+    return npad, n
+
+
 def fit(kernel: KernelSpec, x, y, noise: float, jitter: float = 0.0, device=None, variance: str = "f64") -> GPFit:
     """K_y = K(x,x) + (noise+jitter)·I → L = chol(K_y) → W = L⁻¹ → α = Wᵀ W y.
 
@@ -183,14 +199,7 @@ def fit(kernel: KernelSpec, x, y, noise: float, jitter: float = 0.0, device=None
     ntr = X.shape[0]
     if ntr < 1:
         raise ValueError("need at least one training point")
-    npad = padded_points(ntr)
-    n = bd * npad
-    if n % NB:  # scalar (ARD) family: the matrix order itself must be a multiple of 128
-        npad = (npad + NB - 1) // NB * NB
-        n = bd * npad
-    if variance == "ozaki" and n % 256:  # int8 GEMM tiles are 256 wide
-        npad = (npad + 127) // 128 * 128
-        n = bd * npad
+    npad, n = fit_layout(kernel, ntr, variance)
     s = _stream_handle(dev)
     desc = kernel.desc()
     A = torch.empty((n, n), dtype=torch.float64, device=dev)
@@ -214,7 +223,7 @@ def fit(kernel: KernelSpec, x, y, noise: float, jitter: float = 0.0, device=None
     pwork = torch.empty(pbytes // 8 + 1, dtype=torch.float64, device=dev)
     N.check(L.gp2d_potrs_inv(_ptr(A), n, n, _ptr(Y), _ptr(alpha), _ptr(pwork), pbytes, s), "gp2d_potrs_inv")
     gp = GPFit(kernel=kernel, noise=float(noise), x=X, n_train=ntr, n_pad=npad, W=A, alpha=alpha, device=dev,
-               y=Y)
+               y=Y, beta=pwork[:n])   # gp2d_potrs_inv leaves β = W·y at the head of its workspace
     if variance == "ozaki":
         ozaki_prepare(gp)
     return gp
@@ -232,6 +241,63 @@ def ozaki_prepare(gp: GPFit) -> GPFit:
                                  ctypes.byref(nmod), _stream_handle(gp.device)), "gp2d_ozaki_prepare")
     gp.extra["ozaki"] = (wres, rowscale, int(nmod.value))
     return gp
+
+
+@dataclass
+class KstarPlanes:
+    """INT8 residue planes of K*ᵀ for a whole grid (every chunk), generated ahead of the fit:
+    they depend on the training points, the grid and the kernel only (not on α), so they can
+    run on a side stream while the fit runs (gp2d_ozaki_kstar)."""
+    kernel: KernelSpec
+    x: torch.Tensor
+    m: int
+    n: int
+    n_pad: int
+    chunk: int
+    nmod: int
+    bres: torch.Tensor
+    event: torch.cuda.Event
+    xg: torch.Tensor = None
+
+
+def kstar_planes(kernel: KernelSpec, x, xg, noise: float, jitter: float = 0.0, chunk: int = 8192, stream=None,
+                 out: KstarPlanes | None = None, device=None) -> KstarPlanes:
+    """Launch the K* residue planes of grid `xg` against training points `x` on `stream`
+    (default: the current stream) after the current stream's pending work; returns at once.
+    The moduli count is gp2d_ozaki_nmod_apriori's bound for K_y,ii = kdiag + noise + jitter,
+    which covers any fit of these hyperparameters.  `out` reuses a previous buffer."""
+    if not kernel.is_vector:
+        raise ValueError("K* planes are an ozaki-engine feature (vector families)")
+    dev = _require_device(device)
+    L = N.lib()
+    d = kernel.input_dim
+    X = _as_points(x, d, dev)
+    G = _as_points(xg, d, dev)
+    ntr, m = X.shape[0], G.shape[0]
+    npad, n = fit_layout(kernel, ntr, "ozaki")
+    chunk = max(128, (int(chunk) + 127) // 128 * 128)
+    desc = kernel.desc()
+    nmod = int(L.gp2d_ozaki_nmod_apriori(n, ctypes.byref(desc), float(noise + jitter)))
+    if nmod <= 0:
+        N.check(-1, "gp2d_ozaki_nmod_apriori")
+    nbytes = int(L.gp2d_ozaki_kstar_bytes(n, m, chunk, nmod))
+    bres = out.bres if (out is not None and out.bres.numel() >= nbytes) else \
+        torch.empty(max(nbytes, 1), dtype=torch.int8, device=dev)
+    main = torch.cuda.current_stream(dev)
+    st = stream if stream is not None else main
+    if st is not main:
+        st.wait_stream(main)   # the points (and a reused buffer's last reader) are ordered before
+    N.check(L.gp2d_ozaki_kstar(_ptr(X), ntr, npad, _ptr(G), m, ctypes.byref(desc), nmod, chunk, _ptr(bres),
+                               bres.numel(), ctypes.c_void_p(st.cuda_stream)), "gp2d_ozaki_kstar")
+    if st is not main:
+        # the caching allocator must not hand these blocks to main-stream work (the fit)
+        # while the side stream still reads / writes them
+        for t in (X, G, bres):
+            t.record_stream(st)
+    ev = torch.cuda.Event()
+    ev.record(st)
+    return KstarPlanes(kernel=kernel, x=X, m=m, n=n, n_pad=npad, chunk=chunk, nmod=nmod, bres=bres, event=ev,
+                       xg=G)
 
 
 _VAR_MODES = {"latent": N.VAR_LATENT, "gpy": N.VAR_NOISY, "noisy": N.VAR_NOISY, "sklearn": N.VAR_CLIPPED,
@@ -253,7 +319,10 @@ class Predictor:
             self.wbytes = int(N.lib().gp2d_predict_workspace(gp.n, self.chunk, bd))
         self.work = torch.empty(self.wbytes // 8 + 1, dtype=torch.float64, device=gp.device)
 
-    def __call__(self, xg, var_mode: str = "latent", compute_var: bool = True, out=None):
+    def __call__(self, xg, var_mode: str = "latent", compute_var: bool = True, out=None,
+                 planes: KstarPlanes | None = None):
+        """planes: K* residue planes of this same grid from kstar_planes() (ozaki engine):
+        the predict then skips K* generation and takes the mean as Vᵀβ."""
         gp = self.gp
         L = N.lib()
         d, bd = gp.kernel.input_dim, gp.kernel.block_dim
@@ -265,6 +334,19 @@ class Predictor:
         else:
             mean, var = out
         desc = gp.kernel.desc()
+        if planes is not None and compute_var and self.ozaki and "ozaki" in gp.extra and gp.beta is not None:
+            if planes.m != m or planes.n != gp.n or planes.chunk != self.chunk:
+                raise ValueError("K* planes were made for another grid, fit layout or chunk size")
+            wres, rowscale, nmod = gp.extra["ozaki"]
+            s = torch.cuda.current_stream(gp.device)
+            s.wait_event(planes.event)
+            rc = L.gp2d_predict_ozaki_planes(_ptr(wres), _ptr(rowscale), nmod, gp.n, _ptr(gp.beta), _ptr(planes.bres),
+                                             planes.nmod, gp.n_train, gp.n_pad, m, ctypes.byref(desc),
+                                             _VAR_MODES[var_mode], float(gp.noise), _ptr(mean), _ptr(var),
+                                             self.chunk, _ptr(self.work), self.wbytes, ctypes.c_void_p(s.cuda_stream))
+            if rc != -3:   # −3: the fit needs more moduli than the planes carry → inline K* below
+                N.check(rc, "gp2d_predict_ozaki_planes")
+                return mean, var
         if self.ozaki and "ozaki" in gp.extra:
             wres, rowscale, nmod = gp.extra["ozaki"]
             N.check(L.gp2d_predict_ozaki(_ptr(wres), _ptr(rowscale), nmod, gp.n, _ptr(gp.alpha), _ptr(gp.x), gp.n_train,

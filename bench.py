@@ -46,6 +46,9 @@ def parse():
     ap.add_argument("--fit-mode", default="bcast", choices=["bcast", "replicate"])
     ap.add_argument("--variance", default="ozaki", choices=["ozaki", "f64"],
                     help="variance contraction: exact INT8 Ozaki-II emulation (default) or FP64 MFMA")
+    ap.add_argument("--kstar-ahead", type=int, default=1,
+                    help="ozaki: generate the K* residue planes on a side stream concurrently with the fit "
+                         "(mean from V^T beta); 0 = inline per chunk after the fit")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-sample-points", type=int, default=2048)
     ap.add_argument("--pmc-json", default=None)
@@ -115,15 +118,21 @@ def main():
     mean = torch.empty(2 * m, dtype=torch.float64, device=dev)
     var = torch.empty(2 * m, dtype=torch.float64, device=dev)
     pred_cache = {}
+    ahead = bool(args.kstar_ahead) and args.variance == "ozaki"
+    side = torch.cuda.Stream(dev) if ahead else None
 
     def step():
+        planes = None
+        if ahead:   # K* planes depend on (X_train, grid, kernel) only: overlap them with the fit
+            planes = E.kstar_planes(spec, xt, xg, noise, chunk=args.chunk, stream=side, out=pred_cache.get("k"))
+            pred_cache["k"] = planes
         gp = GD.fit_sharded(spec, xt, yt, noise, dev, mode=args.fit_mode, variance=args.variance)
         pr = pred_cache.get("p")
         if pr is None or pr.gp.n != gp.n or pr.ozaki != ("ozaki" in gp.extra):
             pr = E.Predictor(gp, args.chunk)
             pred_cache["p"] = pr
         pr.gp = gp
-        pr(xg, out=(mean, var))
+        pr(xg, out=(mean, var), planes=planes)
         return gp
 
     for _ in range(args.warmup):

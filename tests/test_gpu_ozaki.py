@@ -93,3 +93,90 @@ def test_ozaki_too_few_moduli_poisons_instead_of_wrapping():
     v = var.cpu().numpy()
     assert np.isnan(v).mean() > 0.5
     np.testing.assert_array_equal(mu.cpu().numpy(), mu_ok.cpu().numpy())  # the mean path is separate
+
+
+# ---------------------------------------------------------------- K* planes ahead of the fit
+# gp2d_ozaki_kstar builds the K* residue planes before the fit (they need no α); the mean is
+# then Σ_i V_ij β_i from the CRT kernel (β = W·y).  Same 1e-10 gate; the variance partials
+# are the same integers as the inline path, so the variance is bit-identical to it.
+def _ahead(ks, x, y, xg, noise, chunk, side=True):
+    st = torch.cuda.Stream() if side else None
+    planes = E.kstar_planes(ks, x, xg, noise, chunk=chunk, stream=st)
+    gp = E.fit(ks, x, y, noise=noise, variance="ozaki")
+    pr = E.Predictor(gp, chunk)
+    mu, var = pr(xg, planes=planes)
+    return gp, planes, mu.cpu().numpy(), var.cpu().numpy()
+
+
+@pytest.mark.parametrize("ntr,m,kind,l,chunk", [(100, 700, "df", 5.0, 256), (300, 1500, "mixed", 4.0, 1024),
+                                                (1000, 3000, "cf", 3.0, 1024), (37, 1, "df", 5.0, 128),
+                                                (64, 130, "scalar", 6.0, 8192)])
+def test_kstar_ahead_matches_oracle(ntr, m, kind, l, chunk):
+    x, y = tracks(ntr, ntr + 1)
+    rng = np.random.default_rng(m + 3)
+    xg = np.stack([rng.uniform(-5, 65, m), rng.uniform(-5, 50, m)], 1)
+    ratio = 0.5 if kind == "mixed" else 1.0
+    ks = E.KernelSpec(kind=kind, l_df=l, l_cf=l * 1.3, ratio=ratio)
+    gp, planes, mu, var = _ahead(ks, x, y, xg, 0.0025, chunk)
+    mo, vo = O.fit_predict(x, y, xg, kind=kind, l_df=l, l_cf=l * 1.3, ratio=ratio, noise=0.0025)
+    assert rel(mu, mo) < 1e-10
+    assert rel(var, vo) < 1e-10
+    mi, vi = (t.cpu().numpy() for t in E.Predictor(gp, chunk)(xg))
+    assert np.array_equal(var, vi)
+    assert rel(mu, mi) < 1e-11
+
+
+@pytest.mark.parametrize("kind,l,noise,jitter", [("df", 5.0, 0.0025, 0.0), ("cf", 2.0, 1e-4, 0.0),
+                                                  ("mixed", 8.0, 0.5, 1e-6), ("scalar", 1.0, 0.01, 0.0),
+                                                  ("df", 0.7, 1e-6, 0.0)])
+def test_nmod_apriori_bounds_data_driven(kind, l, noise, jitter):
+    x, y = tracks(700, 5)
+    ks = E.KernelSpec(kind=kind, l_df=l, l_cf=l * 1.1, ratio=0.5 if kind == "mixed" else 1.0)
+    gp = E.fit(ks, x, y, noise=noise, jitter=jitter, variance="ozaki")
+    apriori = int(E.N.lib().gp2d_ozaki_nmod_apriori(gp.n, __import__("ctypes").byref(ks.desc()), noise + jitter))
+    assert gp.extra["ozaki"][2] <= apriori <= gp.extra["ozaki"][2] + 1
+
+
+def test_kstar_ahead_too_few_moduli_falls_back_inline():
+    import dataclasses
+    x, y = tracks(300, 11)
+    rng = np.random.default_rng(12)
+    xg = np.stack([rng.uniform(-5, 65, 900), rng.uniform(-5, 50, 900)], 1)
+    ks = E.KernelSpec(kind="df", l_df=5.0)
+    planes = E.kstar_planes(ks, x, xg, 0.0025, chunk=512)
+    gp = E.fit(ks, x, y, noise=0.0025, variance="ozaki")
+    short = dataclasses.replace(planes, nmod=gp.extra["ozaki"][2] - 1)
+    pr = E.Predictor(gp, 512)
+    mu, var = (t.cpu().numpy() for t in pr(xg, planes=short))
+    mi, vi = (t.cpu().numpy() for t in pr(xg))
+    assert np.array_equal(mu, mi) and np.array_equal(var, vi)
+
+
+def test_kstar_ahead_spatiotemporal():
+    rng = np.random.default_rng(21)
+    n, m = 400, 1000
+    x = np.stack([rng.uniform(0, 48, n), rng.uniform(0, 45, n), rng.uniform(0, 60, n)], 1)
+    y = np.concatenate([np.sin(x[:, 1] / 7), np.cos(x[:, 2] / 9)]) + rng.normal(0, 0.05, 2 * n)
+    xg = np.stack([rng.uniform(0, 48, m), rng.uniform(-5, 50, m), rng.uniform(-5, 65, m)], 1)
+    ks = E.KernelSpec(family="vector_st", kind="mixed", l_df=5.0, l_cf=4.0, ratio=0.5, var_t=1.3, l_t=12.0)
+    gp, planes, mu, var = _ahead(ks, x, y, xg, 0.0025, 512)
+    mi, vi = (t.cpu().numpy() for t in E.Predictor(gp, 512)(xg))
+    assert np.array_equal(var, vi)
+    assert rel(mu, mi) < 1e-11
+
+
+def test_kstar_ahead_bench_size_properties():
+    """N_train = 4096 (the bench workload) on a 2-chunk grid: the variance is bit-identical
+    to the inline path and the mean Vᵀβ agrees with K*α to 1e-11 normwise (the gate against the oracle is 1e-10)."""
+    from gp2d import data as D
+    x1, x2, u, v = D.synthetic_tracks(4096, seed=2016)
+    x = np.stack([x1, x2], 1)
+    y = np.concatenate([u, v])
+    _, _, xg = D.bbox_grid(x1, x2, 128, pad=5.0)
+    ks = E.KernelSpec(kind="df", l_df=5.0)
+    gp, planes, mu, var = _ahead(ks, x, y, xg, 0.0025, 8192)
+    assert planes.nmod >= gp.extra["ozaki"][2]
+    mi, vi = (t.cpu().numpy() for t in E.Predictor(gp, 8192)(xg))
+    assert np.array_equal(var, vi)
+    assert rel(mu, mi) < 1e-11
+    assert np.all(np.isfinite(var)) and np.all(var > 0)

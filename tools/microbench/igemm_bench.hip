@@ -6,8 +6,12 @@
 #include <random>
 #include <vector>
 #include <climits>
+#include <cstdlib>
 namespace gp2d { void set_error(const std::string&) {} }
 using namespace gp2d;
+#ifndef IGEMM_KERNEL
+#define IGEMM_KERNEL igemm_nt_mod_kernel
+#endif
 int main() {
   const int n = 8192, nc = 16384, mod = 251;
   std::mt19937 rng(17);
@@ -15,6 +19,7 @@ int main() {
   for (int i = 0; i < n; ++i)
     for (int k = 0; k < n; ++k) A[(size_t)i * n + k] = (k <= i) ? (int8_t)(rng() & 0xff) : 0;
   for (auto& v : B) v = (int8_t)(rng() & 0xff);
+  if (getenv("IGEMM_ZERO")) { for (auto& v : A) v = 0; for (auto& v : B) v = 0; }
   for (int i = 0; i < n; ++i)
     for (int k = 0; k < n; ++k) Ab[slab_offset(i, k, n)] = A[(size_t)i * n + k];
   for (int j = 0; j < nc; ++j)
@@ -25,7 +30,7 @@ int main() {
   (void)hipMemcpy(dB, Bb.data(), B.size(), hipMemcpyHostToDevice);
   hipEvent_t e0, e1; (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
   const dim3 g(nc / IBN, n / IBM);
-  auto launch = [&]() { igemm_nt_mod_kernel<<<g, 512>>>(dA, dB, dC, n, n, nc, n, 1, mod, 1.0 / mod, 1 << 30, 0); };
+  auto launch = [&]() { IGEMM_KERNEL<<<g, 512>>>(dA, dB, dC, n, n, nc, n, 1, mod, 1.0 / mod, 1 << 30, 0); };
   for (int w = 0; w < 3; ++w) launch();
   (void)hipDeviceSynchronize();
   (void)hipEventRecord(e0);
