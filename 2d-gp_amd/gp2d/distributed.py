@@ -35,20 +35,44 @@ def broadcast_fit(gp: E.GPFit | None, spec: E.KernelSpec, noise: float, x, devic
     dist.broadcast(meta, src)
     n, ntr, npad, has_beta = (int(v) for v in meta.tolist())
     nab = 2 * n if has_beta else n
+    blocks = packed_blocks(n)
+    packed = torch.empty(blocks[-1][2], dtype=torch.float64, device=device)
     if rank != src:
-        W = torch.empty((n, n), dtype=torch.float64, device=device)
+        W = torch.zeros((n, n), dtype=torch.float64, device=device)
         ab = torch.empty(nab, dtype=torch.float64, device=device)
         X = torch.empty((ntr, spec.input_dim), dtype=torch.float64, device=device)
     else:
         W, X = gp.W, gp.x
         ab = torch.cat([gp.alpha, gp.beta]) if has_beta else gp.alpha
-    dist.broadcast(W, src)
+        for r0, c1, off in blocks[:-1]:
+            packed[off:off + PACK_ROWS * c1].view(PACK_ROWS, c1).copy_(W[r0:r0 + PACK_ROWS, :c1])
+    # W = L⁻¹ is lower-triangular: only the row blocks' [0, end of their diagonal block)
+    # columns travel (≈ half of n² doubles)
+    dist.broadcast(packed, src)
     dist.broadcast(ab, src)   # α and β = W·y (the mean from precomputed K* planes)
     dist.broadcast(X, src)
     if rank == src:
         return gp
+    for r0, c1, off in blocks[:-1]:
+        W[r0:r0 + PACK_ROWS, :c1].copy_(packed[off:off + PACK_ROWS * c1].view(PACK_ROWS, c1))
     return E.GPFit(kernel=spec, noise=float(noise), x=X, n_train=ntr, n_pad=npad, W=W, alpha=ab[:n],
                    device=torch.device(device), beta=ab[n:] if has_beta else None)
+
+
+PACK_ROWS = 128   # the matrix order is a multiple of 128 (engine.fit_layout)
+
+
+def packed_blocks(n: int):
+    """Row-block packing of a lower-triangular n×n matrix: [(first row, columns kept,
+    offset)] per 128-row block (columns up to the end of its diagonal block), then a final
+    (n, 0, total length) sentinel."""
+    out, off = [], 0
+    for r0 in range(0, n, PACK_ROWS):
+        c1 = min(n, r0 + PACK_ROWS)
+        out.append((r0, c1, off))
+        off += PACK_ROWS * c1
+    out.append((n, 0, off))
+    return out
 
 
 def fit_sharded(spec: E.KernelSpec, x, y, noise: float, device, mode: str = "bcast", jitter: float = 0.0,

@@ -43,12 +43,15 @@ def parse():
     ap.add_argument("--grid", type=int, default=256)
     ap.add_argument("--kind", default="df")
     ap.add_argument("--chunk", type=int, default=8192)
-    ap.add_argument("--fit-mode", default="bcast", choices=["bcast", "replicate"])
+    ap.add_argument("--fit-mode", default="auto", choices=["auto", "bcast", "replicate"],
+                    help="N>1: rank 0 fits and W goes out by RCCL broadcast (bcast), every rank fits "
+                         "(replicate), or whichever of the two the warmup measured faster (auto)")
     ap.add_argument("--variance", default="ozaki", choices=["ozaki", "f64"],
                     help="variance contraction: exact INT8 Ozaki-II emulation (default) or FP64 MFMA")
-    ap.add_argument("--kstar-ahead", type=int, default=1,
+    ap.add_argument("--kstar-ahead", type=int, default=-1,
                     help="ozaki: generate the K* residue planes on a side stream concurrently with the fit "
-                         "(mean from V^T beta); 0 = inline per chunk after the fit")
+                         "(mean from V^T beta); 0 = inline per chunk after the fit; -1 (auto) = only while "
+                         "non-root ranks wait for the factor broadcast (N>1, bcast)")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-sample-points", type=int, default=2048)
     ap.add_argument("--pmc-json", default=None)
@@ -58,9 +61,13 @@ def parse():
 def setup_dist(args):
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     if ws > 1:
-        local = int(os.environ.get("LOCAL_RANK", "0"))
+        # one process per GPU; GP2D_DIST_BACKEND=gloo (and ranks sharing a device) only for
+        # rehearsing the multi-rank path on a one-GPU box
+        local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("GP2D_DIST_BACKEND", "nccl")
+        kw = {"device_id": torch.device("cuda", local)} if backend == "nccl" else {}
+        dist.init_process_group(backend, **kw)
         return ws, dist.get_rank(), torch.device("cuda", local)
     return 1, 0, torch.device("cuda", 0)
 
@@ -118,15 +125,20 @@ def main():
     mean = torch.empty(2 * m, dtype=torch.float64, device=dev)
     var = torch.empty(2 * m, dtype=torch.float64, device=dev)
     pred_cache = {}
-    ahead = bool(args.kstar_ahead) and args.variance == "ozaki"
-    side = torch.cuda.Stream(dev) if ahead else None
+    side = torch.cuda.Stream(dev) if args.variance == "ozaki" else None
+    cfg = {"mode": args.fit_mode if ws > 1 else "local", "ahead": False}
+
+    def set_mode(mode):
+        cfg["mode"] = mode
+        a = args.kstar_ahead
+        cfg["ahead"] = args.variance == "ozaki" and (a == 1 or (a == -1 and ws > 1 and mode == "bcast"))
 
     def step():
         planes = None
-        if ahead:   # K* planes depend on (X_train, grid, kernel) only: overlap them with the fit
+        if cfg["ahead"]:   # K* planes depend on (X_train, grid, kernel) only: overlap them with the fit
             planes = E.kstar_planes(spec, xt, xg, noise, chunk=args.chunk, stream=side, out=pred_cache.get("k"))
             pred_cache["k"] = planes
-        gp = GD.fit_sharded(spec, xt, yt, noise, dev, mode=args.fit_mode, variance=args.variance)
+        gp = GD.fit_sharded(spec, xt, yt, noise, dev, mode=cfg["mode"], variance=args.variance)
         pr = pred_cache.get("p")
         if pr is None or pr.gp.n != gp.n or pr.ozaki != ("ozaki" in gp.extra):
             pr = E.Predictor(gp, args.chunk)
@@ -135,6 +147,22 @@ def main():
         pr(xg, out=(mean, var), planes=planes)
         return gp
 
+    probe = {}
+    if ws > 1 and args.fit_mode == "auto":
+        # measure one step in each mode (after a warm step of each), max over ranks, keep the faster
+        for mode in ("bcast", "replicate"):
+            set_mode(mode)
+            step()
+            barrier(ws)
+            t = time.perf_counter()
+            step()
+            barrier(ws)
+            dt_ = torch.tensor([time.perf_counter() - t], dtype=torch.float64, device=dev)
+            dist.all_reduce(dt_, op=dist.ReduceOp.MAX)
+            probe[mode] = 1e3 * float(dt_.item())
+        set_mode(min(probe, key=probe.get))
+    else:
+        set_mode(cfg["mode"])
     for _ in range(args.warmup):
         step()
     barrier(ws)
@@ -159,7 +187,7 @@ def main():
     barrier(ws)
     t2 = time.perf_counter()
     for _ in range(args.steps):
-        gp = GD.fit_sharded(spec, xt, yt, noise, dev, mode=args.fit_mode, variance=args.variance)
+        gp = GD.fit_sharded(spec, xt, yt, noise, dev, mode=cfg["mode"], variance=args.variance)
         pred_cache["p"].gp = gp
         pred_cache["p"](xg, compute_var=False, out=(mean, var))
     barrier(ws)
@@ -214,7 +242,9 @@ def main():
         "config": {"workload": f"{args.kind} kernel, N_train={args.ntrain}, {G}x{G} grid per GPU, fit+predict "
                                f"(mean+variance)", "n_train": args.ntrain, "grid_per_gpu": f"{G}x{G}",
                    "points_total": m_all, "length_scale_km": 5.0, "noise": noise,
-                   "parallelism": f"grid-sharded x{ws}, factor {args.fit_mode}" + (" (RCCL)" if ws > 1 else "")},
+                   "parallelism": f"grid-sharded x{ws}, factor {cfg['mode']}" +
+                                  (" (RCCL broadcast of packed W)" if ws > 1 and cfg["mode"] == "bcast" else ""),
+                   "fit_mode_probe_ms_per_step": probe or None, "kstar_ahead": cfg["ahead"]},
         "roofline": roof,
         "mean_only_value": mean_only,
     }

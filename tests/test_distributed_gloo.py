@@ -90,3 +90,15 @@ def test_assemble_from_shards_numpy():
         assert vec.size == bd * k
         shards.append((lo, hi, vec))
     assert np.array_equal(GD.assemble_from_shards(m, bd, shards), full)
+
+
+def test_packed_blocks_cover_the_lower_triangle():
+    from gp2d import distributed as GD
+    for n in (128, 256, 1024):
+        blocks = GD.packed_blocks(n)
+        cover = np.zeros((n, n), int)
+        for r0, c1, off in blocks[:-1]:
+            cover[r0:r0 + GD.PACK_ROWS, :c1] += 1
+        assert np.all(cover[np.tril_indices(n)] == 1)       # every lower entry once
+        assert blocks[-1][2] == sum(GD.PACK_ROWS * c1 for _, c1, _ in blocks[:-1])
+        assert blocks[-1][2] <= n * n // 2 + n * GD.PACK_ROWS
