@@ -169,20 +169,33 @@ __global__ __launch_bounds__(256, 2) void gemm_f64_kernel(GemmParams p) {
   if (EPI == EPI_STORE) {
     double* __restrict__ C = p.C + z * p.sC;
     const bool diag_tile = p.c_lower && (bi == bj);
+    const bool has_beta = p.beta != 0.0;
+    // per 16-row group: all 16 C loads in flight together, then the updates and stores
+    // (element-wise load → use → store chains leave one HBM round trip per element)
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi)
+    for (int mi = 0; mi < 4; ++mi) {
+      double old[4][4];
+      if (has_beta) {
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = i0 + wr * 64 + mi * 16 + lk + 4 * r;
+            const int col = j0 + wc * 64 + ni * 16 + lr;
+            old[ni][r] = __builtin_nontemporal_load(C + (int64_t)row * p.ldc + col);
+          }
+      }
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int row = i0 + wr * 64 + mi * 16 + lk + 4 * r;
           const int col = j0 + wc * 64 + ni * 16 + lr;
-          if (diag_tile && col > row) continue;
-          double* cp = C + (int64_t)row * p.ldc + col;
           double v = p.alpha * acc[mi][ni][r];
-          if (p.beta != 0.0) v += p.beta * (*cp);
-          *cp = v;
+          if (has_beta) v = fma(p.beta, old[ni][r], v);
+          if (!(diag_tile && col > row)) C[(int64_t)row * p.ldc + col] = v;
         }
+    }
   } else {
     // column sums of squares of this 128-row slab of V, combined in a fixed order:
     // registers (rows (l>>4)+4r+16mi) -> lanes l, l^16, l^32, l^48 -> the two wave rows.

@@ -474,7 +474,7 @@ int gp2d_predict(const double* W, int64_t n, int64_t ldw, const double* alpha, c
         g_timing.flops.push_back((double)bd * (double)cv * nv * nv);  // 2·(2N)² per point (vector2d)
       }
     }
-    predict_finalize_kernel<<<(unsigned)((ncols + 255) / 256), 256, 0, s>>>(
+    predict_finalize_kernel<<<(unsigned)((ncols + 63) / 64), 64, 0, s>>>(
         pm, nmseg, P, npseg, ncols, cp, cv, c0, m, kss, add, clip, compute_var, mean, var);
     GP2D_CHECK(check_launch("predict_finalize_kernel"));
   }
@@ -608,7 +608,7 @@ static int predict_ozaki_impl(const int8_t* wres, const double* rowscale, int nm
       }
       GP2D_CHECK(check_launch("ozaki_crt_colsq_kernel"));
     }
-    predict_finalize_kernel<<<(unsigned)((ncols + 255) / 256), 256, 0, s>>>(
+    predict_finalize_kernel<<<(unsigned)((ncols + 63) / 64), 64, 0, s>>>(
         pm, pre ? npseg : nmseg, P, npseg, ncols, cp, cv, c0, m, kss, add, clip, compute_var, mean, var);
     GP2D_CHECK(check_launch("predict_finalize_kernel"));
   }

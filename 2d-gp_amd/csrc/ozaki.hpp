@@ -124,20 +124,23 @@ __global__ __launch_bounds__(256) void ozaki_w_res_kernel(const double* __restri
 }
 
 // ------------------------------------------------------------------ K*ᵀ residues + mean
-// Block: 64 lanes × 4 thread rows.  Lane tx covers training points t = 256·bx + 4tx..+3,
-// thread row ty covers grid points p = 16·by + ty + 4q (q < 4).  Writes the residue planes
-// Bres[l] (rows j = grid components, columns k = training components, slab-blocked)
-// and mean partials pm[bx][j] = Σ_{k in block} α_k·K*_jk (one wave = one grid point set,
-// reduced by shuffles in a fixed order).
-constexpr int OZ_KS_T = 256;   // training points per block
-constexpr int OZ_KS_P = 16;    // grid points per block
+// Block: 64 training points × 64 grid points (4 waves).  Lane l covers training points
+// t = 64·bx + 4·(l&15) .. +3 and, in iteration q < 4, grid point p = 64·by + 16q + 4·wave + (l>>4).
+// One wave-wide store per (modulus, entry) then writes 4 consecutive rows × 64 B of one slab
+// tile — 256 contiguous bytes (the slab-blocked layout puts rows of a 256-row tile 64 B
+// apart).  Writes the residue planes Bres[l] (rows j = grid components, columns k =
+// training components, slab-blocked) and mean partials pm[bx][j] = Σ_{k in block} α_k·K*_jk
+// (16-lane shuffle reduction in a fixed order).  alpha == nullptr: planes only.
+constexpr int OZ_KS_T = 64;   // training points per block
+constexpr int OZ_KS_P = 64;   // grid points per block
 
 __global__ __launch_bounds__(256) void ozaki_kstar_kernel(
     const double* __restrict__ xtr, int64_t ntr, int64_t npad, const double* __restrict__ xg, int64_t cv,
     int64_t cp, VecParams vp, const double* __restrict__ alpha, OzakiConsts oc, int8_t* __restrict__ bres,
     double* __restrict__ pm) {
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const int64_t t0 = (int64_t)blockIdx.x * OZ_KS_T + 4 * tx;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int kg = lane & 15, r = lane >> 4;
+  const int64_t t0 = (int64_t)blockIdx.x * OZ_KS_T + 4 * kg;
   const int64_t n = 2 * npad, ncols = 2 * cp;
   double a1[4], a2[4], x0[4], x1[4], x2[4];
   bool tv[4];
@@ -152,8 +155,8 @@ __global__ __launch_bounds__(256) void ozaki_kstar_kernel(
   }
   const double scale = ldexp(1.0, oc.sB);
 #pragma unroll 1
-  for (int q = 0; q < OZ_KS_P / 4; ++q) {
-    const int64_t p = (int64_t)blockIdx.y * OZ_KS_P + ty + 4 * q;
+  for (int q = 0; q < OZ_KS_P / 16; ++q) {
+    const int64_t p = (int64_t)blockIdx.y * OZ_KS_P + 16 * q + 4 * wv + r;
     const bool pv = p < cv;
     double g0 = 0.0, g1 = 0.0, g2 = 0.0;
     if (pv) vec_point(vp, xg, p, g0, g1, g2);
@@ -169,17 +172,19 @@ __global__ __launch_bounds__(256) void ozaki_kstar_kernel(
       mu += a1[u] * k11[u] + a2[u] * k12[u];   // row j = p      (u component of the grid point)
       mv += a1[u] * k12[u] + a2[u] * k22[u];   // row j = cp + p (v component)
     }
-    // fixed-order wave reduction of the mean partials (64 lanes = this block's 256 points)
+    if (pm != nullptr) {
+      // fixed-order reduction over the 16 lanes of this grid point (this block's 64 points)
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      mu += __shfl_xor(mu, o);
-      mv += __shfl_xor(mv, o);
+      for (int o = 8; o > 0; o >>= 1) {
+        mu += __shfl_xor(mu, o);
+        mv += __shfl_xor(mv, o);
+      }
+      if (kg == 0 && p < cp) {
+        pm[(int64_t)blockIdx.x * ncols + p] = mu;
+        pm[(int64_t)blockIdx.x * ncols + cp + p] = mv;
+      }
     }
-    if (pm != nullptr && tx == 0 && p < cp) {
-      pm[(int64_t)blockIdx.x * ncols + p] = mu;
-      pm[(int64_t)blockIdx.x * ncols + cp + p] = mv;
-    }
-    if (p >= cp) continue;
+    if (p >= cp || t0 >= npad) continue;   // npad is a multiple of 64: whole 4-point groups
     // The (v,u) block equals the (u,v) block (k12 is symmetric in the 2×2 kernel block), so
     // only (u,u), (u,v) and (v,v) are stored: the GEMM reads (v,u) tiles from (u,v).
     double xi[3][4];  // [entry: (u,u) (u,v) (v,v)][u]
@@ -189,6 +194,10 @@ __global__ __launch_bounds__(256) void ozaki_kstar_kernel(
       xi[1][u] = rint(k12[u] * scale);
       xi[2][u] = rint(k22[u] * scale);
     }
+    // (grid comp, train comp): (u,u) → row p, col t ; (u,v) → row p, col npad+t ;
+    //                          (v,v) → row cp+p, col npad+t ; (v,u) not stored
+    const int64_t o_uu = slab_offset(p, t0, n), o_uv = slab_offset(p, npad + t0, n),
+                  o_vv = slab_offset(cp + p, npad + t0, n);
     for (int l = 0; l < oc.nmod; ++l) {
       const double m = (double)oc.m[l], im = oc.inv_m[l];
       uint32_t pk[3];
@@ -199,14 +208,10 @@ __global__ __launch_bounds__(256) void ozaki_kstar_kernel(
         for (int u = 0; u < 4; ++u) w |= (uint32_t)(uint8_t)(int8_t)centred_residue(xi[e][u], m, im) << (8 * u);
         pk[e] = w;
       }
-      if (t0 >= npad) continue;  // npad is a multiple of 64, so a 4-point group is all in or all out
       int8_t* plane = bres + (int64_t)l * ncols * n;
-      // (grid comp, train comp): (u,u) → row p, col t ; (u,v) → row p, col npad+t ;
-      //                          (v,v) → row cp+p, col npad+t ; (v,u) not stored
-      // (slab-blocked plane: 4 consecutive columns stay inside one 64-B row segment)
-      *reinterpret_cast<uint32_t*>(plane + slab_offset(p, t0, n)) = pk[0];
-      *reinterpret_cast<uint32_t*>(plane + slab_offset(p, npad + t0, n)) = pk[1];
-      *reinterpret_cast<uint32_t*>(plane + slab_offset(cp + p, npad + t0, n)) = pk[2];
+      *reinterpret_cast<uint32_t*>(plane + o_uu) = pk[0];
+      *reinterpret_cast<uint32_t*>(plane + o_uv) = pk[1];
+      *reinterpret_cast<uint32_t*>(plane + o_vv) = pk[2];
     }
   }
 }

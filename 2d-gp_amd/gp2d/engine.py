@@ -208,11 +208,8 @@ def fit(kernel: KernelSpec, x, y, noise: float, jitter: float = 0.0, device=None
     dinv = torch.empty((n // NB, NB, NB), dtype=torch.float64, device=dev)
     info = torch.zeros(1, dtype=torch.int32, device=dev)
     N.check(L.gp2d_potrf(_ptr(A), n, n, _ptr(dinv), _ptr(info), None, 0, s), "gp2d_potrf")
-    inf = int(info.item())
-    if inf != 0:
-        raise np.linalg.LinAlgError(
-            f"K_y is not positive definite (leading minor of order {inf}); "
-            "increase the noise / jitter (cf. sklearn _gpr.py:350-358)")
+    # TRTRI and α are enqueued behind POTRF before `info` is read (one host sync per fit,
+    # no bubble between the factor and the inverse); a failed factor raises below
     wbytes = int(L.gp2d_trtri_workspace(n))
     work = torch.empty(wbytes // 8 + 1, dtype=torch.float64, device=dev)
     N.check(L.gp2d_trtri(_ptr(A), n, n, _ptr(dinv), _ptr(work), wbytes, s), "gp2d_trtri")
@@ -222,6 +219,11 @@ def fit(kernel: KernelSpec, x, y, noise: float, jitter: float = 0.0, device=None
     pbytes = int(L.gp2d_potrs_workspace(n))
     pwork = torch.empty(pbytes // 8 + 1, dtype=torch.float64, device=dev)
     N.check(L.gp2d_potrs_inv(_ptr(A), n, n, _ptr(Y), _ptr(alpha), _ptr(pwork), pbytes, s), "gp2d_potrs_inv")
+    inf = int(info.item())
+    if inf != 0:
+        raise np.linalg.LinAlgError(
+            f"K_y is not positive definite (leading minor of order {inf}); "
+            "increase the noise / jitter (cf. sklearn _gpr.py:350-358)")
     gp = GPFit(kernel=kernel, noise=float(noise), x=X, n_train=ntr, n_pad=npad, W=A, alpha=alpha, device=dev,
                y=Y, beta=pwork[:n])   # gp2d_potrs_inv leaves β = W·y at the head of its workspace
     if variance == "ozaki":
