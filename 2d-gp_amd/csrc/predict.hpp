@@ -27,7 +27,7 @@ __global__ __launch_bounds__(256) void predict_finalize_kernel(
     const double* __restrict__ pm, int64_t nmseg, const double* __restrict__ P, int64_t npseg,
     int64_t ncols, int64_t cpad, int64_t cvalid, int64_t c0, int64_t m, double kss, double add,
     int clip, int compute_var, double* __restrict__ mean, double* __restrict__ var) {
-  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= ncols) return;
   const int64_t comp = c / cpad, loc = c - comp * cpad;
   if (loc >= cvalid) return;

@@ -219,15 +219,23 @@ def fit(kernel: KernelSpec, x, y, noise: float, jitter: float = 0.0, device=None
     pbytes = int(L.gp2d_potrs_workspace(n))
     pwork = torch.empty(pbytes // 8 + 1, dtype=torch.float64, device=dev)
     N.check(L.gp2d_potrs_inv(_ptr(A), n, n, _ptr(Y), _ptr(alpha), _ptr(pwork), pbytes, s), "gp2d_potrs_inv")
+    gp = GPFit(kernel=kernel, noise=float(noise), x=X, n_train=ntr, n_pad=npad, W=A, alpha=alpha, device=dev,
+               y=Y, beta=pwork[:n])   # gp2d_potrs_inv leaves β = W·y at the head of its workspace
+    err = None
+    if variance == "ozaki":
+        # enqueued before `info` is read: prepare's own synchronisation (the moduli count)
+        # then covers the whole fit, one host round trip instead of two
+        try:
+            ozaki_prepare(gp)
+        except N.GP2DError as e:   # a failed factor (NaN rows) makes prepare fail too: info decides
+            err = e
     inf = int(info.item())
     if inf != 0:
         raise np.linalg.LinAlgError(
             f"K_y is not positive definite (leading minor of order {inf}); "
             "increase the noise / jitter (cf. sklearn _gpr.py:350-358)")
-    gp = GPFit(kernel=kernel, noise=float(noise), x=X, n_train=ntr, n_pad=npad, W=A, alpha=alpha, device=dev,
-               y=Y, beta=pwork[:n])   # gp2d_potrs_inv leaves β = W·y at the head of its workspace
-    if variance == "ozaki":
-        ozaki_prepare(gp)
+    if err is not None:
+        raise err
     return gp
 
 

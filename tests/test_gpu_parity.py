@@ -120,11 +120,13 @@ def test_potrf_trtri_potrs_abi(n):
     assert rel(A2.cpu().numpy(), np.linalg.inv(Lref)) < 1e-12
 
 
-def test_not_positive_definite_raises():
-    """Non-SPD K_y → LAPACK-style info → numpy.linalg.LinAlgError (np.linalg.inv / sklearn paths)."""
+@pytest.mark.parametrize("variance", ["f64", "ozaki"])
+def test_not_positive_definite_raises(variance):
+    """Non-SPD K_y → LAPACK-style info → numpy.linalg.LinAlgError (np.linalg.inv / sklearn paths),
+    also when the Ozaki preparation runs on the failed factor before `info` is read."""
     x = np.zeros((3, 2))  # three identical points, no noise: singular K
     with pytest.raises(np.linalg.LinAlgError):
-        E.fit(E.KernelSpec(kind="df", l_df=1.0), x, np.zeros(6), noise=-1e-3)
+        E.fit(E.KernelSpec(kind="df", l_df=1.0), x, np.zeros(6), noise=-1e-3, variance=variance)
 
 
 def test_sharded_predict_bit_identical():
