@@ -276,12 +276,14 @@ int launch_panel(double* A, int64_t lda, int k, int64_t n, const double* dinv, h
 }
 }  // namespace
 
-// Right-looking blocked Cholesky with one step of look-ahead on two internal streams:
-//   crit: update of block column k+1 → its diagonal factorisation → its panel TRSM,
-//   bulk: the rest of step k's trailing SYRK (columns ≥ k+2),
+// Right-looking blocked Cholesky (NB = 128) with look-ahead on two internal streams and the
+// trailing update delayed over pairs of panels:
+//   crit: for pair (k, k+1): block column k+1 ← panel k, factor k+1; block column k+2 ←
+//         panels k and k+1, factor k+2 (diagonal block + panel TRSM each),
+//   bulk: SYRK of columns ≥ k+3 with both panels (K = 256),
 // so the single-workgroup diagonal kernel hides under the chip-wide SYRK.  Data regions are
-// disjoint (column block k+1 vs ≥ k+2); per step, bulk waits for panel k and crit waits for
-// SYRK k before it updates block column k+2.  The caller's stream is joined at both ends.
+// disjoint (block columns k+1, k+2 vs ≥ k+3); bulk waits for panel k+1, crit waits for the
+// pair's SYRK before it updates block column k+3.  The caller's stream is joined at both ends.
 #define GP2D_EV(call) do { if ((call) != hipSuccess) { set_error(#call " failed"); return -1; } } while (0)
 int gp2d_potrf(double* A, int64_t n, int64_t lda, double* dinv, int* info_dev, void*, size_t, void* stream) {
   GP2D_REQUIRE(n % NB == 0 && n > 0, "potrf: n must be a positive multiple of 128");
@@ -296,37 +298,55 @@ int gp2d_potrf(double* A, int64_t n, int64_t lda, double* dinv, int* info_dev, v
   GP2D_EV(hipEventRecord(e_join, s));
   GP2D_EV(hipStreamWaitEvent(sc, e_join, 0));
   GP2D_EV(hipStreamWaitEvent(sb, e_join, 0));
-  potrf_diag_kernel<<<1, 256, 0, sc>>>(A, lda, 0, dinv, info_dev);
-  GP2D_CHECK(check_launch("potrf_diag_kernel"));
-  GP2D_CHECK(launch_panel(A, lda, 0, n, dinv, sc));
-  GP2D_EV(hipEventRecord(e_pan, sc));
-  for (int k = 0; k + 1 < nb; ++k) {
-    const int k0 = k * NB, k1 = k0 + NB;
-    const double* Lk = A + (int64_t)k1 * lda + k0;     // panel k, rows ≥ k+1
-    // bulk: trailing update of columns ≥ k+2 (lower tiles) once panel k is done
-    GP2D_EV(hipStreamWaitEvent(sb, e_pan, 0));
-    const int rest = (int)(n - k1 - NB);
-    if (rest > 0) {
-      GemmParams q = gemm_params();
-      q.A = Lk + (int64_t)NB * lda; q.lda = lda;
-      q.B = q.A; q.ldb = lda;
-      q.C = A + (int64_t)(k1 + NB) * lda + (k1 + NB); q.ldc = lda;
-      q.M = rest; q.N = rest; q.K = NB;
-      q.alpha = -1.0; q.beta = 1.0; q.c_lower = 1;
-      GP2D_CHECK((launch_gemm<true, EPI_STORE>(q, 1, sb)));
-    }
-    GP2D_EV(hipEventRecord(e_syrk, sb));
-    // crit: A[k+1.., k+1] −= L[k+1.., k] · L[k+1, k]ᵀ (B = the first NB rows of the panel),
-    // then factor diagonal block k+1 and its panel
-    gemm_f64_panel_kernel<<<(unsigned)((n - k1) / PNL_R), 256, 0, sc>>>(Lk, lda, Lk, lda, A + (int64_t)k1 * lda + k1,
-                                                                        lda, -1.0, 1.0);
-    GP2D_CHECK(check_launch("gemm_f64_panel_kernel"));
-    potrf_diag_kernel<<<1, 256, 0, sc>>>(A, lda, k1, dinv, info_dev);
+  // A[j.., j] −= L[j.., p] · L[j, p]ᵀ: block column j receives panel p (skinny K = 128 GEMM,
+  // B = the NB rows of block j of the panel)
+  auto colupdate = [&](int j, int p) -> int {
+    const int64_t j0 = (int64_t)j * NB;
+    const double* Lp = A + j0 * lda + (int64_t)p * NB;
+    gemm_f64_panel_kernel<<<(unsigned)((n - j0) / PNL_R), 256, 0, sc>>>(Lp, lda, Lp, lda, A + j0 * lda + j0, lda,
+                                                                         -1.0, 1.0);
+    return check_launch("gemm_f64_panel_kernel");
+  };
+  // diagonal block j (Cholesky + inverse) and its panel TRSM
+  auto factor = [&](int j) -> int {
+    potrf_diag_kernel<<<1, 256, 0, sc>>>(A, lda, j * NB, dinv, info_dev);
     GP2D_CHECK(check_launch("potrf_diag_kernel"));
-    GP2D_CHECK(launch_panel(A, lda, k + 1, n, dinv, sc));
-    GP2D_EV(hipEventRecord(e_pan, sc));
-    // block column k+2 must have received SYRK k before crit updates it
-    GP2D_EV(hipStreamWaitEvent(sc, e_syrk, 0));
+    return launch_panel(A, lda, j, n, dinv, sc);
+  };
+  GP2D_CHECK(factor(0));
+  // Delayed trailing updates: panels are consumed in pairs, so the bulk SYRK runs with K = 256
+  // (half the launches and half the C read/write traffic per flop of K = 128 updates).  Per
+  // pair (k, k+1), block column k+2 gets both panels through two skinny updates on crit and
+  // columns ≥ k+3 get them through one SYRK on bulk.
+  int k = 0;
+  while (k + 1 < nb) {
+    if (k + 2 < nb) {
+      GP2D_CHECK(colupdate(k + 1, k));   // columns ≤ k+1 of earlier panels arrived by earlier SYRKs
+      GP2D_CHECK(factor(k + 1));
+      GP2D_EV(hipEventRecord(e_pan, sc));   // panels k, k+1 done
+      GP2D_EV(hipStreamWaitEvent(sb, e_pan, 0));
+      const int64_t f0 = (int64_t)(k + 3) * NB;
+      if (f0 < n) {
+        GemmParams q = gemm_params();
+        q.A = A + f0 * lda + (int64_t)k * NB; q.lda = lda;   // rows ≥ k+3 of panels k, k+1
+        q.B = q.A; q.ldb = lda;
+        q.C = A + f0 * lda + f0; q.ldc = lda;
+        q.M = (int)(n - f0); q.N = q.M; q.K = 2 * NB;
+        q.alpha = -1.0; q.beta = 1.0; q.c_lower = 1;
+        GP2D_CHECK((launch_gemm<true, EPI_STORE>(q, 1, sb)));
+      }
+      GP2D_EV(hipEventRecord(e_syrk, sb));
+      GP2D_CHECK(colupdate(k + 2, k));
+      GP2D_CHECK(colupdate(k + 2, k + 1));
+      GP2D_CHECK(factor(k + 2));
+      // block column k+3 must have received this pair's SYRK before crit updates it
+      GP2D_EV(hipStreamWaitEvent(sc, e_syrk, 0));
+      k += 2;
+    } else {   // last block column: only panel k is outstanding
+      GP2D_CHECK(colupdate(k + 1, k));
+      GP2D_CHECK(factor(k + 1));
+      k += 1;
+    }
   }
   GP2D_EV(hipEventRecord(e_join, sb));
   GP2D_EV(hipStreamWaitEvent(sc, e_join, 0));
