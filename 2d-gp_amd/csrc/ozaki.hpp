@@ -676,15 +676,24 @@ __global__ __launch_bounds__(256) void ozaki_crt_colsq_kernel(const uint8_t* __r
       double H[16], T[16];
 #pragma unroll
       for (int c = 0; c < 16; ++c) { H[c] = 0.0; T[c] = 0.0; }
-      for (int l = 0; l < oc.nmod; ++l) {
-        const uint4 v = *reinterpret_cast<const uint4*>(cres + l * plane + j * n + i0);
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-        const double h = oc.h[l], t = oc.t[l];
+      // planes in groups of 4 with the group's loads issued together; a group's planes past
+      // nmod re-read plane nmod−1 (cached) and add nothing (h = t = 0 beyond nmod)
+      const int nm1 = oc.nmod - 1;
+      for (int l0 = 0; l0 < oc.nmod; l0 += 4) {
+        uint4 v[4];
 #pragma unroll
-        for (int c = 0; c < 16; ++c) {
-          const double cl = (double)((w[c >> 2] >> (8 * (c & 3))) & 0xffu);
-          H[c] = fma(cl, h, H[c]);   // exact: multiples of 2^-33 below 2^12
-          T[c] = fma(cl, t, T[c]);
+        for (int u = 0; u < 4; ++u)
+          v[u] = *reinterpret_cast<const uint4*>(cres + (int64_t)min(l0 + u, nm1) * plane + j * n + i0);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+          const double h = oc.h[l0 + u], t = oc.t[l0 + u];
+#pragma unroll
+          for (int c = 0; c < 16; ++c) {
+            const double cl = (double)((w[c >> 2] >> (8 * (c & 3))) & 0xffu);
+            H[c] = fma(cl, h, H[c]);   // exact: multiples of 2^-33 below 2^12
+            T[c] = fma(cl, t, T[c]);
+          }
         }
       }
 #pragma unroll

@@ -12,7 +12,10 @@ using namespace gp2d;
 #endif
 int main() {
   for (int m : {8064, 4096, 1024, 32640}) {
-    const int K = 128, ld = m + 128;
+#ifndef SYRK_K
+#define SYRK_K 128
+#endif
+    const int K = SYRK_K, ld = m + SYRK_K;
     std::mt19937_64 rng(5);
     std::uniform_real_distribution<double> U(-1, 1);
     std::vector<double> A((size_t)m * ld), C((size_t)m * ld);
