@@ -105,8 +105,10 @@ __global__ __launch_bounds__(256) void ozaki_w_res_kernel(const double* __restri
   const int si = (int)rowscale[i];
   __syncthreads();
   if (tid == 0) rowscale[i] = ldexp(oc.M, -si - oc.sB);
-  // 4 consecutive k per thread → one packed dword store per plane
-  for (int64_t k0 = (int64_t)tid * 4; k0 < n; k0 += 1024) {
+  // 4 consecutive k per thread → one packed dword store per plane.  Only k < the end of the
+  // row's 256-row block is written: the GEMM (a_lower) never reads past its diagonal tile.
+  const int64_t kend = std::min<int64_t>(n, (i / 256 + 1) * 256);
+  for (int64_t k0 = (int64_t)tid * 4; k0 < kend; k0 += 1024) {
     double x[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
