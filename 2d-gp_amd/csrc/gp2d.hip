@@ -555,6 +555,28 @@ int gp2d_ozaki_prepare(const double* W, int64_t n, int64_t ldw, const gp2d_kerne
   return 0;
 }
 
+int gp2d_ozaki_prepare_async(const double* W, int64_t n, int64_t ldw, const gp2d_kernel_t* k, double diag_add,
+                             int8_t* wres, double* rowscale, int* nmod_out, void* stream) {
+  GP2D_CHECK(validate_kernel(k));
+  GP2D_REQUIRE(is_vector_family(k), "ozaki: vector families only");
+  GP2D_REQUIRE(n % IBM == 0 && n > 0, "ozaki: n must be a positive multiple of 256");
+  GP2D_REQUIRE(nmod_out != nullptr, "ozaki: nmod_out is NULL");
+  // the a-priori count bounds the data-driven one for any fit with this K_y diagonal (no host
+  // round trip); a violated bound could only come from a failed factor and is poisoned by CRT
+  const int nmod = gp2d_ozaki_nmod_apriori(n, k, diag_add);
+  GP2D_REQUIRE(nmod > 0, "ozaki: a-priori bound exceeds the modulus table");
+  hipStream_t s = S(stream);
+  double* l1 = reinterpret_cast<double*>(wres);  // scratch (unused here), overwritten below
+  ozaki_w_scale_kernel<<<(unsigned)n, 256, 0, s>>>(W, n, ldw, rowscale, l1);
+  GP2D_CHECK(check_launch("ozaki_w_scale_kernel"));
+  OzakiConsts oc;
+  GP2D_CHECK(make_ozaki_consts(nmod, k, oc));
+  ozaki_w_res_kernel<<<(unsigned)n, 256, 0, s>>>(W, n, ldw, oc, wres, rowscale);
+  GP2D_CHECK(check_launch("ozaki_w_res_kernel"));
+  *nmod_out = nmod;
+  return 0;
+}
+
 size_t gp2d_predict_ozaki_workspace(int64_t n, int64_t chunk) {
   const int nm = ozaki_nmod_for(n);
   if (nm <= 0) return 0;

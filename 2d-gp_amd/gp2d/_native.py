@@ -22,7 +22,8 @@ EXPORTS = (
     "gp2d_abi_version", "gp2d_padded_points", "gp2d_block_dim", "gp2d_kernel_diag",
     "gp2d_assemble", "gp2d_potrf_workspace", "gp2d_potrf", "gp2d_trtri_workspace", "gp2d_trtri",
     "gp2d_potrs_workspace", "gp2d_potrs_inv", "gp2d_predict_workspace", "gp2d_predict",
-    "gp2d_ozaki_nmod", "gp2d_ozaki_wres_bytes", "gp2d_ozaki_prepare", "gp2d_predict_ozaki_workspace",
+    "gp2d_ozaki_nmod", "gp2d_ozaki_wres_bytes", "gp2d_ozaki_prepare", "gp2d_ozaki_prepare_async",
+    "gp2d_predict_ozaki_workspace",
     "gp2d_predict_ozaki", "gp2d_ozaki_nmod_apriori", "gp2d_ozaki_kstar_bytes", "gp2d_ozaki_kstar",
     "gp2d_predict_ozaki_planes_workspace", "gp2d_predict_ozaki_planes", "gp2d_lml", "gp2d_lml_grad_count",
     "gp2d_lml_grad_workspace", "gp2d_lml_grad",
@@ -81,6 +82,7 @@ _SIGS = {
     "gp2d_ozaki_wres_bytes": (_SZ, [_I64]),
     "gp2d_ozaki_prepare": (_I, [_P, _I64, _I64, _KP, _P, _P, ctypes.POINTER(_I), _P]),
     "gp2d_ozaki_nmod_apriori": (_I, [_I64, _KP, _D]),
+    "gp2d_ozaki_prepare_async": (_I, [_P, _I64, _I64, _KP, _D, _P, _P, ctypes.POINTER(_I), _P]),
     "gp2d_ozaki_kstar_bytes": (_SZ, [_I64, _I64, _I64, _I]),
     "gp2d_ozaki_kstar": (_I, [_P, _I64, _I64, _P, _I64, _KP, _I, _I64, _P, _SZ, _P]),
     "gp2d_predict_ozaki_planes_workspace": (_SZ, [_I64, _I64]),

@@ -86,7 +86,7 @@ def fit_sharded(spec: E.KernelSpec, x, y, noise: float, device, mode: str = "bca
     gp = E.fit(spec, x, y, noise, jitter=jitter, device=device, variance=variance) if rank == 0 else None
     gp = broadcast_fit(gp, spec, noise, x, device)
     if variance == "ozaki" and "ozaki" not in gp.extra:
-        E.ozaki_prepare(gp)
+        E.ozaki_prepare(gp, diag_add=float(noise + jitter))   # a-priori moduli count: no host sync
     return gp
 
 

@@ -223,10 +223,10 @@ def fit(kernel: KernelSpec, x, y, noise: float, jitter: float = 0.0, device=None
                y=Y, beta=pwork[:n])   # gp2d_potrs_inv leaves β = W·y at the head of its workspace
     err = None
     if variance == "ozaki":
-        # enqueued before `info` is read: prepare's own synchronisation (the moduli count)
-        # then covers the whole fit, one host round trip instead of two
+        # enqueued before `info` is read, with the a-priori moduli count: the fit's only host
+        # round trip is the info read below
         try:
-            ozaki_prepare(gp)
+            ozaki_prepare(gp, diag_add=float(noise + jitter))
         except N.GP2DError as e:   # a failed factor (NaN rows) makes prepare fail too: info decides
             err = e
     inf = int(info.item())
@@ -239,16 +239,24 @@ def fit(kernel: KernelSpec, x, y, noise: float, jitter: float = 0.0, device=None
     return gp
 
 
-def ozaki_prepare(gp: GPFit) -> GPFit:
-    """Residue planes of W for the INT8 variance engine (once per fit)."""
+def ozaki_prepare(gp: GPFit, diag_add: float | None = None) -> GPFit:
+    """Residue planes of W for the INT8 variance engine (once per fit).  With `diag_add`
+    (the noise + jitter of K_y's diagonal) the moduli count is the a-priori bound and nothing
+    synchronises (gp2d_ozaki_prepare_async); without it, the data-driven count of the
+    factor's row bounds (one device → host read)."""
     L = N.lib()
     n = gp.n
     wres = torch.empty(int(L.gp2d_ozaki_wres_bytes(n)), dtype=torch.int8, device=gp.device)
     rowscale = torch.empty(n, dtype=torch.float64, device=gp.device)
     desc = gp.kernel.desc()
     nmod = ctypes.c_int(0)
-    N.check(L.gp2d_ozaki_prepare(_ptr(gp.W), n, n, ctypes.byref(desc), _ptr(wres), _ptr(rowscale),
-                                 ctypes.byref(nmod), _stream_handle(gp.device)), "gp2d_ozaki_prepare")
+    if diag_add is not None:
+        N.check(L.gp2d_ozaki_prepare_async(_ptr(gp.W), n, n, ctypes.byref(desc), float(diag_add), _ptr(wres),
+                                           _ptr(rowscale), ctypes.byref(nmod), _stream_handle(gp.device)),
+                "gp2d_ozaki_prepare_async")
+    else:
+        N.check(L.gp2d_ozaki_prepare(_ptr(gp.W), n, n, ctypes.byref(desc), _ptr(wres), _ptr(rowscale),
+                                     ctypes.byref(nmod), _stream_handle(gp.device)), "gp2d_ozaki_prepare")
     gp.extra["ozaki"] = (wres, rowscale, int(nmod.value))
     return gp
 

@@ -137,6 +137,12 @@ int    gp2d_ozaki_nmod(int64_t n);
 size_t gp2d_ozaki_wres_bytes(int64_t n);
 int    gp2d_ozaki_prepare(const double* W, int64_t n, int64_t ldw, const gp2d_kernel_t* k,
                           int8_t* wres, double* rowscale, int* nmod_out, void* stream);
+/* gp2d_ozaki_prepare_async: as gp2d_ozaki_prepare without the host round trip — the moduli
+ * count is gp2d_ozaki_nmod_apriori(n, k, diag_add) (diag_add = the noise + jitter on K_y's
+ * diagonal), which bounds the data-driven count for any fit of these hyperparameters.     */
+int    gp2d_ozaki_prepare_async(const double* W, int64_t n, int64_t ldw, const gp2d_kernel_t* k,
+                                double diag_add, int8_t* wres, double* rowscale, int* nmod_out,
+                                void* stream);
 size_t gp2d_predict_ozaki_workspace(int64_t n, int64_t chunk);
 int    gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int nmod, int64_t n,
                           const double* alpha, const double* xtr, int64_t ntr, int64_t ntr_pad,

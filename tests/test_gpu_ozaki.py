@@ -180,3 +180,26 @@ def test_kstar_ahead_bench_size_properties():
     assert np.array_equal(var, vi)
     assert rel(mu, mi) < 1e-11
     assert np.all(np.isfinite(var)) and np.all(var > 0)
+
+
+@pytest.mark.parametrize("kind,l,noise", [("df", 5.0, 0.0025), ("mixed", 3.0, 1e-4), ("cf", 8.0, 0.3)])
+def test_async_prepare_matches_data_driven(kind, l, noise):
+    """engine.fit prepares the W residue planes with the a-priori moduli count (no host
+    round trip); the data-driven preparation gives the same posterior (to the CRT constants'
+    rounding when the counts differ) and never more moduli."""
+    x, y = tracks(500, 17)
+    rng = np.random.default_rng(18)
+    xg = np.stack([rng.uniform(-5, 65, 1200), rng.uniform(-5, 50, 1200)], 1)
+    ks = E.KernelSpec(kind=kind, l_df=l, l_cf=l * 1.2, ratio=0.5 if kind == "mixed" else 1.0)
+    gp = E.fit(ks, x, y, noise=noise, variance="ozaki")
+    n_async = gp.extra["ozaki"][2]
+    ma, va = (t.cpu().numpy() for t in E.predict(gp, xg, chunk=512))
+    E.ozaki_prepare(gp)   # data-driven count (synchronises)
+    n_data = gp.extra["ozaki"][2]
+    md, vd = (t.cpu().numpy() for t in E.predict(gp, xg, chunk=512))
+    assert n_data <= n_async <= n_data + 1
+    if n_async == n_data:
+        assert np.array_equal(va, vd) and np.array_equal(ma, md)
+    assert rel(va, vd) < 1e-12 and rel(ma, md) < 1e-13
+    mo, vo = O.fit_predict(x, y, xg, kind=kind, l_df=l, l_cf=l * 1.2, ratio=ks.ratio, noise=noise)
+    assert rel(va, vo) < 1e-10 and rel(ma, mo) < 1e-10
