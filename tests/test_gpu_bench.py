@@ -1,0 +1,37 @@
+"""bench.py's one-line JSON contract (the driver parses it), on a tiny workload."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("no HIP device", allow_module_level=True)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("variance", ["ozaki", "f64"])
+def test_bench_json_contract(variance):
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--ntrain", "256", "--grid", "32", "--steps", "2",
+           "--warmup", "1", "--chunk", "1024", "--cpu-sample-points", "64", "--variance", variance]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=100, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+                "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert key in d, key
+    assert d["n_gpus"] == 1 and d["steps"] == 2 and d["warmup"] == 1 and d["higher_is_better"] is True
+    assert d["value"] > 0 and abs(d["value"] - 32 * 32 / (d["ms_per_step"] * 1e-3)) / d["value"] < 1e-6
+    assert d["vs_baseline"] is None and d["scaling"] == "weak" and "workload" in d["config"]
+    r = d["roofline"]
+    for key in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert key in r, key
+    assert r["bound"] == "mfma" and 0 < r["frac"] < 1 and abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-12
+    c = d["cpu_baseline"]
+    assert c["value"] > 0 and c["kind"] == "port" and c["cores"] >= 1 and c["sample"]
