@@ -195,72 +195,38 @@ size_t gp2d_potrf_workspace(int64_t) { return 0; }
 
 namespace {
 // POTRF streams (one set per device, created lazily): `crit` carries the critical path
-// (block-column update, diagonal block, panel TRSM) at the highest priority, `bulk` the
-// trailing SYRK.  GP2D_CU_RESERVE=R (R > 0) gives `crit` CUs [0, R) and `bulk` the rest
-// through hardware CU masks, so the single-workgroup diagonal kernel never shares a CU with
-// SYRK tiles.
+// (block-column updates, diagonal block, panel TRSM) at the highest priority, `bulk` the
+// trailing SYRK.  (Hardware CU masks splitting the CUs between the two were measured slower
+// at every split)
 struct FactorStreams {
   std::mutex mu;
-  std::vector<hipStream_t> crit, bulk, aux;   // indexed by device (aux: K* planes, bulk's CUs)
+  std::vector<hipStream_t> crit, bulk;   // indexed by device
   std::vector<std::vector<hipEvent_t>> ev;
 };
 FactorStreams g_fs;
-
-static int cu_reserve() {
-  const char* e = std::getenv("GP2D_CU_RESERVE");
-  return e ? std::max(0, std::atoi(e)) : 0;
-}
 
 int factor_streams(hipStream_t* crit, hipStream_t* bulk, std::vector<hipEvent_t>** evs) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) { set_error("hipGetDevice failed"); return -1; }
   std::lock_guard<std::mutex> lk(g_fs.mu);
   if ((int)g_fs.crit.size() <= dev) {
-    g_fs.crit.resize(dev + 1, nullptr); g_fs.bulk.resize(dev + 1, nullptr); g_fs.aux.resize(dev + 1, nullptr);
+    g_fs.crit.resize(dev + 1, nullptr); g_fs.bulk.resize(dev + 1, nullptr);
     g_fs.ev.resize(dev + 1);
   }
   if (!g_fs.crit[dev]) {
-    const int R = cu_reserve();
-    int ncu = 0;
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) ncu = 0;
-    if (R > 0 && R < ncu) {
-      std::vector<uint32_t> mc((ncu + 31) / 32, 0u), mb((ncu + 31) / 32, 0u);
-      for (int c = 0; c < ncu; ++c) (c < R ? mc : mb)[c / 32] |= 1u << (c % 32);
-      if (hipExtStreamCreateWithCUMask(&g_fs.crit[dev], (uint32_t)mc.size(), mc.data()) != hipSuccess ||
-          hipExtStreamCreateWithCUMask(&g_fs.bulk[dev], (uint32_t)mb.size(), mb.data()) != hipSuccess ||
-          hipExtStreamCreateWithCUMask(&g_fs.aux[dev], (uint32_t)mb.size(), mb.data()) != hipSuccess) {
-        set_error("hipExtStreamCreateWithCUMask failed"); return -1;
-      }
-    } else {
-      int lo = 0, hi = 0;
-      if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) { lo = 0; hi = 0; }
-      if (hipStreamCreateWithPriority(&g_fs.crit[dev], hipStreamNonBlocking, hi) != hipSuccess ||
-          hipStreamCreateWithPriority(&g_fs.bulk[dev], hipStreamNonBlocking, lo) != hipSuccess ||
-          hipStreamCreateWithPriority(&g_fs.aux[dev], hipStreamNonBlocking, lo) != hipSuccess) {
-        set_error("hipStreamCreate failed"); return -1;
-      }
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) { lo = 0; hi = 0; }
+    if (hipStreamCreateWithPriority(&g_fs.crit[dev], hipStreamNonBlocking, hi) != hipSuccess ||
+        hipStreamCreateWithPriority(&g_fs.bulk[dev], hipStreamNonBlocking, lo) != hipSuccess) {
+      set_error("hipStreamCreate failed"); return -1;
     }
-    g_fs.ev[dev].resize(5);
+    g_fs.ev[dev].resize(3);
     for (auto& e : g_fs.ev[dev])
       if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) { set_error("hipEventCreate failed"); return -1; }
   }
   *crit = g_fs.crit[dev];
   *bulk = g_fs.bulk[dev];
   *evs = &g_fs.ev[dev];
-  return 0;
-}
-
-// The K* planes on the aux stream (the bulk CUs when GP2D_CU_RESERVE masks them), joined
-// to the caller's stream at both ends.
-int aux_stream(hipStream_t* aux, hipEvent_t* e_in, hipEvent_t* e_out) {
-  hipStream_t c, b;
-  std::vector<hipEvent_t>* ev;
-  GP2D_CHECK(factor_streams(&c, &b, &ev));
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  *aux = g_fs.aux[dev];
-  *e_in = (*ev)[3];
-  *e_out = (*ev)[4];
   return 0;
 }
 
@@ -730,14 +696,7 @@ int gp2d_ozaki_kstar(const double* xtr, int64_t ntr, int64_t ntr_pad, const doub
   const VecParams vp = make_vec_params(k);
   const int64_t nmseg = (ntr_pad + OZ_KS_T - 1) / OZ_KS_T;
   const size_t stride = (size_t)nmod * (size_t)n * (size_t)(2 * round_up(chunk, IBN));
-  hipStream_t s0 = S(stream), s = s0;
-  hipEvent_t e_in = nullptr, e_out = nullptr;
-  if (cu_reserve() > 0) {   // experiment: keep the K* planes off the POTRF critical-path CUs
-    GP2D_CHECK(aux_stream(&s, &e_in, &e_out));
-    if (hipEventRecord(e_in, s0) != hipSuccess || hipStreamWaitEvent(s, e_in, 0) != hipSuccess) {
-      set_error("ozaki_kstar: stream join failed"); return -1;
-    }
-  }
+  hipStream_t s = S(stream);
   int64_t ci = 0;
   for (int64_t c0 = 0; c0 < m; c0 += chunk, ++ci) {
     const int64_t cv = std::min<int64_t>(chunk, m - c0);
@@ -745,9 +704,6 @@ int gp2d_ozaki_kstar(const double* xtr, int64_t ntr, int64_t ntr_pad, const doub
     ozaki_kstar_kernel<<<dim3((unsigned)nmseg, (unsigned)(cp / OZ_KS_P)), 256, 0, s>>>(
         xtr, ntr, ntr_pad, xg + point_dim(k) * c0, cv, cp, vp, nullptr, oc, bres + ci * stride, nullptr);
     GP2D_CHECK(check_launch("ozaki_kstar_kernel"));
-  }
-  if (s != s0 && (hipEventRecord(e_out, s) != hipSuccess || hipStreamWaitEvent(s0, e_out, 0) != hipSuccess)) {
-    set_error("ozaki_kstar: stream join failed"); return -1;
   }
   return 0;
 }

@@ -470,171 +470,6 @@ __global__ __launch_bounds__(512, 1) void igemm_nt_mod_kernel(const int8_t* __re
   }
 }
 
-// ------------------------------------------------------------------ INT8 NT GEMM mod m, v2
-// Same contract, tiles, slab layout, swizzle and epilogue as igemm_nt_mod_kernel, with a
-// staggered two-group schedule: the 8 waves are two groups of 4 (group g = wave row wr, one
-// wave of each group per SIMD), and every slab is two phases per wave separated by raw
-// barriers —
-//   READ  : issue this wave's LDS-DMA pieces of slab s+D, read all 12 fragments of slab s
-//           (8 A + 4 B, ds_read_b128), wait for them (lgkmcnt(0)); group 1 also waits for its
-//           own pieces of slab s+1 (vmcnt);
-//   MFMA  : 32 v_mfma_i32_16x16x64_i8 on the fragments (setprio 1); group 0 waits for its own
-//           pieces of slab s+1.
-// Group 1 runs one barrier behind group 0 (one extra barrier up front, group 0 one extra at
-// the end), so on every SIMD one wave is in its MFMA phase while the other reads — the matrix
-// core never waits for the LDS reads or the DMA issue of its own wave.
-// Ordering (barriers Y_s / Z_s open group 0's READ s / MFMA s; group 1's READ s is (Z_s, Y_s+1)):
-//   RAW: every wave's pieces of slab s+1 landed (its vmcnt) before Y_{s+1}, the first read of
-//        slab s+1 (group 0's READ s+1);
-//   WAR: the ring has D+1 stages; slab s+D overwrites slab s−1, whose last reads (group 1's
-//        READ s−1, retired by its lgkmcnt(0)) ended at Y_s, before either group issues it.
-template <int D>
-__device__ __forceinline__ void vmwait_upto(int c) {   // s_waitcnt vmcnt(4·min(c, D−1))
-  static_assert(D >= 1 && D <= 4, "prefetch distance 1..4");
-  if (c >= 3 && D >= 4) { asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); return; }
-  if (c >= 2 && D >= 3) { asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); return; }
-  if (c >= 1 && D >= 2) { asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); return; }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-#ifndef GP2D_IGEMM2_D
-#define GP2D_IGEMM2_D 3
-#endif
-constexpr int I2_D = GP2D_IGEMM2_D;           // slabs in flight ahead of the one being read
-constexpr int I2_NSTAGE = I2_D + 1;           // ring stages (32 KB each)
-
-__global__ __launch_bounds__(512, 1) void igemm2_nt_mod_kernel(const int8_t* __restrict__ A,
-                                                               const int8_t* __restrict__ B,
-                                                               uint8_t* __restrict__ C, int64_t ldc, int M, int N,
-                                                               int K, int a_lower, int modulus, double inv_mod,
-                                                               int alias_rb, int alias_ks) {
-  __shared__ __attribute__((aligned(16))) int8_t smem[I2_NSTAGE * I_STAGE];
-  const int bj = blockIdx.x;
-  const int bi = (int)(gridDim.y - 1 - blockIdx.y);   // heavy (long-K) row blocks first
-  const int i0 = bi * IBM, j0 = bj * IBN;
-  const int ke = a_lower ? min(K, i0 + IBM) : K;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = __builtin_amdgcn_readfirstlane(wid >> 2), wc = wid & 3;   // wr = the wave's group (SGPR: the
-  // group branches below must be scalar, s_barrier / s_waitcnt ignore EXEC)
-  const int l16 = lane & 15, lq = lane >> 4;
-  const int64_t kslabs = K / IBK;
-  const int8_t* Ap = A + (int64_t)bi * kslabs * I_OP;
-  const bool alias = bj >= alias_rb;
-  const int8_t* Bp = B + (int64_t)bj * kslabs * I_OP;
-  const int8_t* Bq = B + ((int64_t)(alias ? bj - alias_rb : 0) * kslabs + alias_ks) * I_OP;
-
-  i4v acc[8][4];
-#pragma unroll
-  for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = i4v{0, 0, 0, 0};
-
-  const int drow = lane >> 2, dchunk = lane & 3;
-  auto issue = [&](int s) {
-#ifdef GP2D_IGEMM_NO_DMA
-    return;
-#endif
-    int8_t* As = smem + (s % I2_NSTAGE) * I_STAGE;
-    int8_t* Bs = As + I_OP;
-    const int8_t* Ag = Ap + (int64_t)s * I_OP;
-    const int8_t* Bg = ((alias && s < alias_ks) ? Bq : Bp) + (int64_t)s * I_OP;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int row = wid * 32 + h * 16 + drow;
-      const int off = row * IBK + 16 * swz16(row, dchunk);
-      __builtin_amdgcn_global_load_lds((const void*)(Ag + off), (lds_ptr_t)(As + (wid * 32 + h * 16) * IBK), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(Bg + off), (lds_ptr_t)(Bs + (wid * 32 + h * 16) * IBK), 16, 0, 0);
-    }
-  };
-  const uint32_t lds_base = (uint32_t)(size_t)(lds_ptr_t)smem;
-  i4v a[8], b[4];
-#ifdef GP2D_IGEMM_NO_LDSREAD
-#pragma unroll
-  for (int u = 0; u < 8; ++u) a[u] = i4v{lane * 77 + u, u * 13 + wid, lane ^ 0x5a5a5a5a, lane * 0x01010101};
-#pragma unroll
-  for (int u = 0; u < 4; ++u) b[u] = i4v{lane * 31 + u, u ^ wid, lane * 0x3c3c3c3c, ~lane};
-#endif
-  auto read_frags = [&](int s) {
-#ifdef GP2D_IGEMM_NO_LDSREAD
-    return;
-#endif
-    const uint32_t As = lds_base + (s % I2_NSTAGE) * I_STAGE;
-    const uint32_t Bs = As + I_OP;
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni) {
-      const int row = wc * 64 + ni * 16 + l16;
-      const uint32_t ad = Bs + row * IBK + 16 * swz16(row, lq);
-      asm volatile("ds_read_b128 %0, %1" : "=v"(b[ni]) : "v"(ad) : "memory");
-    }
-#pragma unroll
-    for (int mi = 0; mi < 8; ++mi) {
-      const int row = wr * 128 + mi * 16 + l16;
-      const uint32_t ad = As + row * IBK + 16 * swz16(row, lq);
-      asm volatile("ds_read_b128 %0, %1" : "=v"(a[mi]) : "v"(ad) : "memory");
-    }
-  };
-  const int nsl = ke / IBK;   // ≥ 4
-#pragma unroll
-  for (int q = 0; q < I2_D; ++q)
-    if (q < nsl) issue(q);
-  vmwait_upto<I2_D>(min(I2_D, nsl) - 1);   // own pieces of slab 0 landed
-  asm volatile("s_barrier" ::: "memory");  // Y_0
-  if (wr == 1) asm volatile("s_barrier" ::: "memory");   // group 1 runs one barrier behind
-#pragma unroll 1
-  for (int s = 0; s < nsl; ++s) {
-    // ---- READ s
-    if (s + I2_D < nsl) issue(s + I2_D);
-    read_frags(s);
-    if (wr == 1) vmwait_upto<I2_D>(nsl - s - 2);   // own pieces of slab s+1 landed
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    // ---- MFMA s
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni)
-        acc[mi][ni] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-    if (wr == 0) vmwait_upto<I2_D>(nsl - s - 2);
-    asm volatile("s_barrier" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  if (wr == 0) asm volatile("s_barrier" ::: "memory");   // match group 1's extra barrier
-  asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  // Epilogue (as igemm_nt_mod_kernel): residues mod m, LDS transpose, coalesced column stores.
-  uint8_t* T = reinterpret_cast<uint8_t*>(smem);
-  constexpr int TP = IBM + 16;
-  const float fim = (float)inv_mod;
-#pragma unroll
-  for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni) {
-      uint32_t pk = 0;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int v = acc[mi][ni][u];
-        const int q = (int)floorf((float)v * fim);
-        int res = v - q * modulus;
-        res += (res < 0) ? modulus : 0;
-        res -= (res >= modulus) ? modulus : 0;
-        pk |= (uint32_t)res << (8 * u);
-      }
-      const int rloc = wr * 128 + mi * 16 + 4 * lq;
-      const int cloc = wc * 64 + ni * 16 + l16;
-      *reinterpret_cast<uint32_t*>(T + cloc * TP + rloc) = pk;
-    }
-  __syncthreads();
-#pragma unroll
-  for (int p = 0; p < (IBM * IBN / 16) / 512; ++p) {
-    const int id = tid + 512 * p;
-    const int cloc = id >> 4, ch = id & 15;
-    const uint4 v = *reinterpret_cast<const uint4*>(T + cloc * TP + 16 * ch);
-    *reinterpret_cast<uint4*>(C + (int64_t)(j0 + cloc) * ldc + i0 + 16 * ch) = v;
-  }
-}
-
 // ------------------------------------------------------------------ CRT + column Σ V²
 // Residue planes are column-major ([j][i], ld = n).  One wave per OZ_CRT_COLS consecutive
 // columns and a 1024-row segment: lane l reconstructs rows 16l..16l+15 (one 16-B load per

@@ -2,6 +2,7 @@
 // 8192×16384×8192 lower-triangular launch, and 4096 sampled outputs checked against a
 // CPU dot product.  Build variants with -DGP2D_IGEMM_NO_DMA / -DGP2D_IGEMM_NO_MFMA.
 #include "../../2d-gp_amd/csrc/ozaki.hpp"
+#include "igemm_v2.hpp"
 #include <cstdio>
 #include <random>
 #include <vector>
