@@ -2,12 +2,12 @@
 // (Ozaki scheme II: error-free integer splitting + Chinese-remainder reconstruction).
 //
 // The variance needs q_j = Σ_i V_ij² with V = W·K*ᵀ (W = L⁻¹, lower-triangular).  On
-// MI355X the FP64 MFMA peak is 78.6 TF while v_mfma_i32_32x32x32_i8 runs at 4.7 POPS
+// MI355X the FP64 MFMA peak is 78.6 TF while the int8 MFMAs run at 4.7 POPS back to back
 // (measured, tools/microbench/i8_mfma.hip), so the product is computed exactly in
 // integers instead:
 //   1. scale: Wint = rint(W_ik·2^{s_i}) (per-row power of two, |Wint| < 2^p) and
 //      Bint = rint(K*_jk·2^{s_B}) (one power of two from the analytic bound |K*| ≤ kss);
-//      both are exact integers held in fp64 (p = 42 < 53);
+//      both are exact integers held in fp64 (p = 50; DESIGN.md §3.1 for why 50);
 //   2. residues: for L pairwise-coprime moduli m_l ≤ 256 (Π m_l > n·2^{2p}), the
 //      centred residues of Wint / Bint fit int8; P_l = Wres_l · Bres_lᵀ is exact in
 //      int32 (|P_l| ≤ n·128²) and reduced mod m_l in the GEMM epilogue (uint8 planes);
