@@ -104,8 +104,8 @@ static int ozaki_nmod_bits(double log2_pmax) {
   }
   return -1;
 }
-// worst case (sizing): |Pint| ≤ n·2^p·2^{p−1}
-static int ozaki_nmod_for(int64_t n) { return ozaki_nmod_bits(std::log2((double)n) + 2.0 * OZ_P - 1.0); }
+// worst case (sizing): |Pint| ≤ n·2^{pW}·2^{pB−1}
+static int ozaki_nmod_for(int64_t n) { return ozaki_nmod_bits(std::log2((double)n) + OZ_PW + OZ_PB - 1.0); }
 
 static int64_t modinv(int64_t a, int64_t m) {  // a⁻¹ mod m (a, m coprime)
   int64_t t = 0, nt = 1, r = m, nr = ((a % m) + m) % m;
@@ -152,7 +152,7 @@ static int make_ozaki_consts(int nmod, const gp2d_kernel_t* k, OzakiConsts& oc) 
     oc.t[l] = ((double)inv - h * (double)ml) / (double)ml;  // h·m_l is exact (≤ 41 bits)
   }
   const double bmax = kstar_bound(k);
-  oc.sB = OZ_P - 1 - (int)std::ceil(std::log2(bmax));
+  oc.sB = OZ_PB - 1 - (int)std::ceil(std::log2(bmax));
   oc.vlimit = 4.0 * std::sqrt(gp2d_kernel_diag(k));
   return 0;
 }
@@ -493,9 +493,9 @@ int gp2d_ozaki_prepare(const double* W, int64_t n, int64_t ldw, const gp2d_kerne
     return -1;
   }
   // Bound on |Pint_ij| = |Σ_k Wint_ik·Bint_kj| per row i, the smaller of
-  //   (a) ‖Wint_i‖₁ · max|Bint|  ≤ l1_i · 2^{p−1}                       (always valid), and
+  //   (a) ‖Wint_i‖₁ · max|Bint|  ≤ l1_i · 2^{pB−1}                      (always valid), and
   //   (b) 2^{s_i+s_B}·|V_ij| + rounding terms, with |V_ij| ≤ ‖V_j‖₂ ≤ √kss (the posterior
-  //       variance kss − ‖V_j‖² is ≥ 0; factor 2 of slack), rounding ≤ n·2^{p−2} + l1_i + n.
+  //       variance kss − ‖V_j‖² is ≥ 0; factor 2 of slack), rounding ≤ n·2^{pB−2} + l1_i + n.
   // (b) is ≈ 5 bits tighter on the rows of L⁻¹; the identity rows of padded points take (a).
   // A violated bound cannot pass silently: the CRT kernel poisons columns with |V| > 4√kss.
   int sB = 0;
@@ -507,8 +507,8 @@ int gp2d_ozaki_prepare(const double* W, int64_t n, int64_t ldw, const gp2d_kerne
   const double sq = 2.0 * std::sqrt(gp2d_kernel_diag(k));
   double bmax = 1.0;
   for (int64_t i = 0; i < n; ++i) {
-    const double a = std::ldexp(hl1[i] * 1.01, OZ_P - 1);
-    const double b = std::ldexp(sq, (int)hs[i] + sB) + std::ldexp((double)n, OZ_P - 2) + hl1[i] + (double)n;
+    const double a = std::ldexp(hl1[i] * 1.01, OZ_PB - 1);
+    const double b = std::ldexp(sq, (int)hs[i] + sB) + std::ldexp((double)n, OZ_PB - 2) + hl1[i] + (double)n;
     bmax = std::max(bmax, std::min(a, b));
   }
   const int nmod = ozaki_nmod_bits(std::log2(bmax));
@@ -554,14 +554,14 @@ size_t gp2d_predict_ozaki_workspace(int64_t n, int64_t chunk) {
 
 // One chunked predict over the m grid points.  K* residue planes come either from the
 // inline ozaki_kstar_kernel (pre == nullptr: planes in the workspace, mean partials Σ α·K*)
-// or from gp2d_ozaki_kstar run earlier (pre: nmod_pre planes per chunk, chunk c at
-// pre + c·pre_stride; the mean is then Σ_i V_ij·β_i from the CRT kernel, β = W·y).
+// or from gp2d_ozaki_kstar run earlier (pre: planes per chunk at pre + c·pre_stride; the same
+// kernel then runs mean-only, so the mean is bit-identical to the inline path).
 static int predict_ozaki_impl(const int8_t* wres, const double* rowscale, int nmod, int64_t n,
-                              const double* alpha, const double* beta, const double* xtr, int64_t ntr,
+                              const double* alpha, const double* xtr, int64_t ntr,
                               int64_t ntr_pad, const double* xg, int64_t m, const gp2d_kernel_t* k, int var_mode,
                               double noise, int compute_var, double* mean, double* var, int64_t chunk,
                               int8_t* bres, uint8_t* cres, double* pm, double* P, const int8_t* pre,
-                              int nmod_pre, size_t pre_stride, hipStream_t s) {
+                              size_t pre_stride, hipStream_t s) {
   OzakiConsts oc;
   GP2D_CHECK(make_ozaki_consts(nmod, k, oc));
   const int nm = oc.nmod;
@@ -578,16 +578,12 @@ static int predict_ozaki_impl(const int8_t* wres, const double* rowscale, int nm
     const int64_t cv = std::min<int64_t>(chunk, m - c0);
     const int64_t cp = round_up(cv, IBN);   // whole 256-row tiles per component half (B aliasing)
     const int64_t ncols = 2 * cp;
-    const int8_t* B = bres;
-    size_t bplane = (size_t)ncols * n;
-    if (pre) {
-      B = pre + (size_t)ci * pre_stride;
-      bplane = (size_t)ncols * n;
-    } else {
-      ozaki_kstar_kernel<<<dim3((unsigned)nmseg, (unsigned)(cp / OZ_KS_P)), 256, 0, s>>>(
-          xtr, ntr, ntr_pad, xg + point_dim(k) * c0, cv, cp, vp, alpha, compute_var ? oc : oc_mean_only, bres, pm);
-      GP2D_CHECK(check_launch("ozaki_kstar_kernel"));
-    }
+    const int8_t* B = pre ? pre + (size_t)ci * pre_stride : bres;
+    const size_t bplane = (size_t)ncols * n;
+    ozaki_kstar_kernel<<<dim3((unsigned)nmseg, (unsigned)(cp / OZ_KS_P)), 256, 0, s>>>(
+        xtr, ntr, ntr_pad, xg + point_dim(k) * c0, cv, cp, vp, alpha, (compute_var && !pre) ? oc : oc_mean_only,
+        bres, pm);
+    GP2D_CHECK(check_launch("ozaki_kstar_kernel"));
     if (compute_var) {
       hipEvent_t e0 = nullptr, e1 = nullptr;
       {
@@ -609,18 +605,13 @@ static int predict_ozaki_impl(const int8_t* wres, const double* rowscale, int nm
         g_timing.flops.push_back(2.0 * (double)cv * nv * nv);  // FP64-equivalent algorithmic flop
       }
       const dim3 cgrid((unsigned)((ncols + OZ_CRT_BCOLS - 1) / OZ_CRT_BCOLS), (unsigned)npseg);
-      if (pre) {
-        ozaki_crt_colsq_kernel<true><<<cgrid, 256, 0, s>>>(cres, n, ncols, oc, rowscale, P, beta, pm);
-      } else {
-        ozaki_crt_colsq_kernel<false><<<cgrid, 256, 0, s>>>(cres, n, ncols, oc, rowscale, P, nullptr, nullptr);
-      }
+      ozaki_crt_colsq_kernel<<<cgrid, 256, 0, s>>>(cres, n, ncols, oc, rowscale, P);
       GP2D_CHECK(check_launch("ozaki_crt_colsq_kernel"));
     }
     predict_finalize_kernel<<<(unsigned)((ncols + 63) / 64), 64, 0, s>>>(
-        pm, pre ? npseg : nmseg, P, npseg, ncols, cp, cv, c0, m, kss, add, clip, compute_var, mean, var);
+        pm, nmseg, P, npseg, ncols, cp, cv, c0, m, kss, add, clip, compute_var, mean, var);
     GP2D_CHECK(check_launch("predict_finalize_kernel"));
   }
-  (void)nmod_pre;
   return 0;
 }
 
@@ -649,11 +640,11 @@ int gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int nmod, int
   uint8_t* cres = reinterpret_cast<uint8_t*>(bres + (size_t)nm * n * ncols_max);
   double* pm = reinterpret_cast<double*>(cres + (size_t)nm * n * ncols_max);
   double* P = pm + (size_t)(n / 2 / OZ_KS_T + 1) * ncols_max;
-  return predict_ozaki_impl(wres, rowscale, nmod, n, alpha, nullptr, xtr, ntr, ntr_pad, xg, m, k, var_mode, noise,
-                            compute_var, mean, var, chunk, bres, cres, pm, P, nullptr, 0, 0, S(stream));
+  return predict_ozaki_impl(wres, rowscale, nmod, n, alpha, xtr, ntr, ntr_pad, xg, m, k, var_mode, noise,
+                            compute_var, mean, var, chunk, bres, cres, pm, P, nullptr, 0, S(stream));
 }
 
-// ---- K* residue planes ahead of the fit (the planes need no α: see the CRT kernel)
+// ---- K* residue planes ahead of the fit (they depend on the points and the kernel only)
 int gp2d_ozaki_nmod_apriori(int64_t n, const gp2d_kernel_t* k, double diag_add) {
   // gp2d_ozaki_prepare's per-row bound (b) with the largest row exponent any fit can have:
   // W_ii = 1/L_ii ≥ 1/√(K_y,ii) (L_ii² = K_y,ii − Σ L_ik²), so max_k |W_ik| ≥ 1/√(kss + diag_add)
@@ -663,13 +654,13 @@ int gp2d_ozaki_nmod_apriori(int64_t n, const gp2d_kernel_t* k, double diag_add) 
   if (validate_kernel(k) != 0 || !is_vector_family(k) || n <= 0) return -1;
   const double kss = gp2d_kernel_diag(k);
   const double dmin = (1.0 - std::ldexp(1.0, -40)) / std::sqrt(kss + diag_add);
-  const int smax = OZ_P - 1 - (int)std::floor(std::log2(dmin));
+  const int smax = OZ_PW - 1 - (int)std::floor(std::log2(dmin));
   OzakiConsts probe;
   if (make_ozaki_consts(1, k, probe) != 0) return -1;
   const double sq = 2.0 * std::sqrt(kss);
-  const double b = std::ldexp(sq, smax + probe.sB) + std::ldexp((double)n, OZ_P - 2) + std::ldexp((double)n, OZ_P) +
+  const double b = std::ldexp(sq, smax + probe.sB) + std::ldexp((double)n, OZ_PB - 2) + std::ldexp((double)n, OZ_PW) +
                    (double)n;
-  const double a_id = 1.01 * std::ldexp(1.0, 2 * OZ_P - 2);
+  const double a_id = 1.01 * std::ldexp(1.0, OZ_PW + OZ_PB - 2);
   return ozaki_nmod_bits(std::log2(std::max(b, a_id)));
 }
 
@@ -715,10 +706,11 @@ size_t gp2d_predict_ozaki_planes_workspace(int64_t n, int64_t chunk) {
   return (size_t)nm * (size_t)n * (size_t)ncols + sizeof(double) * ozaki_partials(n) * (size_t)ncols;
 }
 
-int gp2d_predict_ozaki_planes(const int8_t* wres, const double* rowscale, int nmod, int64_t n, const double* beta,
-                              const int8_t* bres, int nmod_b, int64_t ntr, int64_t ntr_pad, int64_t m,
-                              const gp2d_kernel_t* k, int var_mode, double noise, double* mean, double* var,
-                              int64_t chunk, void* work, size_t work_bytes, void* stream) {
+int gp2d_predict_ozaki_planes(const int8_t* wres, const double* rowscale, int nmod, int64_t n, const double* alpha,
+                              const double* xtr, int64_t ntr, int64_t ntr_pad, const double* xg, int64_t m,
+                              const gp2d_kernel_t* k, int var_mode, double noise, const int8_t* bres, int nmod_b,
+                              double* mean, double* var, int64_t chunk, void* work, size_t work_bytes,
+                              void* stream) {
   GP2D_CHECK(validate_kernel(k));
   GP2D_REQUIRE(is_vector_family(k), "ozaki: vector families only");
   GP2D_REQUIRE(n == 2 * ntr_pad && n % IBM == 0, "ozaki: n must equal 2·ntr_pad and be a multiple of 256");
@@ -726,7 +718,7 @@ int gp2d_predict_ozaki_planes(const int8_t* wres, const double* rowscale, int nm
   GP2D_REQUIRE(work != nullptr && work_bytes >= gp2d_predict_ozaki_planes_workspace(n, chunk),
                "ozaki: workspace too small");
   GP2D_REQUIRE(var_mode >= 0 && var_mode <= 2, "predict: bad var_mode");
-  GP2D_REQUIRE(beta != nullptr && bres != nullptr, "ozaki_planes: beta and the K* planes are required");
+  GP2D_REQUIRE(alpha != nullptr && bres != nullptr, "ozaki_planes: alpha and the K* planes are required");
   if (m <= 0) return 0;
   GP2D_REQUIRE(nmod > 0 && nmod <= ozaki_nmod_for(n), "ozaki: nmod exceeds the worst-case count");
   if (nmod > nmod_b) {
@@ -738,8 +730,8 @@ int gp2d_predict_ozaki_planes(const int8_t* wres, const double* rowscale, int nm
   double* pm = reinterpret_cast<double*>(cres + (size_t)nmod * n * ncols_max);
   double* P = pm + (size_t)std::max<int64_t>(n / 2 / OZ_KS_T + 1, n / OZ_CRT_ROWS + 1) * ncols_max;
   const size_t stride = (size_t)nmod_b * (size_t)n * (size_t)ncols_max;
-  return predict_ozaki_impl(wres, rowscale, nmod, n, nullptr, beta, nullptr, ntr, ntr_pad, nullptr, m, k, var_mode,
-                            noise, 1, mean, var, chunk, nullptr, cres, pm, P, bres, nmod_b, stride, S(stream));
+  return predict_ozaki_impl(wres, rowscale, nmod, n, alpha, xtr, ntr, ntr_pad, xg, m, k, var_mode, noise, 1, mean,
+                            var, chunk, nullptr, cres, pm, P, bres, stride, S(stream));
 }
 
 // ------------------------------------------------- LOG MARGINAL LIKELIHOOD (§8f.1)

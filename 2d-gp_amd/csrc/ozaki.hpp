@@ -5,10 +5,10 @@
 // MI355X the FP64 MFMA peak is 78.6 TF while the int8 MFMAs run at 4.7 POPS back to back
 // (measured, tools/microbench/i8_mfma.hip), so the product is computed exactly in
 // integers instead:
-//   1. scale: Wint = rint(W_ik·2^{s_i}) (per-row power of two, |Wint| < 2^p) and
-//      Bint = rint(K*_jk·2^{s_B}) (one power of two from the analytic bound |K*| ≤ kss);
-//      both are exact integers held in fp64 (p = 50; DESIGN.md §3.1 for why 50);
-//   2. residues: for L pairwise-coprime moduli m_l ≤ 256 (Π m_l > n·2^{2p}), the
+//   1. scale: Wint = rint(W_ik·2^{s_i}) (per-row power of two, |Wint| < 2^{pW}) and
+//      Bint = rint(K*_jk·2^{s_B}) (one power of two from the analytic bound |K*| ≤ kss,
+//      |Bint| < 2^{pB}); both are exact integers held in fp64 (pW = 49, pB = 45);
+//   2. residues: for L pairwise-coprime moduli m_l ≤ 256 (Π m_l > n·2^{pW+pB}), the
 //      centred residues of Wint / Bint fit int8; P_l = Wres_l · Bres_lᵀ is exact in
 //      int32 (|P_l| ≤ n·128²) and reduced mod m_l in the GEMM epilogue (uint8 planes);
 //   3. CRT: Pint/M = frac(Σ_l c_l·inv_l/m_l), evaluated with an exact high part
@@ -24,10 +24,23 @@
 namespace gp2d {
 
 constexpr int OZ_MAXMOD = 16;
-#ifndef GP2D_OZ_P
-#define GP2D_OZ_P 50
+#ifdef GP2D_OZ_P                   // one precision for both operands (dev builds)
+#define GP2D_OZ_PW GP2D_OZ_P
+#define GP2D_OZ_PB GP2D_OZ_P
 #endif
-constexpr int OZ_P = GP2D_OZ_P;    // integer bits of the scaled operands (≤ 50: residues stay exact)
+#ifndef GP2D_OZ_PW
+#define GP2D_OZ_PW 49
+#endif
+#ifndef GP2D_OZ_PB
+#define GP2D_OZ_PB 45
+#endif
+// integer bits of the scaled operands: W rows (OZ_PW) and K* (OZ_PB); ≤ 52 keeps the
+// scaled values exact in fp64, the moduli count follows OZ_PW + OZ_PB.  The rounding of W
+// dominates the error, so 49 + 45 (12 moduli at the bench size) is more accurate than
+// 47 + 47 and close to 50 + 50 (13 moduli); measured in DESIGN.md §3.1.
+constexpr int OZ_PW = GP2D_OZ_PW;
+constexpr int OZ_PB = GP2D_OZ_PB;
+static_assert(OZ_PW <= 52 && OZ_PB <= 52, "ozaki: scaled operands must stay exact in fp64");
 constexpr int OZ_HBITS = 33;       // exact high part of inv_l / m_l
 
 struct OzakiConsts {
@@ -84,7 +97,7 @@ __global__ __launch_bounds__(256) void ozaki_w_scale_kernel(const double* __rest
   for (int64_t k = tid; k <= i; k += 256) mx = fmax(mx, fabs(w[k]));
   mx = block_reduce(mx, red, true);
   const int e = (mx > 0.0) ? ilogb(mx) : 0;    // 2^e ≤ mx < 2^{e+1}
-  const int si = OZ_P - 1 - e;                 // |W·2^si| < 2^OZ_P
+  const int si = OZ_PW - 1 - e;                // |W·2^si| < 2^OZ_PW
   double sum = 0.0;
   for (int64_t k = tid; k <= i; k += 256) sum += fabs(rint(ldexp(w[k], si)));
   sum = block_reduce(sum, red, false);
@@ -132,7 +145,8 @@ __global__ __launch_bounds__(256) void ozaki_w_res_kernel(const double* __restri
 // tile — 256 contiguous bytes (the slab-blocked layout puts rows of a 256-row tile 64 B
 // apart).  Writes the residue planes Bres[l] (rows j = grid components, columns k =
 // training components, slab-blocked) and mean partials pm[bx][j] = Σ_{k in block} α_k·K*_jk
-// (16-lane shuffle reduction in a fixed order).  alpha == nullptr: planes only.
+// (16-lane shuffle reduction in a fixed order).  alpha == nullptr: planes only; oc.nmod == 0:
+// mean only (the planes were built earlier by gp2d_ozaki_kstar).
 constexpr int OZ_KS_T = 64;   // training points per block
 constexpr int OZ_KS_P = 64;   // grid points per block
 
@@ -474,41 +488,30 @@ __global__ __launch_bounds__(512, 1) void igemm_nt_mod_kernel(const int8_t* __re
 // Residue planes are column-major ([j][i], ld = n).  One wave per OZ_CRT_COLS consecutive
 // columns and a 1024-row segment: lane l reconstructs rows 16l..16l+15 (one 16-B load per
 // plane and column), squares, and the wave reduces each column in a fixed shuffle order →
-// partial[seg][j].  The lane's 16 row scales (and β values) stay in registers across the
-// wave's columns.
-//
-// MEAN: also Q[seg][j] = Σ_i V_ij·β_i with β = W·y, because K*α = K*·Wᵀ(W y) = Vᵀβ — the mean
-// then needs no α when the K* planes are generated, so they can be built before (and
-// concurrently with) the fit (gp2d_ozaki_kstar).
+// partial[seg][j].  The lane's 16 row scales stay in registers across the wave's columns.
 constexpr int OZ_CRT_ROWS = 1024;
 constexpr int OZ_CRT_COLS = 4;    // columns per wave
 constexpr int OZ_CRT_BCOLS = 4 * OZ_CRT_COLS;   // columns per 256-thread block
 
-template <bool MEAN>
 __global__ __launch_bounds__(256) void ozaki_crt_colsq_kernel(const uint8_t* __restrict__ cres, int64_t n,
                                                               int64_t ncols, OzakiConsts oc,
                                                               const double* __restrict__ rowscale,
-                                                              double* __restrict__ P,
-                                                              const double* __restrict__ beta,
-                                                              double* __restrict__ Q) {
+                                                              double* __restrict__ P) {
   const int lane = threadIdx.x & 63;
   const int64_t jw = (int64_t)blockIdx.x * OZ_CRT_BCOLS + (threadIdx.x >> 6) * OZ_CRT_COLS;
   const int64_t seg = blockIdx.y;
   const int64_t i0 = seg * OZ_CRT_ROWS + 16 * lane;
   if (jw >= ncols) return;
   const bool rows_ok = i0 < n;
-  double rs[16], bt[16];
+  double rs[16];
 #pragma unroll
-  for (int c = 0; c < 16; ++c) {
-    rs[c] = rows_ok ? rowscale[i0 + c] : 0.0;
-    bt[c] = (MEAN && rows_ok) ? beta[i0 + c] : 0.0;
-  }
+  for (int c = 0; c < 16; ++c) rs[c] = rows_ok ? rowscale[i0 + c] : 0.0;
   const int64_t plane = n * ncols;
 #pragma unroll 1
   for (int jc = 0; jc < OZ_CRT_COLS; ++jc) {
     const int64_t j = jw + jc;
     if (j >= ncols) break;
-    double acc = 0.0, mq = 0.0;
+    double acc = 0.0;
     if (rows_ok) {
       double H[16], T[16];
 #pragma unroll
@@ -538,7 +541,6 @@ __global__ __launch_bounds__(256) void ozaki_crt_colsq_kernel(const uint8_t* __r
         const double f = (H[c] - rint(H[c])) + T[c];   // Pint / M, centred
         const double vij = f * rs[c];
         acc = fma(vij, vij, acc);
-        if constexpr (MEAN) mq = fma(vij, bt[c], mq);
         // |V_ij| ≤ ‖V_j‖₂ ≤ √kss: a value past the limit can only come from a CRT wrap-around
         // (|Pint| ≥ M/2, i.e. too few moduli) — poison the column instead of returning garbage
         if (fabs(vij) > oc.vlimit) acc = __builtin_nan("");
@@ -547,11 +549,6 @@ __global__ __launch_bounds__(256) void ozaki_crt_colsq_kernel(const uint8_t* __r
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
     if (lane == 0) P[seg * ncols + j] = acc;
-    if constexpr (MEAN) {
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) mq += __shfl_xor(mq, o);
-      if (lane == 0) Q[seg * ncols + j] = mq;
-    }
   }
 }
 

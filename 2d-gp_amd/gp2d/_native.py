@@ -12,6 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GP2D_LIB", os.path.join(_HERE, "libgp2d.so"))
+ABI_VERSION = 2          # GP2D_ABI_VERSION in include/gp2d.h
 
 FAMILY_VECTOR2D, FAMILY_ARD_RBF, FAMILY_VECTOR_ST = 0, 1, 2
 KIND_SCALAR, KIND_DIVFREE, KIND_CURLFREE, KIND_MIXED = 0, 1, 2, 3
@@ -86,8 +87,8 @@ _SIGS = {
     "gp2d_ozaki_kstar_bytes": (_SZ, [_I64, _I64, _I64, _I]),
     "gp2d_ozaki_kstar": (_I, [_P, _I64, _I64, _P, _I64, _KP, _I, _I64, _P, _SZ, _P]),
     "gp2d_predict_ozaki_planes_workspace": (_SZ, [_I64, _I64]),
-    "gp2d_predict_ozaki_planes": (_I, [_P, _P, _I, _I64, _P, _P, _I, _I64, _I64, _I64, _KP, _I, _D, _P, _P, _I64,
-                                       _P, _SZ, _P]),
+    "gp2d_predict_ozaki_planes": (_I, [_P, _P, _I, _I64, _P, _P, _I64, _I64, _P, _I64, _KP, _I, _D, _P, _I, _P, _P,
+                                       _I64, _P, _SZ, _P]),
     "gp2d_predict_ozaki_workspace": (_SZ, [_I64, _I64]),
     "gp2d_predict_ozaki": (_I, [_P, _P, _I, _I64, _P, _P, _I64, _I64, _P, _I64, _KP, _I, _D, _I, _P, _P, _I64, _P,
                                 _SZ, _P]),
@@ -123,7 +124,7 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.gp2d_abi_version() != 1:
+        if L.gp2d_abi_version() != ABI_VERSION:
             raise NativeLibraryError("libgp2d.so ABI version mismatch")
         _lib = L
         return _lib

@@ -24,39 +24,37 @@ def world():
 
 
 def broadcast_fit(gp: E.GPFit | None, spec: E.KernelSpec, noise: float, x, device, src: int = 0) -> E.GPFit:
-    """Broadcast W, α (with β = W·y when the fit has it) and the training points from `src` to every rank (RCCL
+    """Broadcast W, α and the training points from `src` to every rank (RCCL
     ncclBroadcast under the 'nccl' backend).  Ranks other than `src` pass gp=None."""
     ws, rank = world()
     if ws == 1:
         return gp
-    meta = torch.zeros(4, dtype=torch.int64, device=device)
+    meta = torch.zeros(3, dtype=torch.int64, device=device)
     if rank == src:
-        meta[0], meta[1], meta[2], meta[3] = gp.n, gp.n_train, gp.n_pad, int(gp.beta is not None)
+        meta[0], meta[1], meta[2] = gp.n, gp.n_train, gp.n_pad
     dist.broadcast(meta, src)
-    n, ntr, npad, has_beta = (int(v) for v in meta.tolist())
-    nab = 2 * n if has_beta else n
+    n, ntr, npad = (int(v) for v in meta.tolist())
     blocks = packed_blocks(n)
     packed = torch.empty(blocks[-1][2], dtype=torch.float64, device=device)
     if rank != src:
         W = torch.zeros((n, n), dtype=torch.float64, device=device)
-        ab = torch.empty(nab, dtype=torch.float64, device=device)
+        alpha = torch.empty(n, dtype=torch.float64, device=device)
         X = torch.empty((ntr, spec.input_dim), dtype=torch.float64, device=device)
     else:
-        W, X = gp.W, gp.x
-        ab = torch.cat([gp.alpha, gp.beta]) if has_beta else gp.alpha
+        W, X, alpha = gp.W, gp.x, gp.alpha
         for r0, c1, off in blocks[:-1]:
             packed[off:off + PACK_ROWS * c1].view(PACK_ROWS, c1).copy_(W[r0:r0 + PACK_ROWS, :c1])
     # W = L⁻¹ is lower-triangular: only the row blocks' [0, end of their diagonal block)
     # columns travel (≈ half of n² doubles)
     dist.broadcast(packed, src)
-    dist.broadcast(ab, src)   # α and β = W·y (the mean from precomputed K* planes)
+    dist.broadcast(alpha, src)
     dist.broadcast(X, src)
     if rank == src:
         return gp
     for r0, c1, off in blocks[:-1]:
         W[r0:r0 + PACK_ROWS, :c1].copy_(packed[off:off + PACK_ROWS * c1].view(PACK_ROWS, c1))
-    return E.GPFit(kernel=spec, noise=float(noise), x=X, n_train=ntr, n_pad=npad, W=W, alpha=ab[:n],
-                   device=torch.device(device), beta=ab[n:] if has_beta else None)
+    return E.GPFit(kernel=spec, noise=float(noise), x=X, n_train=ntr, n_pad=npad, W=W, alpha=alpha,
+                   device=torch.device(device))
 
 
 PACK_ROWS = 128   # the matrix order is a multiple of 128 (engine.fit_layout)

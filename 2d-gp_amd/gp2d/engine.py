@@ -141,7 +141,6 @@ class GPFit:
     info: int = 0
     extra: dict = field(default_factory=dict)
     y: torch.Tensor = None   # (n,) padded observations (LML)
-    beta: torch.Tensor = None  # (n,) W·y (the mean from precomputed K* planes: K*α = (W K*ᵀ)ᵀβ)
 
     @property
     def n(self) -> int:
@@ -220,7 +219,8 @@ def fit(kernel: KernelSpec, x, y, noise: float, jitter: float = 0.0, device=None
     pwork = torch.empty(pbytes // 8 + 1, dtype=torch.float64, device=dev)
     N.check(L.gp2d_potrs_inv(_ptr(A), n, n, _ptr(Y), _ptr(alpha), _ptr(pwork), pbytes, s), "gp2d_potrs_inv")
     gp = GPFit(kernel=kernel, noise=float(noise), x=X, n_train=ntr, n_pad=npad, W=A, alpha=alpha, device=dev,
-               y=Y, beta=pwork[:n])   # gp2d_potrs_inv leaves β = W·y at the head of its workspace
+               y=Y)
+    del pwork
     err = None
     if variance == "ozaki":
         # enqueued before `info` is read, with the a-priori moduli count: the fit's only host
@@ -340,7 +340,7 @@ class Predictor:
     def __call__(self, xg, var_mode: str = "latent", compute_var: bool = True, out=None,
                  planes: KstarPlanes | None = None):
         """planes: K* residue planes of this same grid from kstar_planes() (ozaki engine):
-        the predict then skips K* generation and takes the mean as Vᵀβ."""
+        the variance GEMMs read them and the K* kernel runs mean-only (same results as without)."""
         gp = self.gp
         L = N.lib()
         d, bd = gp.kernel.input_dim, gp.kernel.block_dim
@@ -352,16 +352,17 @@ class Predictor:
         else:
             mean, var = out
         desc = gp.kernel.desc()
-        if planes is not None and compute_var and self.ozaki and "ozaki" in gp.extra and gp.beta is not None:
+        if planes is not None and compute_var and self.ozaki and "ozaki" in gp.extra:
             if planes.m != m or planes.n != gp.n or planes.chunk != self.chunk:
                 raise ValueError("K* planes were made for another grid, fit layout or chunk size")
             wres, rowscale, nmod = gp.extra["ozaki"]
             s = torch.cuda.current_stream(gp.device)
             s.wait_event(planes.event)
-            rc = L.gp2d_predict_ozaki_planes(_ptr(wres), _ptr(rowscale), nmod, gp.n, _ptr(gp.beta), _ptr(planes.bres),
-                                             planes.nmod, gp.n_train, gp.n_pad, m, ctypes.byref(desc),
-                                             _VAR_MODES[var_mode], float(gp.noise), _ptr(mean), _ptr(var),
-                                             self.chunk, _ptr(self.work), self.wbytes, ctypes.c_void_p(s.cuda_stream))
+            rc = L.gp2d_predict_ozaki_planes(_ptr(wres), _ptr(rowscale), nmod, gp.n, _ptr(gp.alpha), _ptr(gp.x),
+                                             gp.n_train, gp.n_pad, _ptr(G), m, ctypes.byref(desc),
+                                             _VAR_MODES[var_mode], float(gp.noise), _ptr(planes.bres), planes.nmod,
+                                             _ptr(mean), _ptr(var), self.chunk, _ptr(self.work), self.wbytes,
+                                             ctypes.c_void_p(s.cuda_stream))
             if rc != -3:   # −3: the fit needs more moduli than the planes carry → inline K* below
                 N.check(rc, "gp2d_predict_ozaki_planes")
                 return mean, var

@@ -50,7 +50,7 @@ def parse():
                     help="variance contraction: exact INT8 Ozaki-II emulation (default) or FP64 MFMA")
     ap.add_argument("--kstar-ahead", type=int, default=-1,
                     help="ozaki: generate the K* residue planes on a side stream concurrently with the fit "
-                         "(mean from V^T beta); 0 = inline per chunk after the fit; -1 (auto) = only while "
+                         "(the mean stays K* alpha in fp64); 0 = inline per chunk after the fit; -1 (auto) = only while "
                          "non-root ranks wait for the factor broadcast (N>1, bcast)")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-sample-points", type=int, default=2048)

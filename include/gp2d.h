@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define GP2D_ABI_VERSION 1
+#define GP2D_ABI_VERSION 2
 
 /* kernel families */
 #define GP2D_FAMILY_VECTOR2D 0   /* 2×2 matrix-valued SE kernels on (x1, x2)          */
@@ -150,15 +150,17 @@ int    gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int nmod, 
                           int var_mode, double noise, int compute_var,
                           double* mean, double* var, int64_t chunk,
                           void* work, size_t work_bytes, void* stream);
-/* K* residue planes ahead of the fit.  K*α = K*·Wᵀ(W y) = Vᵀβ with V = W·K*ᵀ (the product
- * the variance already computes) and β = W·y (the first half of gp2d_potrs_inv), so the K*
- * planes need no α and can be generated before / concurrently with the fit:
+/* K* residue planes ahead of the fit.  The int8 residues of K* depend only on the training
+ * points, the grid and the kernel, so they can be generated before / concurrently with the
+ * fit (e.g. while a rank waits for the factor broadcast):
  * gp2d_ozaki_nmod_apriori: a moduli count that bounds gp2d_ozaki_prepare's data-driven one
  *   for any fit of this kernel with diagonal K_y,ii = kdiag + diag_add (−1 on bad input);
  * gp2d_ozaki_kstar: the planes of every chunk of the m grid points (nmod planes per chunk,
  *   chunk c at bres + c·nmod·n·2·⌈chunk/256⌉·256 bytes; size gp2d_ozaki_kstar_bytes);
- * gp2d_predict_ozaki_planes: GEMMs + CRT (+ mean Σ V_ij β_i) + finalize from those planes;
- *   returns −3 if the fit needs more moduli than nmod_b (the caller regenerates).
+ * gp2d_predict_ozaki_planes: gp2d_predict_ozaki (compute_var = 1) with the variance GEMMs
+ *   reading those planes; the mean K*α is evaluated in fp64 as in gp2d_predict_ozaki, so
+ *   both outputs are bit-identical to it.  Returns −3 if the fit needs more moduli than
+ *   nmod_b (the caller regenerates).
  * Replaces the same reference calls as gp2d_predict_ozaki (compute_Ks + getMean + the
  * variance diagonal, GP_laser.py:122-136).                                              */
 int    gp2d_ozaki_nmod_apriori(int64_t n, const gp2d_kernel_t* k, double diag_add);
@@ -168,10 +170,10 @@ int    gp2d_ozaki_kstar(const double* xtr, int64_t ntr, int64_t ntr_pad, const d
                         void* stream);
 size_t gp2d_predict_ozaki_planes_workspace(int64_t n, int64_t chunk);
 int    gp2d_predict_ozaki_planes(const int8_t* wres, const double* rowscale, int nmod, int64_t n,
-                                 const double* beta, const int8_t* bres, int nmod_b, int64_t ntr,
-                                 int64_t ntr_pad, int64_t m, const gp2d_kernel_t* k, int var_mode,
-                                 double noise, double* mean, double* var, int64_t chunk,
-                                 void* work, size_t work_bytes, void* stream);
+                                 const double* alpha, const double* xtr, int64_t ntr, int64_t ntr_pad,
+                                 const double* xg, int64_t m, const gp2d_kernel_t* k, int var_mode,
+                                 double noise, const int8_t* bres, int nmod_b, double* mean, double* var,
+                                 int64_t chunk, void* work, size_t work_bytes, void* stream);
 
 /* ---- hyperparameters: log marginal likelihood and its gradient -----
  * Replaces the objective of GPy model.optimize / optimize_restarts (krig.py:450,

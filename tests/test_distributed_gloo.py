@@ -48,9 +48,8 @@ def _worker(rank, world, port, out_dir):
         W = torch.tril(torch.randn(n, n, generator=g, dtype=torch.float64))
         alpha = torch.randn(n, generator=g, dtype=torch.float64)
         X = torch.randn(100, 2, generator=g, dtype=torch.float64)
-        beta = torch.randn(n, generator=g, dtype=torch.float64)
         gp = E.GPFit(kernel=spec, noise=0.01, x=X, n_train=100, n_pad=128, W=W, alpha=alpha,
-                     device=torch.device("cpu"), beta=beta)
+                     device=torch.device("cpu"))
     else:
         gp = None
     got = GD.broadcast_fit(gp, spec, 0.01, None, "cpu")
@@ -58,7 +57,7 @@ def _worker(rank, world, port, out_dir):
     xg = torch.stack([torch.linspace(0, 9, m, dtype=torch.float64), torch.linspace(3, -2, m, dtype=torch.float64)], 1)
     lo, hi, mean, var = GD.predict_shard(_fake_predict, xg)
     fm, fv = GD.gather_shards(m, 2, lo, hi, mean, var, "cpu")
-    torch.save({"W": got.W, "alpha": got.alpha, "beta": got.beta, "x": got.x, "n_pad": got.n_pad, "lo": lo, "hi": hi,
+    torch.save({"W": got.W, "alpha": got.alpha, "x": got.x, "n_pad": got.n_pad, "lo": lo, "hi": hi,
                 "mean": fm, "var": fv}, os.path.join(out_dir, f"rank{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
@@ -69,7 +68,6 @@ def test_broadcast_and_shards_world2(tmp_path):
     mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
     r = [torch.load(os.path.join(tmp_path, f"rank{i}.pt"), weights_only=True) for i in range(world)]
     assert torch.equal(r[0]["W"], r[1]["W"]) and torch.equal(r[0]["alpha"], r[1]["alpha"])
-    assert torch.equal(r[0]["beta"], r[1]["beta"])
     assert torch.equal(r[0]["x"], r[1]["x"]) and r[1]["n_pad"] == 128
     assert r[0]["lo"] == 0 and r[0]["hi"] == r[1]["lo"] and r[1]["hi"] == 1000 and r[0]["hi"] % 64 == 0
     m = 1000
