@@ -543,25 +543,43 @@ int gp2d_ozaki_prepare_async(const double* W, int64_t n, int64_t ldw, const gp2d
   return 0;
 }
 
+// ---- zero-slab skipping: K* block flags → per-B-tile slab lists (ozaki_slab_list_kernel)
+static int g_oz_skip = 1;
+// block flags of one chunk: [cp/64 grid blocks][npad/64 training blocks] bytes
+static size_t oz_flag_bytes(int64_t n, int64_t chunk) {
+  const int64_t cp = round_up(chunk < 1 ? 1 : chunk, IBN);
+  return (size_t)round_up((cp / OZ_KS_P) * (n / 2 / OZ_KS_T), 256);
+}
+// slab lists + prefix counts of one chunk (ints)
+static size_t oz_list_bytes(int64_t n, int64_t chunk) {
+  const int64_t nbj = 2 * round_up(chunk < 1 ? 1 : chunk, IBN) / IBN, ks = n / IBK;
+  return sizeof(int) * (size_t)(nbj * ks + nbj * (ks / 4 + 1));
+}
+
 size_t gp2d_predict_ozaki_workspace(int64_t n, int64_t chunk) {
   const int nm = ozaki_nmod_for(n);
   if (nm <= 0) return 0;
   const int64_t cp = round_up(chunk < 1 ? 1 : chunk, IBN);
   const int64_t ncols = 2 * cp;
   return 2 * (size_t)nm * (size_t)n * (size_t)ncols                        // Bres + Cres planes
-         + sizeof(double) * ((size_t)(n / 2 / OZ_KS_T + 1) + (size_t)(n / OZ_CRT_ROWS + 1)) * ncols;
+         + sizeof(double) * ((size_t)(n / 2 / OZ_KS_T + 1) + (size_t)(n / OZ_CRT_ROWS + 1)) * ncols
+         + oz_flag_bytes(n, chunk) + oz_list_bytes(n, chunk);
 }
+
+void gp2d_ozaki_set_skip(int on) { g_oz_skip = on ? 1 : 0; }
 
 // One chunked predict over the m grid points.  K* residue planes come either from the
 // inline ozaki_kstar_kernel (pre == nullptr: planes in the workspace, mean partials Σ α·K*)
-// or from gp2d_ozaki_kstar run earlier (pre: planes per chunk at pre + c·pre_stride; the same
-// kernel then runs mean-only, so the mean is bit-identical to the inline path).
+// or from gp2d_ozaki_kstar run earlier (pre: planes per chunk at pre + c·pre_stride, their
+// block flags pre_flags bytes further; the same kernel then runs mean-only, so the mean is
+// bit-identical to the inline path).  The int8 GEMMs skip the K slabs whose K* tile is all
+// zero (exact: they add nothing); flags → slab lists per chunk in `skip` (oz_list_bytes).
 static int predict_ozaki_impl(const int8_t* wres, const double* rowscale, int nmod, int64_t n,
                               const double* alpha, const double* xtr, int64_t ntr,
                               int64_t ntr_pad, const double* xg, int64_t m, const gp2d_kernel_t* k, int var_mode,
                               double noise, int compute_var, double* mean, double* var, int64_t chunk,
-                              int8_t* bres, uint8_t* cres, double* pm, double* P, const int8_t* pre,
-                              size_t pre_stride, hipStream_t s) {
+                              int8_t* bres, uint8_t* cres, double* pm, double* P, uint8_t* flags, int* skip,
+                              const int8_t* pre, size_t pre_stride, size_t pre_flags, hipStream_t s) {
   OzakiConsts oc;
   GP2D_CHECK(make_ozaki_consts(nmod, k, oc));
   const int nm = oc.nmod;
@@ -579,11 +597,21 @@ static int predict_ozaki_impl(const int8_t* wres, const double* rowscale, int nm
     const int64_t cp = round_up(cv, IBN);   // whole 256-row tiles per component half (B aliasing)
     const int64_t ncols = 2 * cp;
     const int8_t* B = pre ? pre + (size_t)ci * pre_stride : bres;
+    const uint8_t* F = pre ? reinterpret_cast<const uint8_t*>(B) + pre_flags : flags;
     const size_t bplane = (size_t)ncols * n;
+    const bool inline_planes = compute_var && !pre;
     ozaki_kstar_kernel<<<dim3((unsigned)nmseg, (unsigned)(cp / OZ_KS_P)), 256, 0, s>>>(
-        xtr, ntr, ntr_pad, xg + point_dim(k) * c0, cv, cp, vp, alpha, (compute_var && !pre) ? oc : oc_mean_only,
-        bres, pm);
+        xtr, ntr, ntr_pad, xg + point_dim(k) * c0, cv, cp, vp, alpha, inline_planes ? oc : oc_mean_only, bres, pm,
+        inline_planes ? flags : nullptr);
     GP2D_CHECK(check_launch("ozaki_kstar_kernel"));
+    const int nbj = (int)(ncols / IBN), kslabs = (int)(n / IBK);
+    const bool use_skip = compute_var && g_oz_skip && kslabs <= (1 << 20);
+    int* slist = skip;
+    int* scnt = skip + (int64_t)nbj * kslabs;
+    if (use_skip) {
+      ozaki_slab_list_kernel<<<(unsigned)nbj, 64, 0, s>>>(F, (int)(ntr_pad / OZ_KS_T), nbj, kslabs, slist, scnt);
+      GP2D_CHECK(check_launch("ozaki_slab_list_kernel"));
+    }
     if (compute_var) {
       hipEvent_t e0 = nullptr, e1 = nullptr;
       {
@@ -594,7 +622,8 @@ static int predict_ozaki_impl(const int8_t* wres, const double* rowscale, int nm
       for (int l = 0; l < nm; ++l) {
         igemm_nt_mod_kernel<<<ggrid, 512, 0, s>>>(wres + (size_t)l * n * n, B + (size_t)l * bplane,
                                                   cres + (size_t)l * n * ncols, n, (int)n, (int)ncols, (int)n, 1,
-                                                  oc.m[l], oc.inv_m[l], (int)(cp / IBN), (int)(ntr_pad / IBK));
+                                                  oc.m[l], oc.inv_m[l], (int)(cp / IBN), (int)(ntr_pad / IBK),
+                                                  use_skip ? slist : nullptr, use_skip ? scnt : nullptr);
         GP2D_CHECK(check_launch("igemm_nt_mod_kernel"));
       }
       if (e0) {
@@ -640,8 +669,11 @@ int gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int nmod, int
   uint8_t* cres = reinterpret_cast<uint8_t*>(bres + (size_t)nm * n * ncols_max);
   double* pm = reinterpret_cast<double*>(cres + (size_t)nm * n * ncols_max);
   double* P = pm + (size_t)(n / 2 / OZ_KS_T + 1) * ncols_max;
+  uint8_t* flags = reinterpret_cast<uint8_t*>(P + (size_t)(n / OZ_CRT_ROWS + 1) * ncols_max);
+  int* skip = reinterpret_cast<int*>(flags + oz_flag_bytes(n, chunk));
   return predict_ozaki_impl(wres, rowscale, nmod, n, alpha, xtr, ntr, ntr_pad, xg, m, k, var_mode, noise,
-                            compute_var, mean, var, chunk, bres, cres, pm, P, nullptr, 0, S(stream));
+                            compute_var, mean, var, chunk, bres, cres, pm, P, flags, skip, nullptr, 0, 0,
+                            S(stream));
 }
 
 // ---- K* residue planes ahead of the fit (they depend on the points and the kernel only)
@@ -667,7 +699,7 @@ int gp2d_ozaki_nmod_apriori(int64_t n, const gp2d_kernel_t* k, double diag_add) 
 size_t gp2d_ozaki_kstar_bytes(int64_t n, int64_t m, int64_t chunk, int nmod) {
   if (n <= 0 || m <= 0 || chunk <= 0 || nmod <= 0) return 0;
   const int64_t nchunks = (m + chunk - 1) / chunk;
-  return (size_t)nchunks * (size_t)nmod * (size_t)n * (size_t)(2 * round_up(chunk, IBN));
+  return (size_t)nchunks * ((size_t)nmod * (size_t)n * (size_t)(2 * round_up(chunk, IBN)) + oz_flag_bytes(n, chunk));
 }
 
 int gp2d_ozaki_kstar(const double* xtr, int64_t ntr, int64_t ntr_pad, const double* xg, int64_t m,
@@ -686,14 +718,17 @@ int gp2d_ozaki_kstar(const double* xtr, int64_t ntr, int64_t ntr_pad, const doub
   GP2D_CHECK(make_ozaki_consts(nmod, k, oc));
   const VecParams vp = make_vec_params(k);
   const int64_t nmseg = (ntr_pad + OZ_KS_T - 1) / OZ_KS_T;
-  const size_t stride = (size_t)nmod * (size_t)n * (size_t)(2 * round_up(chunk, IBN));
+  const size_t planes = (size_t)nmod * (size_t)n * (size_t)(2 * round_up(chunk, IBN));
+  const size_t stride = planes + oz_flag_bytes(n, chunk);   // chunk: planes, then block flags
   hipStream_t s = S(stream);
   int64_t ci = 0;
   for (int64_t c0 = 0; c0 < m; c0 += chunk, ++ci) {
     const int64_t cv = std::min<int64_t>(chunk, m - c0);
     const int64_t cp = round_up(cv, IBN);
+    int8_t* bc = bres + ci * stride;
     ozaki_kstar_kernel<<<dim3((unsigned)nmseg, (unsigned)(cp / OZ_KS_P)), 256, 0, s>>>(
-        xtr, ntr, ntr_pad, xg + point_dim(k) * c0, cv, cp, vp, nullptr, oc, bres + ci * stride, nullptr);
+        xtr, ntr, ntr_pad, xg + point_dim(k) * c0, cv, cp, vp, nullptr, oc, bc, nullptr,
+        reinterpret_cast<uint8_t*>(bc + planes));
     GP2D_CHECK(check_launch("ozaki_kstar_kernel"));
   }
   return 0;
@@ -703,7 +738,8 @@ size_t gp2d_predict_ozaki_planes_workspace(int64_t n, int64_t chunk) {
   const int nm = ozaki_nmod_for(n);
   if (nm <= 0 || n <= 0) return 0;
   const int64_t ncols = 2 * round_up(chunk < 1 ? 1 : chunk, IBN);
-  return (size_t)nm * (size_t)n * (size_t)ncols + sizeof(double) * ozaki_partials(n) * (size_t)ncols;
+  return (size_t)nm * (size_t)n * (size_t)ncols + sizeof(double) * ozaki_partials(n) * (size_t)ncols +
+         oz_list_bytes(n, chunk);
 }
 
 int gp2d_predict_ozaki_planes(const int8_t* wres, const double* rowscale, int nmod, int64_t n, const double* alpha,
@@ -729,9 +765,20 @@ int gp2d_predict_ozaki_planes(const int8_t* wres, const double* rowscale, int nm
   uint8_t* cres = reinterpret_cast<uint8_t*>(work);
   double* pm = reinterpret_cast<double*>(cres + (size_t)nmod * n * ncols_max);
   double* P = pm + (size_t)std::max<int64_t>(n / 2 / OZ_KS_T + 1, n / OZ_CRT_ROWS + 1) * ncols_max;
-  const size_t stride = (size_t)nmod_b * (size_t)n * (size_t)ncols_max;
+  int* skip = reinterpret_cast<int*>(P + (size_t)(n / OZ_CRT_ROWS + 1) * ncols_max);
+  const size_t planes = (size_t)nmod_b * (size_t)n * (size_t)ncols_max;
+  const size_t stride = planes + oz_flag_bytes(n, chunk);
   return predict_ozaki_impl(wres, rowscale, nmod, n, alpha, xtr, ntr, ntr_pad, xg, m, k, var_mode, noise, 1, mean,
-                            var, chunk, nullptr, cres, pm, P, bres, stride, S(stream));
+                            var, chunk, nullptr, cres, pm, P, nullptr, skip, bres, stride, planes, S(stream));
+}
+
+int gp2d_morton_codes(const double* pts, int64_t n, int dim, double* bbox, int64_t* codes, void* stream) {
+  GP2D_REQUIRE(pts && bbox && codes && n > 0 && (dim == 2 || dim == 3), "morton_codes: bad arguments");
+  hipStream_t s = S(stream);
+  morton_bbox_kernel<<<1, 1024, 0, s>>>(pts, n, dim, bbox);
+  GP2D_CHECK(check_launch("morton_bbox_kernel"));
+  morton_code_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(pts, n, dim, bbox, codes);
+  return check_launch("morton_code_kernel");
 }
 
 // ------------------------------------------------- LOG MARGINAL LIKELIHOOD (§8f.1)

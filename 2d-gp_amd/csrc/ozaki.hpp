@@ -153,7 +153,7 @@ constexpr int OZ_KS_P = 64;   // grid points per block
 __global__ __launch_bounds__(256) void ozaki_kstar_kernel(
     const double* __restrict__ xtr, int64_t ntr, int64_t npad, const double* __restrict__ xg, int64_t cv,
     int64_t cp, VecParams vp, const double* __restrict__ alpha, OzakiConsts oc, int8_t* __restrict__ bres,
-    double* __restrict__ pm) {
+    double* __restrict__ pm, uint8_t* __restrict__ flags) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int kg = lane & 15, r = lane >> 4;
   const int64_t t0 = (int64_t)blockIdx.x * OZ_KS_T + 4 * kg;
@@ -170,6 +170,7 @@ __global__ __launch_bounds__(256) void ozaki_kstar_kernel(
     a2[u] = (alpha != nullptr && t < npad) ? alpha[npad + t] : 0.0;
   }
   const double scale = ldexp(1.0, oc.sB);
+  bool nz = false;   // a nonzero scaled entry in this thread's part of the block
 #pragma unroll 1
   for (int q = 0; q < OZ_KS_P / 16; ++q) {
     const int64_t p = (int64_t)blockIdx.y * OZ_KS_P + 16 * q + 4 * wv + r;
@@ -209,6 +210,7 @@ __global__ __launch_bounds__(256) void ozaki_kstar_kernel(
       xi[0][u] = rint(k11[u] * scale);
       xi[1][u] = rint(k12[u] * scale);
       xi[2][u] = rint(k22[u] * scale);
+      nz = nz || xi[0][u] != 0.0 || xi[1][u] != 0.0 || xi[2][u] != 0.0;
     }
     // (grid comp, train comp): (u,u) → row p, col t ; (u,v) → row p, col npad+t ;
     //                          (v,v) → row cp+p, col npad+t ; (v,u) not stored
@@ -230,6 +232,44 @@ __global__ __launch_bounds__(256) void ozaki_kstar_kernel(
       *reinterpret_cast<uint32_t*>(plane + o_vv) = pk[2];
     }
   }
+  // block flag (grid block by, training block bx): 0 iff every stored residue is zero, so the
+  // int8 GEMM may skip the K slabs of this training block for this grid block
+  if (flags != nullptr) {
+    const int any = __syncthreads_or(nz ? 1 : 0);
+    if (threadIdx.x == 0) flags[(int64_t)blockIdx.y * gridDim.x + blockIdx.x] = any ? 1 : 0;
+  }
+}
+
+// Per 256-row B tile bj: the ascending list of K slabs whose K* tile is not all zero
+// (list[bj][0..]) and cnt[bj][kb] = the number of listed slabs below slab 4·kb (kb ≤ K/256),
+// from the K* kernel's block flags [cp/64][npad/64].  Rows bj < nbj/2 are the u components
+// of grid tile bj, the rest the v components of tile bj − nbj/2; slab s covers training block
+// s mod (npad/64) (u, then v components).  A slab is kept when any of the tile's four 64-point
+// grid blocks has a nonzero entry with that training block (all component pairs share the flag).
+// One wave per tile: ballot + popcount compaction in slab order.
+__global__ __launch_bounds__(64) void ozaki_slab_list_kernel(const uint8_t* __restrict__ flags, int ntb, int nbj,
+                                                             int kslabs, int* __restrict__ list,
+                                                             int* __restrict__ cnt) {
+  const int bj = blockIdx.x, lane = threadIdx.x;
+  const int g = bj % (nbj / 2);
+  const uint8_t* f = flags + (int64_t)(4 * g) * ntb;
+  int* L = list + (int64_t)bj * kslabs;
+  int* C = cnt + (int64_t)bj * (kslabs / 4 + 1);
+  int c = 0;
+  for (int s0 = 0; s0 < kslabs; s0 += 64) {
+    const int sl = s0 + lane;
+    bool keep = false;
+    if (sl < kslabs) {
+      const int tb = sl % ntb;
+      keep = (f[tb] | f[ntb + tb] | f[2 * ntb + tb] | f[3 * ntb + tb]) != 0;
+    }
+    const uint64_t bal = __ballot(keep);
+    const int below = c + __popcll(bal & ((1ull << lane) - 1ull));
+    if (keep) L[below] = sl;
+    if (sl < kslabs && (sl & 3) == 0) C[sl >> 2] = below;
+    c += __popcll(bal);
+  }
+  if (lane == 0) C[kslabs >> 2] = c;
 }
 
 // ------------------------------------------------------------------ INT8 NT GEMM mod m
@@ -290,11 +330,16 @@ __device__ __forceinline__ void vmwait_barrier(std::integral_constant<int, W>) {
 // B tiles (row block rb ≥ alias_rb, k slab s < alias_ks) are read from (rb − alias_rb,
 // s + alias_ks): the K* planes store the (v,u) block only as its equal (u,v) block.
 // alias_rb = INT_MAX disables the aliasing.
+// slist / scnt (optional, ozaki_slab_list_kernel): the K loop of B tile bj runs over the listed
+// slabs only — the others have an all-zero K* tile and add exactly nothing.  A tile whose list
+// is shorter than the ring's prologue (1 or 2 slabs) runs dense.
 __global__ __launch_bounds__(512, 1) void igemm_nt_mod_kernel(const int8_t* __restrict__ A,
                                                               const int8_t* __restrict__ B,
                                                               uint8_t* __restrict__ C, int64_t ldc, int M, int N,
                                                               int K, int a_lower, int modulus, double inv_mod,
-                                                              int alias_rb, int alias_ks) {
+                                                              int alias_rb, int alias_ks,
+                                                              const int* __restrict__ slist,
+                                                              const int* __restrict__ scnt) {
   __shared__ __attribute__((aligned(16))) int8_t smem[I_NSTAGE * I_STAGE];
   const int bj = blockIdx.x;
   const int bi = (int)(gridDim.y - 1 - blockIdx.y);   // heavy (long-K) row blocks first
@@ -308,6 +353,19 @@ __global__ __launch_bounds__(512, 1) void igemm_nt_mod_kernel(const int8_t* __re
   const bool alias = bj >= alias_rb;
   const int8_t* Bp = B + (int64_t)bj * kslabs * I_OP;
   const int8_t* Bq = B + ((int64_t)(alias ? bj - alias_rb : 0) * kslabs + alias_ks) * I_OP;
+#ifdef GP2D_IGEMM_EPI_ONLY
+  int nsl = 0;
+#else
+  int nsl = ke / IBK;
+#endif
+  const int* sl = nullptr;   // slab list of this B tile (nullptr: dense K loop)
+  if (slist != nullptr) {
+    const int c = scnt[(int64_t)bj * (kslabs / 4 + 1) + ke / IBM];
+    if (c == 0 || c >= I_NSTAGE - 1) {
+      nsl = c;
+      sl = slist + (int64_t)bj * kslabs;
+    }
+  }
 
   i4v acc[8][4];
 #pragma unroll
@@ -317,14 +375,15 @@ __global__ __launch_bounds__(512, 1) void igemm_nt_mod_kernel(const int8_t* __re
 
   // wave w moves rows [32w, 32w+32) of both operands: 2 contiguous 1 KB pieces each
   const int drow = lane >> 2, dchunk = lane & 3;
-  auto issue = [&](int s, int st) {
+  // ks: the K slab (already mapped through the list) loaded into ring stage st
+  auto issue = [&](int ks, int st) {
 #ifdef GP2D_IGEMM_NO_DMA
     return;
 #endif
     int8_t* As = smem + st * I_STAGE;
     int8_t* Bs = As + I_OP;
-    const int8_t* Ag = Ap + (int64_t)s * I_OP;
-    const int8_t* Bg = ((alias && s < alias_ks) ? Bq : Bp) + (int64_t)s * I_OP;
+    const int8_t* Ag = Ap + (int64_t)ks * I_OP;
+    const int8_t* Bg = ((alias && ks < alias_ks) ? Bq : Bp) + (int64_t)ks * I_OP;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int row = wid * 32 + h * 16 + drow;
@@ -369,14 +428,15 @@ __global__ __launch_bounds__(512, 1) void igemm_nt_mod_kernel(const int8_t* __re
       for (int ni = 0; ni < 4; ++ni)
         acc[4 * half + u][ni] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[u], b[ni], acc[4 * half + u][ni], 0, 0, 0);
   };
-#ifdef GP2D_IGEMM_EPI_ONLY
-  const int nsl = 0;
-#else
-  const int nsl = ke / IBK;
-#endif
+  // list lookups run one step ahead of their DMA: the load of step s's index is issued during
+  // step s − 1.  Through the constant address space it is a scalar load (s_load, counted by
+  // lgkmcnt); a vector load would need vmcnt(0), which also drains the slabs in flight.
+  typedef const __attribute__((address_space(4))) int* const_int_ptr;
+  auto slab = [&](int s) -> int { return sl ? ((const_int_ptr)sl)[min(s, nsl - 1)] : s; };
   if (nsl > 0) {
 #pragma unroll
-    for (int q = 0; q < I_NSTAGE - 1; ++q) issue(q, q);
+    for (int q = 0; q < I_NSTAGE - 1; ++q) issue(slab(q), q);
+    int knext = slab(I_NSTAGE - 1);
     vmwait_barrier(std::integral_constant<int, I_NSTAGE - 2>{});   // slab 0 landed (nsl ≥ 4 ≥ I_NSTAGE − 1)
     // Per slab: MFMA half 0 (A rows 0-63 of the wave) → barrier publishing slab s+1 → reads
     // of slab s+1's B and A-half-0 fragments into the other register set → MFMA half 1.
@@ -400,7 +460,10 @@ __global__ __launch_bounds__(512, 1) void igemm_nt_mod_kernel(const int8_t* __re
       constexpr int w = decltype(w_c)::value;
       const int st = s % I_NSTAGE;
       // the stage written is slab s−1's: nobody reads it after the previous barrier
-      if constexpr (dma) issue(s + I_NSTAGE - 1, (s + I_NSTAGE - 1) % I_NSTAGE);
+      if constexpr (dma) {
+        issue(knext, (s + I_NSTAGE - 1) % I_NSTAGE);
+        knext = slab(s + I_NSTAGE);
+      }
       reada(st, 1, a1);
       asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");  // b, a0 landed
       __builtin_amdgcn_sched_barrier(0);
@@ -482,6 +545,68 @@ __global__ __launch_bounds__(512, 1) void igemm_nt_mod_kernel(const int8_t* __re
     const uint4 v = *reinterpret_cast<const uint4*>(T + cloc * TP + 16 * ch);
     *reinterpret_cast<uint4*>(C + (int64_t)(j0 + cloc) * ldc + i0 + 16 * ch) = v;
   }
+}
+
+// ------------------------------------------------------------------ Morton order (point sorting)
+// Bounding box of n points (dim 2 or 3): one 1024-thread workgroup, bbox[c] = min, bbox[3+c] = max.
+__global__ __launch_bounds__(1024) void morton_bbox_kernel(const double* __restrict__ P, int64_t n, int dim,
+                                                           double* __restrict__ bbox) {
+  __shared__ double red[2][3][32];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (int64_t i = tid; i < n; i += 1024)
+    for (int c = 0; c < dim; ++c) {
+      const double v = P[i * dim + c];
+      lo[c] = fmin(lo[c], v);
+      hi[c] = fmax(hi[c], v);
+    }
+  for (int c = 0; c < dim; ++c) {
+    for (int o = 32; o > 0; o >>= 1) {
+      lo[c] = fmin(lo[c], __shfl_xor(lo[c], o));
+      hi[c] = fmax(hi[c], __shfl_xor(hi[c], o));
+    }
+    if (lane == 0) { red[0][c][w] = lo[c]; red[1][c][w] = hi[c]; }
+  }
+  __syncthreads();
+  if (tid < dim) {
+    double a = INFINITY, b = -INFINITY;
+    for (int q = 0; q < 16; ++q) { a = fmin(a, red[0][tid][q]); b = fmax(b, red[1][tid][q]); }
+    bbox[tid] = a;
+    bbox[3 + tid] = b;
+  }
+}
+
+__device__ __forceinline__ uint64_t spread2(uint64_t v) {   // 21 bits → every 2nd bit
+  v = (v | (v << 16)) & 0x0000FFFF0000FFFFull;
+  v = (v | (v << 8)) & 0x00FF00FF00FF00FFull;
+  v = (v | (v << 4)) & 0x0F0F0F0F0F0F0F0Full;
+  v = (v | (v << 2)) & 0x3333333333333333ull;
+  return (v | (v << 1)) & 0x5555555555555555ull;
+}
+__device__ __forceinline__ uint64_t spread3(uint64_t v) {   // 21 bits → every 3rd bit
+  v &= 0x1FFFFFull;
+  v = (v | (v << 32)) & 0x001F00000000FFFFull;
+  v = (v | (v << 16)) & 0x001F0000FF0000FFull;
+  v = (v | (v << 8)) & 0x100F00F00F00F00Full;
+  v = (v | (v << 4)) & 0x10C30C30C30C30C3ull;
+  return (v | (v << 2)) & 0x1249249249249249ull;
+}
+
+// Z-order code of each point in its bounding box (21 bits per coordinate).
+__global__ __launch_bounds__(256) void morton_code_kernel(const double* __restrict__ P, int64_t n, int dim,
+                                                          const double* __restrict__ bbox,
+                                                          int64_t* __restrict__ code) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  uint64_t c = 0;
+  for (int k = 0; k < dim; ++k) {
+    const double lo = bbox[k], span = fmax(bbox[3 + k] - lo, 1e-300);
+    double q = rint((P[i * dim + k] - lo) / span * 2097151.0);
+    q = fmin(fmax(q, 0.0), 2097151.0);
+    const uint64_t v = (uint64_t)q;
+    c |= (dim == 2 ? spread2(v) : spread3(v)) << k;
+  }
+  code[i] = (int64_t)c;
 }
 
 // ------------------------------------------------------------------ CRT + column Σ V²

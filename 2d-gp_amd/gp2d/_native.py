@@ -26,7 +26,7 @@ EXPORTS = (
     "gp2d_ozaki_nmod", "gp2d_ozaki_wres_bytes", "gp2d_ozaki_prepare", "gp2d_ozaki_prepare_async",
     "gp2d_predict_ozaki_workspace",
     "gp2d_predict_ozaki", "gp2d_ozaki_nmod_apriori", "gp2d_ozaki_kstar_bytes", "gp2d_ozaki_kstar",
-    "gp2d_predict_ozaki_planes_workspace", "gp2d_predict_ozaki_planes", "gp2d_lml", "gp2d_lml_grad_count",
+    "gp2d_predict_ozaki_planes_workspace", "gp2d_predict_ozaki_planes", "gp2d_ozaki_set_skip", "gp2d_morton_codes", "gp2d_lml", "gp2d_lml_grad_count",
     "gp2d_lml_grad_workspace", "gp2d_lml_grad",
     "gp2d_kernel_grad_count", "gp2d_kernel_grad_workspace", "gp2d_kernel_grad",
     "gp2d_timing_enable", "gp2d_timing_read", "gp2d_last_error",
@@ -90,6 +90,8 @@ _SIGS = {
     "gp2d_predict_ozaki_planes": (_I, [_P, _P, _I, _I64, _P, _P, _I64, _I64, _P, _I64, _KP, _I, _D, _P, _I, _P, _P,
                                        _I64, _P, _SZ, _P]),
     "gp2d_predict_ozaki_workspace": (_SZ, [_I64, _I64]),
+    "gp2d_ozaki_set_skip": (None, [_I]),
+    "gp2d_morton_codes": (_I, [_P, _I64, _I, _P, _P, _P]),
     "gp2d_predict_ozaki": (_I, [_P, _P, _I, _I64, _P, _P, _I64, _I64, _P, _I64, _KP, _I, _D, _I, _P, _P, _I64, _P,
                                 _SZ, _P]),
     "gp2d_lml": (_I, [_P, _I64, _I64, _P, _P, _I64, _P, _P]),

@@ -74,13 +74,14 @@ def packed_blocks(n: int):
 
 
 def fit_sharded(spec: E.KernelSpec, x, y, noise: float, device, mode: str = "bcast", jitter: float = 0.0,
-                variance: str = "f64"):
+                variance: str = "f64", check: bool = True):
     """mode 'bcast': rank 0 fits, factor broadcast over RCCL; 'replicate': every rank
     fits redundantly (no communication).  With variance='ozaki' every rank derives its
-    INT8 residue planes from the broadcast factor locally (no extra traffic)."""
+    INT8 residue planes from the broadcast factor locally (no extra traffic).  check=False as
+    in engine.fit (replicate mode; in bcast mode rank 0 checks before broadcasting)."""
     ws, rank = world()
     if ws == 1 or mode == "replicate":
-        return E.fit(spec, x, y, noise, jitter=jitter, device=device, variance=variance)
+        return E.fit(spec, x, y, noise, jitter=jitter, device=device, variance=variance, check=check)
     gp = E.fit(spec, x, y, noise, jitter=jitter, device=device, variance=variance) if rank == 0 else None
     gp = broadcast_fit(gp, spec, noise, x, device)
     if variance == "ozaki" and "ozaki" not in gp.extra:

@@ -38,6 +38,24 @@ def _require_device(device=None) -> torch.device:
     return torch.device(device if device is not None else "cuda")
 
 
+def morton_order(P: torch.Tensor) -> torch.Tensor:
+    """Permutation that sorts device points (N, d), d ∈ {2, 3}, along a Z-order (Morton) curve
+    of their bounding box (gp2d_morton_codes, 21 bits per coordinate; stable sort, so
+    deterministic).  The ozaki engine orders training and grid points this way so that 64
+    consecutive training points and 256 consecutive grid points are spatially compact: K*
+    tiles of far-apart groups are then exactly zero and the int8 GEMMs skip them
+    (csrc/ozaki.hpp, ozaki_slab_list_kernel)."""
+    n, d = P.shape
+    if n <= 1 or d not in (2, 3):
+        return torch.arange(n, device=P.device)
+    P = P.contiguous()
+    scratch = torch.empty(6, dtype=torch.float64, device=P.device)
+    code = torch.empty(n, dtype=torch.int64, device=P.device)
+    N.check(N.lib().gp2d_morton_codes(_ptr(P), n, d, _ptr(scratch), _ptr(code), _stream_handle(P.device)),
+            "gp2d_morton_codes")
+    return torch.argsort(code, stable=True)
+
+
 def _as_points(x, dim: int, device) -> torch.Tensor:
     if isinstance(x, torch.Tensor):
         t = x.to(device=device, dtype=torch.float64)
@@ -141,6 +159,18 @@ class GPFit:
     info: int = 0
     extra: dict = field(default_factory=dict)
     y: torch.Tensor = None   # (n,) padded observations (LML)
+    perm: torch.Tensor = None  # ozaki engine: x = x_input[perm] (Morton order; α, W follow x)
+    pending: tuple = None      # fit(check=False): (pinned info copy, its event, prepare error)
+
+    def check(self) -> "GPFit":
+        """Raise what fit(check=False) deferred: LinAlgError for a non-SPD K_y (waits only
+        for the factor's info flag, not for later work on the stream)."""
+        if self.pending is not None:
+            info_host, ev, err = self.pending
+            self.pending = None
+            ev.synchronize()
+            _raise_fit_errors(int(info_host.item()), err)
+        return self
 
     @property
     def n(self) -> int:
@@ -178,14 +208,25 @@ def fit_layout(kernel: KernelSpec, n_train: int, variance: str = "f64"):
     return npad, n
 
 
-def fit(kernel: KernelSpec, x, y, noise: float, jitter: float = 0.0, device=None, variance: str = "f64") -> GPFit:
+def _raise_fit_errors(inf: int, err):
+    if inf != 0:
+        raise np.linalg.LinAlgError(
+            f"K_y is not positive definite (leading minor of order {inf}); "
+            "increase the noise / jitter (cf. sklearn _gpr.py:350-358)")
+    if err is not None:
+        raise err
+
+
+def fit(kernel: KernelSpec, x, y, noise: float, jitter: float = 0.0, device=None, variance: str = "f64",
+        check: bool = True) -> GPFit:
     """K_y = K(x,x) + (noise+jitter)·I → L = chol(K_y) → W = L⁻¹ → α = Wᵀ W y.
 
     variance: 'f64'   — predictive variance by the FP64-MFMA contraction;
               'ozaki' — the same contraction emulated exactly on the INT8 matrix cores
                         (Ozaki scheme II, csrc/ozaki.hpp); vector2d family only.
     Raises numpy.linalg.LinAlgError if K_y is not positive definite (the
-    reference's np.linalg.inv / GPy jitchol / sklearn error paths).
+    reference's np.linalg.inv / GPy jitchol / sklearn error paths).  check=False returns
+    without waiting for the factor (no host sync); the error is raised by GPFit.check().
     """
     if variance not in VARIANCE_ENGINES:
         raise ValueError(f"variance must be one of {VARIANCE_ENGINES}")
@@ -199,6 +240,10 @@ def fit(kernel: KernelSpec, x, y, noise: float, jitter: float = 0.0, device=None
     if ntr < 1:
         raise ValueError("need at least one training point")
     npad, n = fit_layout(kernel, ntr, variance)
+    perm = None
+    if variance == "ozaki" and ntr > 1:   # Morton order: exact-zero K* slabs cluster (skipped)
+        perm = morton_order(X)
+        X = X[perm].contiguous()
     s = _stream_handle(dev)
     desc = kernel.desc()
     A = torch.empty((n, n), dtype=torch.float64, device=dev)
@@ -207,6 +252,12 @@ def fit(kernel: KernelSpec, x, y, noise: float, jitter: float = 0.0, device=None
     dinv = torch.empty((n // NB, NB, NB), dtype=torch.float64, device=dev)
     info = torch.zeros(1, dtype=torch.int32, device=dev)
     N.check(L.gp2d_potrf(_ptr(A), n, n, _ptr(dinv), _ptr(info), None, 0, s), "gp2d_potrf")
+    info_host = ev = None
+    if not check:
+        info_host = torch.empty(1, dtype=torch.int32, pin_memory=True)
+        info_host.copy_(info, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(dev))
     # TRTRI and α are enqueued behind POTRF before `info` is read (one host sync per fit,
     # no bubble between the factor and the inverse); a failed factor raises below
     wbytes = int(L.gp2d_trtri_workspace(n))
@@ -214,12 +265,15 @@ def fit(kernel: KernelSpec, x, y, noise: float, jitter: float = 0.0, device=None
     N.check(L.gp2d_trtri(_ptr(A), n, n, _ptr(dinv), _ptr(work), wbytes, s), "gp2d_trtri")
     del work, dinv
     Y = _pad_obs(y, ntr, npad, bd, dev)
+    if perm is not None:
+        for c in range(bd):
+            Y[c * npad:c * npad + ntr] = Y[c * npad:c * npad + ntr][perm]
     alpha = torch.empty(n, dtype=torch.float64, device=dev)
     pbytes = int(L.gp2d_potrs_workspace(n))
     pwork = torch.empty(pbytes // 8 + 1, dtype=torch.float64, device=dev)
     N.check(L.gp2d_potrs_inv(_ptr(A), n, n, _ptr(Y), _ptr(alpha), _ptr(pwork), pbytes, s), "gp2d_potrs_inv")
     gp = GPFit(kernel=kernel, noise=float(noise), x=X, n_train=ntr, n_pad=npad, W=A, alpha=alpha, device=dev,
-               y=Y)
+               y=Y, perm=perm)
     del pwork
     err = None
     if variance == "ozaki":
@@ -229,13 +283,10 @@ def fit(kernel: KernelSpec, x, y, noise: float, jitter: float = 0.0, device=None
             ozaki_prepare(gp, diag_add=float(noise + jitter))
         except N.GP2DError as e:   # a failed factor (NaN rows) makes prepare fail too: info decides
             err = e
-    inf = int(info.item())
-    if inf != 0:
-        raise np.linalg.LinAlgError(
-            f"K_y is not positive definite (leading minor of order {inf}); "
-            "increase the noise / jitter (cf. sklearn _gpr.py:350-358)")
-    if err is not None:
-        raise err
+    if not check:
+        gp.pending = (info_host, ev, err)
+        return gp
+    _raise_fit_errors(int(info.item()), err)
     return gp
 
 
@@ -275,7 +326,8 @@ class KstarPlanes:
     nmod: int
     bres: torch.Tensor
     event: torch.cuda.Event
-    xg: torch.Tensor = None
+    xg: torch.Tensor = None     # the grid in plane order (Morton)
+    order: torch.Tensor = None  # plane row j ↔ input grid point order[j]
 
 
 def kstar_planes(kernel: KernelSpec, x, xg, noise: float, jitter: float = 0.0, chunk: int = 8192, stream=None,
@@ -290,7 +342,10 @@ def kstar_planes(kernel: KernelSpec, x, xg, noise: float, jitter: float = 0.0, c
     L = N.lib()
     d = kernel.input_dim
     X = _as_points(x, d, dev)
+    X = X[morton_order(X)].contiguous()          # the order fit() gives the training points
     G = _as_points(xg, d, dev)
+    order = morton_order(G)
+    G = G[order].contiguous()
     ntr, m = X.shape[0], G.shape[0]
     npad, n = fit_layout(kernel, ntr, "ozaki")
     chunk = max(128, (int(chunk) + 127) // 128 * 128)
@@ -315,7 +370,34 @@ def kstar_planes(kernel: KernelSpec, x, xg, noise: float, jitter: float = 0.0, c
     ev = torch.cuda.Event()
     ev.record(st)
     return KstarPlanes(kernel=kernel, x=X, m=m, n=n, n_pad=npad, chunk=chunk, nmod=nmod, bres=bres, event=ev,
-                       xg=G)
+                       xg=G, order=order)
+
+
+def ozaki_executed_fraction(kernel: KernelSpec, x, xg, noise: float, jitter: float = 0.0, chunk: int = 8192,
+                            device=None) -> float:
+    """Measurement helper (bench.py): the fraction of the dense int8 GEMM work (W lower-
+    triangular, every K slab) the zero-slab skipping executes for this training set and grid —
+    read from the K* block flags gp2d_ozaki_kstar stores after each chunk's planes, with the
+    slab-list rules of ozaki_slab_list_kernel / igemm_nt_mod_kernel."""
+    pl = kstar_planes(kernel, x, xg, noise, jitter, chunk, device=device)
+    pl.event.synchronize()
+    n, ntb, m, ch = pl.n, pl.n_pad // 64, pl.m, pl.chunk
+    cpm = (ch + 255) // 256 * 256
+    planes = pl.nmod * n * 2 * cpm
+    stride = planes + ((cpm // 64) * ntb + 255) // 256 * 256
+    nbi = n // 256
+    ke_slabs = 4 * np.arange(1, nbi + 1)          # a_lower: row block bi reads slabs < 4(bi+1)
+    executed = dense = 0
+    for ci, c0 in enumerate(range(0, m, ch)):
+        cp = (min(ch, m - c0) + 255) // 256 * 256
+        off = ci * stride + planes
+        f = pl.bres[off:off + (cp // 64) * ntb].view(torch.uint8).cpu().numpy().reshape(cp // 256, 4, ntb)
+        kept = np.concatenate([f.any(1)] * 2, axis=1)            # (grid tile, slab): u then v blocks
+        cum = np.cumsum(kept, axis=1)[:, ke_slabs - 1]           # listed slabs below each row block's end
+        run = np.where((cum > 0) & (cum < 3), ke_slabs[None, :], cum)   # 1–2 slabs run dense
+        executed += 2 * int(run.sum())                           # u rows and v rows of each tile
+        dense += 2 * (cp // 256) * int(ke_slabs.sum())
+    return executed / dense if dense else 1.0
 
 
 _VAR_MODES = {"latent": N.VAR_LATENT, "gpy": N.VAR_NOISY, "noisy": N.VAR_NOISY, "sklearn": N.VAR_CLIPPED,
@@ -352,27 +434,41 @@ class Predictor:
         else:
             mean, var = out
         desc = gp.kernel.desc()
-        if planes is not None and compute_var and self.ozaki and "ozaki" in gp.extra:
-            if planes.m != m or planes.n != gp.n or planes.chunk != self.chunk:
-                raise ValueError("K* planes were made for another grid, fit layout or chunk size")
-            wres, rowscale, nmod = gp.extra["ozaki"]
-            s = torch.cuda.current_stream(gp.device)
-            s.wait_event(planes.event)
-            rc = L.gp2d_predict_ozaki_planes(_ptr(wres), _ptr(rowscale), nmod, gp.n, _ptr(gp.alpha), _ptr(gp.x),
-                                             gp.n_train, gp.n_pad, _ptr(G), m, ctypes.byref(desc),
-                                             _VAR_MODES[var_mode], float(gp.noise), _ptr(planes.bres), planes.nmod,
-                                             _ptr(mean), _ptr(var), self.chunk, _ptr(self.work), self.wbytes,
-                                             ctypes.c_void_p(s.cuda_stream))
-            if rc != -3:   # −3: the fit needs more moduli than the planes carry → inline K* below
-                N.check(rc, "gp2d_predict_ozaki_planes")
-                return mean, var
         if self.ozaki and "ozaki" in gp.extra:
             wres, rowscale, nmod = gp.extra["ozaki"]
-            N.check(L.gp2d_predict_ozaki(_ptr(wres), _ptr(rowscale), nmod, gp.n, _ptr(gp.alpha), _ptr(gp.x), gp.n_train,
-                                         gp.n_pad, _ptr(G), m, ctypes.byref(desc), _VAR_MODES[var_mode],
-                                         float(gp.noise), int(bool(compute_var)), _ptr(mean), _ptr(var), self.chunk,
-                                         _ptr(self.work), self.wbytes, _stream_handle(gp.device)),
-                    "gp2d_predict_ozaki")
+            use_planes = planes is not None and compute_var
+            if use_planes and (planes.m != m or planes.n != gp.n or planes.chunk != self.chunk):
+                raise ValueError("K* planes were made for another grid, fit layout or chunk size")
+            # the variance runs on the grid in Morton order (zero K* tiles cluster and are
+            # skipped); every output point is independent of the others, so reordering
+            # changes no bits — the results are scattered back to the input order
+            order = None
+            Gs, ms, vs = G, mean, var
+            if compute_var and m > 1:
+                order = planes.order if use_planes else morton_order(G)
+                Gs = planes.xg if use_planes else G[order].contiguous()
+                ms = torch.empty(bd * m, dtype=torch.float64, device=gp.device)
+                vs = torch.empty(bd * m, dtype=torch.float64, device=gp.device)
+            rc = -3
+            if use_planes:
+                s = torch.cuda.current_stream(gp.device)
+                s.wait_event(planes.event)
+                rc = L.gp2d_predict_ozaki_planes(_ptr(wres), _ptr(rowscale), nmod, gp.n, _ptr(gp.alpha), _ptr(gp.x),
+                                                 gp.n_train, gp.n_pad, _ptr(Gs), m, ctypes.byref(desc),
+                                                 _VAR_MODES[var_mode], float(gp.noise), _ptr(planes.bres),
+                                                 planes.nmod, _ptr(ms), _ptr(vs), self.chunk, _ptr(self.work),
+                                                 self.wbytes, ctypes.c_void_p(s.cuda_stream))
+                if rc != -3:   # −3: the fit needs more moduli than the planes carry → inline K*
+                    N.check(rc, "gp2d_predict_ozaki_planes")
+            if rc == -3:
+                N.check(L.gp2d_predict_ozaki(_ptr(wres), _ptr(rowscale), nmod, gp.n, _ptr(gp.alpha), _ptr(gp.x),
+                                             gp.n_train, gp.n_pad, _ptr(Gs), m, ctypes.byref(desc),
+                                             _VAR_MODES[var_mode], float(gp.noise), int(bool(compute_var)),
+                                             _ptr(ms), _ptr(vs), self.chunk, _ptr(self.work), self.wbytes,
+                                             _stream_handle(gp.device)), "gp2d_predict_ozaki")
+            if order is not None:
+                mean.view(bd, m)[:, order] = ms.view(bd, m)
+                var.view(bd, m)[:, order] = vs.view(bd, m)
             return mean, (var if compute_var else None)
         N.check(L.gp2d_predict(_ptr(gp.W), gp.n, gp.n, _ptr(gp.alpha), _ptr(gp.x), gp.n_train, gp.n_pad,
                                _ptr(G), m, ctypes.byref(desc), _VAR_MODES[var_mode], float(gp.noise),

@@ -199,6 +199,8 @@ class Krig:
         if with_factor:
             d["W"] = _to_numpy(self.gp.W)
             d["alpha"] = _to_numpy(self.gp.alpha)
+            if self.gp.perm is not None:   # W and α follow the training points in X[perm] order
+                d["perm"] = _to_numpy(self.gp.perm)
         np.savez(path, **d)
 
     @classmethod

@@ -144,6 +144,14 @@ int    gp2d_ozaki_prepare_async(const double* W, int64_t n, int64_t ldw, const g
                                 double diag_add, int8_t* wres, double* rowscale, int* nmod_out,
                                 void* stream);
 size_t gp2d_predict_ozaki_workspace(int64_t n, int64_t chunk);
+/* The variance GEMMs skip K slabs (64 training components) whose K* tile is exactly zero for
+ * a 256-row grid tile — exact, such slabs add nothing.  gp2d_ozaki_set_skip(0) runs them
+ * dense (A/B measurement and the bit-identity test); default on.                       */
+void   gp2d_ozaki_set_skip(int on);
+/* Z-order (Morton) codes of n points (dim 2 or 3) in their bounding box, 21 bits per
+ * coordinate (bbox: 6 doubles of device scratch).  The ozaki engine sorts training and grid
+ * points by these codes so that all-zero K* tiles cluster into skippable slabs.          */
+int    gp2d_morton_codes(const double* pts, int64_t n, int dim, double* bbox, int64_t* codes, void* stream);
 int    gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int nmod, int64_t n,
                           const double* alpha, const double* xtr, int64_t ntr, int64_t ntr_pad,
                           const double* xg, int64_t m, const gp2d_kernel_t* k,
@@ -155,8 +163,9 @@ int    gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int nmod, 
  * fit (e.g. while a rank waits for the factor broadcast):
  * gp2d_ozaki_nmod_apriori: a moduli count that bounds gp2d_ozaki_prepare's data-driven one
  *   for any fit of this kernel with diagonal K_y,ii = kdiag + diag_add (−1 on bad input);
- * gp2d_ozaki_kstar: the planes of every chunk of the m grid points (nmod planes per chunk,
- *   chunk c at bres + c·nmod·n·2·⌈chunk/256⌉·256 bytes; size gp2d_ozaki_kstar_bytes);
+ * gp2d_ozaki_kstar: the planes of every chunk of the m grid points (per chunk: nmod planes
+ *   of n·2·⌈chunk/256⌉·256 bytes, then the K* block flags the GEMMs' zero-slab skipping
+ *   reads; size gp2d_ozaki_kstar_bytes);
  * gp2d_predict_ozaki_planes: gp2d_predict_ozaki (compute_var = 1) with the variance GEMMs
  *   reading those planes; the mean K*α is evaluated in fp64 as in gp2d_predict_ozaki, so
  *   both outputs are bit-identical to it.  Returns −3 if the fit needs more moduli than

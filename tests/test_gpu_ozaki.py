@@ -200,3 +200,58 @@ def test_async_prepare_matches_data_driven(kind, l, noise):
     assert rel(va, vd) < 1e-12 and rel(ma, md) < 1e-13
     mo, vo = O.fit_predict(x, y, xg, kind=kind, l_df=l, l_cf=l * 1.2, ratio=ks.ratio, noise=noise)
     assert rel(va, vo) < 1e-10 and rel(ma, mo) < 1e-10
+
+
+# ---------------------------------------------------------------- zero-slab skipping
+# The ozaki engine orders training and grid points along a Morton curve; K* tiles between
+# far-apart groups are then exactly zero and the int8 GEMMs skip those K slabs.  Skipping
+# must be exact (bit-identical to the dense K loop) and match the oracle.
+@pytest.mark.parametrize("kind,l", [("df", 3.0), ("mixed", 4.0)])
+def test_zero_slab_skip_is_exact(kind, l):
+    rng = np.random.default_rng(31)
+    n, m = 1500, 5000
+    x = np.stack([rng.uniform(0, 150, n), rng.uniform(0, 120, n)], 1)     # wide domain: ≫ 8ℓ
+    y = np.concatenate([np.sin(x[:, 1] / 17), np.cos(x[:, 0] / 23)]) + rng.normal(0, 0.05, 2 * n)
+    xg = np.stack([rng.uniform(-5, 155, m), rng.uniform(-5, 125, m)], 1)
+    ks = E.KernelSpec(kind=kind, l_df=l, l_cf=l * 1.2, ratio=0.5 if kind == "mixed" else 1.0)
+    gp = E.fit(ks, x, y, noise=0.0025, variance="ozaki")
+    L = E.N.lib()
+    try:
+        L.gp2d_ozaki_set_skip(0)
+        md, vd = (t.cpu().numpy() for t in E.predict(gp, xg, chunk=1024))
+    finally:
+        L.gp2d_ozaki_set_skip(1)
+    ms, vs = (t.cpu().numpy() for t in E.predict(gp, xg, chunk=1024))
+    assert np.array_equal(ms, md) and np.array_equal(vs, vd)
+    # the wide domain (≫ 8ℓ) leaves many K* tiles exactly zero: the GEMMs skip a good part of the work
+    frac = E.ozaki_executed_fraction(ks, x, xg, 0.0025, chunk=1024)
+    assert 0.0 < frac < 0.8
+    sub = np.random.default_rng(2).choice(m, 300, replace=False)
+    mo, vo = O.fit_predict(x, y, xg[sub], kind=kind, l_df=l, l_cf=l * 1.2, ratio=ks.ratio, noise=0.0025)
+    idx = np.concatenate([sub, m + sub])
+    assert rel(vs[idx], vo) < 1e-10 and rel(ms[idx], mo) < 1e-10
+
+
+def test_zero_slab_skip_far_grid_and_planes():
+    """A grid block far from every observation: every K slab is skipped (empty list), so the
+    variance is exactly the prior kss and the mean exactly 0; the K*-planes-ahead path (block
+    flags travel with the planes) gives the same bits."""
+    rng = np.random.default_rng(41)
+    n = 700
+    x = np.stack([rng.uniform(0, 60, n), rng.uniform(0, 45, n)], 1)
+    y = np.concatenate([np.sin(x[:, 1] / 7), np.cos(x[:, 0] / 9)]) + rng.normal(0, 0.05, 2 * n)
+    near = np.stack([rng.uniform(0, 60, 900), rng.uniform(0, 45, 900)], 1)
+    far = np.stack([rng.uniform(900, 960, 700), rng.uniform(900, 945, 700)], 1)
+    xg = np.concatenate([near, far])
+    ks = E.KernelSpec(kind="df", l_df=5.0)
+    gp = E.fit(ks, x, y, noise=0.0025, variance="ozaki")
+    mu, var = (t.cpu().numpy() for t in E.predict(gp, xg, chunk=512))
+    M = xg.shape[0]
+    kss = float(E.N.lib().gp2d_kernel_diag(__import__("ctypes").byref(ks.desc())))
+    far_idx = np.concatenate([np.arange(900, M), M + np.arange(900, M)])
+    assert np.all(var[far_idx] == kss) and np.all(mu[far_idx] == 0.0)
+    _, planes, ma, va = _ahead(ks, x, y, xg, 0.0025, 512)
+    assert np.array_equal(ma, mu) and np.array_equal(va, var)
+    mo, vo = O.fit_predict(x, y, near[:200], kind="df", l_df=5.0, noise=0.0025)
+    idx = np.concatenate([np.arange(200), M + np.arange(200)])
+    assert rel(var[idx], vo) < 1e-10 and rel(mu[idx], mo) < 1e-10

@@ -127,6 +127,13 @@ def test_not_positive_definite_raises(variance):
     x = np.zeros((3, 2))  # three identical points, no noise: singular K
     with pytest.raises(np.linalg.LinAlgError):
         E.fit(E.KernelSpec(kind="df", l_df=1.0), x, np.zeros(6), noise=-1e-3, variance=variance)
+    # deferred form (bench.py): fit returns at once, GPFit.check() raises the same error
+    gp = E.fit(E.KernelSpec(kind="df", l_df=1.0), x, np.zeros(6), noise=-1e-3, variance=variance, check=False)
+    with pytest.raises(np.linalg.LinAlgError):
+        gp.check()
+    ok = E.fit(E.KernelSpec(kind="df", l_df=1.0), tracks(40, seed=1)[0], tracks(40, seed=1)[1], noise=0.01,
+               variance=variance, check=False)
+    assert ok.check() is ok and ok.pending is None
 
 
 def test_sharded_predict_bit_identical():

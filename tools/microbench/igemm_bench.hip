@@ -12,6 +12,10 @@ namespace gp2d { void set_error(const std::string&) {} }
 using namespace gp2d;
 #ifndef IGEMM_KERNEL
 #define IGEMM_KERNEL igemm_nt_mod_kernel
+#define IGEMM_EXTRA , nullptr, nullptr   // dense K loop (no slab list)
+#endif
+#ifndef IGEMM_EXTRA
+#define IGEMM_EXTRA
 #endif
 int main() {
   const int n = 8192, nc = 16384, mod = 251;
@@ -31,7 +35,7 @@ int main() {
   (void)hipMemcpy(dB, Bb.data(), B.size(), hipMemcpyHostToDevice);
   hipEvent_t e0, e1; (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
   const dim3 g(nc / IBN, n / IBM);
-  auto launch = [&]() { IGEMM_KERNEL<<<g, 512>>>(dA, dB, dC, n, n, nc, n, 1, mod, 1.0 / mod, 1 << 30, 0); };
+  auto launch = [&]() { IGEMM_KERNEL<<<g, 512>>>(dA, dB, dC, n, n, nc, n, 1, mod, 1.0 / mod, 1 << 30, 0 IGEMM_EXTRA); };
   for (int w = 0; w < 3; ++w) launch();
   (void)hipDeviceSynchronize();
   (void)hipEventRecord(e0);
