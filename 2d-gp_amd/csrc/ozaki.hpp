@@ -147,10 +147,13 @@ __global__ __launch_bounds__(256) void ozaki_w_res_kernel(const double* __restri
 // training components, slab-blocked) and mean partials pm[bx][j] = Σ_{k in block} α_k·K*_jk
 // (16-lane shuffle reduction in a fixed order).  alpha == nullptr: planes only; oc.nmod == 0:
 // mean only (the planes were built earlier by gp2d_ozaki_kstar).
+#ifndef GP2D_KS_OCC
+#define GP2D_KS_OCC 4   // min workgroups per CU for ozaki_kstar_kernel: 4 waves/SIMD (48 VGPRs spill, still 12 % faster than 2)
+#endif
 constexpr int OZ_KS_T = 64;   // training points per block
 constexpr int OZ_KS_P = 64;   // grid points per block
 
-__global__ __launch_bounds__(256) void ozaki_kstar_kernel(
+__global__ __launch_bounds__(256, GP2D_KS_OCC) void ozaki_kstar_kernel(
     const double* __restrict__ xtr, int64_t ntr, int64_t npad, const double* __restrict__ xg, int64_t cv,
     int64_t cp, VecParams vp, const double* __restrict__ alpha, OzakiConsts oc, int8_t* __restrict__ bres,
     double* __restrict__ pm, uint8_t* __restrict__ flags) {
