@@ -200,32 +200,34 @@ namespace {
 // at every split)
 struct FactorStreams {
   std::mutex mu;
-  std::vector<hipStream_t> crit, bulk;   // indexed by device
+  std::vector<hipStream_t> crit, bulk, aux;   // indexed by device
   std::vector<std::vector<hipEvent_t>> ev;
 };
 FactorStreams g_fs;
 
-int factor_streams(hipStream_t* crit, hipStream_t* bulk, std::vector<hipEvent_t>** evs) {
+int factor_streams(hipStream_t* crit, hipStream_t* bulk, hipStream_t* aux, std::vector<hipEvent_t>** evs) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) { set_error("hipGetDevice failed"); return -1; }
   std::lock_guard<std::mutex> lk(g_fs.mu);
   if ((int)g_fs.crit.size() <= dev) {
-    g_fs.crit.resize(dev + 1, nullptr); g_fs.bulk.resize(dev + 1, nullptr);
+    g_fs.crit.resize(dev + 1, nullptr); g_fs.bulk.resize(dev + 1, nullptr); g_fs.aux.resize(dev + 1, nullptr);
     g_fs.ev.resize(dev + 1);
   }
   if (!g_fs.crit[dev]) {
     int lo = 0, hi = 0;
     if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) { lo = 0; hi = 0; }
     if (hipStreamCreateWithPriority(&g_fs.crit[dev], hipStreamNonBlocking, hi) != hipSuccess ||
-        hipStreamCreateWithPriority(&g_fs.bulk[dev], hipStreamNonBlocking, lo) != hipSuccess) {
+        hipStreamCreateWithPriority(&g_fs.bulk[dev], hipStreamNonBlocking, lo) != hipSuccess ||
+        hipStreamCreateWithPriority(&g_fs.aux[dev], hipStreamNonBlocking, hi) != hipSuccess) {
       set_error("hipStreamCreate failed"); return -1;
     }
-    g_fs.ev[dev].resize(3);
+    g_fs.ev[dev].resize(5);
     for (auto& e : g_fs.ev[dev])
       if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) { set_error("hipEventCreate failed"); return -1; }
   }
   *crit = g_fs.crit[dev];
   *bulk = g_fs.bulk[dev];
+  *aux = g_fs.aux[dev];
   *evs = &g_fs.ev[dev];
   return 0;
 }
@@ -257,19 +259,19 @@ int gp2d_potrf(double* A, int64_t n, int64_t lda, double* dinv, int* info_dev, v
   GP2D_REQUIRE(dinv != nullptr, "potrf: dinv buffer is required");
   hipStream_t s = S(stream);
   const int nb = (int)(n / NB);
-  hipStream_t sc, sb;
+  hipStream_t sc, sb, sa;
   std::vector<hipEvent_t>* ev;
-  GP2D_CHECK(factor_streams(&sc, &sb, &ev));
-  hipEvent_t e_pan = (*ev)[0], e_syrk = (*ev)[1], e_join = (*ev)[2];
+  GP2D_CHECK(factor_streams(&sc, &sb, &sa, &ev));
+  hipEvent_t e_pan = (*ev)[0], e_syrk = (*ev)[1], e_join = (*ev)[2], e_start = (*ev)[3], e_aux = (*ev)[4];
   GP2D_EV(hipEventRecord(e_join, s));
   GP2D_EV(hipStreamWaitEvent(sc, e_join, 0));
   GP2D_EV(hipStreamWaitEvent(sb, e_join, 0));
   // A[j.., j] −= L[j.., p] · L[j, p]ᵀ: block column j receives panel p (skinny K = 128 GEMM,
   // B = the NB rows of block j of the panel)
-  auto colupdate = [&](int j, int p) -> int {
+  auto colupdate = [&](int j, int p, hipStream_t st) -> int {
     const int64_t j0 = (int64_t)j * NB;
     const double* Lp = A + j0 * lda + (int64_t)p * NB;
-    gemm_f64_panel_kernel<<<(unsigned)((n - j0) / PNL_R), 256, 0, sc>>>(Lp, lda, Lp, lda, A + j0 * lda + j0, lda,
+    gemm_f64_panel_kernel<<<(unsigned)((n - j0) / PNL_R), 256, 0, st>>>(Lp, lda, Lp, lda, A + j0 * lda + j0, lda,
                                                                          -1.0, 1.0);
     return check_launch("gemm_f64_panel_kernel");
   };
@@ -283,11 +285,17 @@ int gp2d_potrf(double* A, int64_t n, int64_t lda, double* dinv, int* info_dev, v
   // Delayed trailing updates: panels are consumed in pairs, so the bulk SYRK runs with K = 256
   // (half the launches and half the C read/write traffic per flop of K = 128 updates).  Per
   // pair (k, k+1), block column k+2 gets both panels through two skinny updates on crit and
-  // columns ≥ k+3 get them through one SYRK on bulk.
+  // columns ≥ k+3 get them through one SYRK on bulk.  Block column k+2's update by panel k
+  // needs neither panel k+1 nor its factor, so it runs on `aux` under factor(k+1)'s
+  // single-workgroup diagonal kernel instead of after it.
   int k = 0;
   while (k + 1 < nb) {
     if (k + 2 < nb) {
-      GP2D_CHECK(colupdate(k + 1, k));   // columns ≤ k+1 of earlier panels arrived by earlier SYRKs
+      GP2D_EV(hipEventRecord(e_start, sc));   // panel k final, earlier SYRKs into column k+2 done
+      GP2D_EV(hipStreamWaitEvent(sa, e_start, 0));
+      GP2D_CHECK(colupdate(k + 2, k, sa));
+      GP2D_EV(hipEventRecord(e_aux, sa));
+      GP2D_CHECK(colupdate(k + 1, k, sc));   // columns ≤ k+1 of earlier panels arrived by earlier SYRKs
       GP2D_CHECK(factor(k + 1));
       GP2D_EV(hipEventRecord(e_pan, sc));   // panels k, k+1 done
       GP2D_EV(hipStreamWaitEvent(sb, e_pan, 0));
@@ -302,14 +310,14 @@ int gp2d_potrf(double* A, int64_t n, int64_t lda, double* dinv, int* info_dev, v
         GP2D_CHECK((launch_gemm<true, EPI_STORE>(q, 1, sb)));
       }
       GP2D_EV(hipEventRecord(e_syrk, sb));
-      GP2D_CHECK(colupdate(k + 2, k));
-      GP2D_CHECK(colupdate(k + 2, k + 1));
+      GP2D_EV(hipStreamWaitEvent(sc, e_aux, 0));
+      GP2D_CHECK(colupdate(k + 2, k + 1, sc));
       GP2D_CHECK(factor(k + 2));
       // block column k+3 must have received this pair's SYRK before crit updates it
       GP2D_EV(hipStreamWaitEvent(sc, e_syrk, 0));
       k += 2;
     } else {   // last block column: only panel k is outstanding
-      GP2D_CHECK(colupdate(k + 1, k));
+      GP2D_CHECK(colupdate(k + 1, k, sc));
       GP2D_CHECK(factor(k + 1));
       k += 1;
     }
