@@ -169,7 +169,9 @@ class GPFit:
             info_host, ev, err = self.pending
             self.pending = None
             ev.synchronize()
-            _raise_fit_errors(int(info_host.item()), err)
+            inf = int(info_host.item())
+            _PINNED_INFO.append(info_host)
+            _raise_fit_errors(inf, err)
         return self
 
     @property
@@ -206,6 +208,11 @@ def fit_layout(kernel: KernelSpec, n_train: int, variance: str = "f64"):
         npad = (npad + 127) // 128 * 128
         n = bd * npad
     return npad, n
+
+
+# pinned 1-int slots for fit(check=False)'s info copies, reused after GPFit.check() (a fresh
+# pinned allocation per fit can stall on the device)
+_PINNED_INFO: list = []
 
 
 def _raise_fit_errors(inf: int, err):
@@ -254,7 +261,7 @@ def fit(kernel: KernelSpec, x, y, noise: float, jitter: float = 0.0, device=None
     N.check(L.gp2d_potrf(_ptr(A), n, n, _ptr(dinv), _ptr(info), None, 0, s), "gp2d_potrf")
     info_host = ev = None
     if not check:
-        info_host = torch.empty(1, dtype=torch.int32, pin_memory=True)
+        info_host = _PINNED_INFO.pop() if _PINNED_INFO else torch.empty(1, dtype=torch.int32, pin_memory=True)
         info_host.copy_(info, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(dev))

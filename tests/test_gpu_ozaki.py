@@ -255,3 +255,23 @@ def test_zero_slab_skip_far_grid_and_planes():
     mo, vo = O.fit_predict(x, y, near[:200], kind="df", l_df=5.0, noise=0.0025)
     idx = np.concatenate([np.arange(200), M + np.arange(200)])
     assert rel(var[idx], vo) < 1e-10 and rel(mu[idx], mo) < 1e-10
+
+
+def test_morton_training_order_is_consistent():
+    """The ozaki fit stores the training points in Morton order (GPFit.perm): x = x_in[perm],
+    α follows it, and order-invariant quantities (LML, predictions) match the f64 fit."""
+    x, y = tracks(500, 61)
+    ks = E.KernelSpec(kind="df", l_df=5.0)
+    go = E.fit(ks, x, y, noise=0.0025, variance="ozaki")
+    gf = E.fit(ks, x, y, noise=0.0025)
+    perm = go.perm.cpu().numpy()
+    assert np.array_equal(np.sort(perm), np.arange(500)) and not np.array_equal(perm, np.arange(500))
+    assert np.array_equal(go.x.cpu().numpy(), x[perm])
+    a_o = go.alpha.cpu().numpy()
+    a_f = gf.alpha.cpu().numpy()
+    npad = go.n_pad
+    for c in range(2):   # α of the reordered fit, component c, back in input order
+        back = np.empty(500)
+        back[perm] = a_o[c * npad:c * npad + 500]
+        assert rel(back, a_f[c * gf.n_pad:c * gf.n_pad + 500]) < 1e-9
+    assert abs(E.log_marginal_likelihood(go) - E.log_marginal_likelihood(gf)) < 1e-9 * abs(E.log_marginal_likelihood(gf))
