@@ -43,9 +43,10 @@ def parse():
     ap.add_argument("--grid", type=int, default=256)
     ap.add_argument("--kind", default="df")
     ap.add_argument("--chunk", type=int, default=8192)
-    ap.add_argument("--fit-mode", default="auto", choices=["auto", "bcast", "replicate"],
-                    help="N>1: rank 0 fits and W goes out by RCCL broadcast (bcast), every rank fits "
-                         "(replicate), or whichever of the two the warmup measured faster (auto)")
+    ap.add_argument("--fit-mode", default="replicate", choices=["auto", "bcast", "replicate"],
+                    help="N>1: every rank fits, no data-path collective (replicate, default); rank 0 "
+                         "fits and W goes out by RCCL broadcast (bcast); or whichever of the two the "
+                         "warmup measured faster (auto)")
     ap.add_argument("--variance", default="ozaki", choices=["ozaki", "f64"],
                     help="variance contraction: exact INT8 Ozaki-II emulation (default) or FP64 MFMA")
     ap.add_argument("--kstar-ahead", type=int, default=-1,
