@@ -148,7 +148,7 @@ __global__ __launch_bounds__(256) void ozaki_w_res_kernel(const double* __restri
 // (16-lane shuffle reduction in a fixed order).  alpha == nullptr: planes only; oc.nmod == 0:
 // mean only (the planes were built earlier by gp2d_ozaki_kstar).
 #ifndef GP2D_KS_OCC
-#define GP2D_KS_OCC 4   // min workgroups per CU for ozaki_kstar_kernel: 4 waves/SIMD (48 VGPRs spill, still 12 % faster than 2)
+#define GP2D_KS_OCC 4   // min workgroups per CU for ozaki_kstar_kernel: 4 waves/SIMD (44 VGPRs spill, still faster than 2)
 #endif
 constexpr int OZ_KS_T = 64;   // training points per block
 constexpr int OZ_KS_P = 64;   // grid points per block
