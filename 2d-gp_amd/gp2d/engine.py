@@ -210,8 +210,8 @@ def fit_layout(kernel: KernelSpec, n_train: int, variance: str = "f64"):
     return npad, n
 
 
-# pinned 1-int slots for fit(check=False)'s info copies, reused after GPFit.check() (a fresh
-# pinned allocation per fit can stall on the device)
+# pinned 1-int slots for fit(check=False)'s info copies, reused after GPFit.check(), so the
+# steady state allocates no pinned memory
 _PINNED_INFO: list = []
 
 
