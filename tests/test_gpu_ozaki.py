@@ -275,3 +275,31 @@ def test_morton_training_order_is_consistent():
         back[perm] = a_o[c * npad:c * npad + 500]
         assert rel(back, a_f[c * gf.n_pad:c * gf.n_pad + 500]) < 1e-9
     assert abs(E.log_marginal_likelihood(go) - E.log_marginal_likelihood(gf)) < 1e-9 * abs(E.log_marginal_likelihood(gf))
+
+
+def test_zero_slab_skip_spatiotemporal_exact():
+    """3-D (T, Y, X) points: Morton order over all three coordinates; skip on/off bit-identical
+    and the oracle gate, with far-in-time grid points exactly at the prior."""
+    rng = np.random.default_rng(71)
+    n, m = 600, 1500
+    x = np.stack([rng.uniform(0, 48, n), rng.uniform(0, 45, n), rng.uniform(0, 60, n)], 1)
+    y = np.concatenate([np.sin(x[:, 1] / 7), np.cos(x[:, 2] / 9)]) + rng.normal(0, 0.05, 2 * n)
+    xg = np.stack([rng.uniform(0, 48, m), rng.uniform(-5, 50, m), rng.uniform(-5, 65, m)], 1)
+    xg[-300:, 0] += 5000.0                       # far in time: K* = 0 through the temporal factor
+    ks = E.KernelSpec(family="vector_st", kind="mixed", l_df=5.0, l_cf=4.0, ratio=0.5, var_t=1.3, l_t=12.0)
+    gp = E.fit(ks, x, y, noise=0.0025, variance="ozaki")
+    L = E.N.lib()
+    try:
+        L.gp2d_ozaki_set_skip(0)
+        md, vd = (t.cpu().numpy() for t in E.predict(gp, xg, chunk=512))
+    finally:
+        L.gp2d_ozaki_set_skip(1)
+    ms, vs = (t.cpu().numpy() for t in E.predict(gp, xg, chunk=512))
+    assert np.array_equal(ms, md) and np.array_equal(vs, vd)
+    kss = float(L.gp2d_kernel_diag(__import__("ctypes").byref(ks.desc())))
+    far = np.concatenate([np.arange(m - 300, m), m + np.arange(m - 300, m)])
+    assert np.all(vs[far] == kss) and np.all(ms[far] == 0.0)
+    mo, vo = O.st_fit_predict(x, y, xg[:400], kind="mixed", l_df=5.0, l_cf=4.0, ratio=0.5, var_t=1.3, l_t=12.0,
+                              noise=0.0025)
+    idx = np.concatenate([np.arange(400), m + np.arange(400)])
+    assert rel(vs[idx], vo) < 1e-10 and rel(ms[idx], mo) < 1e-10
