@@ -140,31 +140,44 @@ __global__ __launch_bounds__(256) void ozaki_w_res_kernel(const double* __restri
 
 // ------------------------------------------------------------------ K*ᵀ residues + mean
 // Block: 64 training points × 64 grid points (4 waves).  Lane l covers training points
-// t = 64·bx + 4·(l&15) .. +3 and, in iteration q < 4, grid point p = 64·by + 16q + 4·wave + (l>>4).
-// One wave-wide store per (modulus, entry) then writes 4 consecutive rows × 64 B of one slab
-// tile — 256 contiguous bytes (the slab-blocked layout puts rows of a 256-row tile 64 B
-// apart).  Writes the residue planes Bres[l] (rows j = grid components, columns k =
-// training components, slab-blocked) and mean partials pm[bx][j] = Σ_{k in block} α_k·K*_jk
-// (16-lane shuffle reduction in a fixed order).  alpha == nullptr: planes only; oc.nmod == 0:
-// mean only (the planes were built earlier by gp2d_ozaki_kstar).
+// t = 64·bx + OZ_KS_PPL·(l mod LG) .. + OZ_KS_PPL − 1 (LG = 64 / OZ_KS_PPL lanes per grid row)
+// and, in iteration q, grid point p = 64·by + RPI·q + RPW·wave + l / LG (RPW = 64 / LG rows per
+// wave, RPI = 4·RPW rows per iteration).  One wave-wide store per (modulus, entry) then writes
+// RPW consecutive rows × 64 B of one slab tile — contiguous bytes (the slab-blocked layout
+// puts rows of a 256-row tile 64 B apart).  Writes the residue planes Bres[l] (rows j = grid
+// components, columns k = training components, slab-blocked) and mean partials
+// pm[bx][j] = Σ_{k in block} α_k·K*_jk (LG-lane shuffle reduction in a fixed order).
+// alpha == nullptr: planes only; oc.nmod == 0: mean only (the planes were built earlier by
+// gp2d_ozaki_kstar).
 #ifndef GP2D_KS_OCC
-#define GP2D_KS_OCC 4   // min workgroups per CU for ozaki_kstar_kernel: 4 waves/SIMD (44 VGPRs spill, still faster than 2)
+#define GP2D_KS_OCC 5   // min workgroups per CU for ozaki_kstar_kernel: 5 waves per SIMD (102 VGPRs)
+#endif
+#ifndef GP2D_KS_PPL
+#define GP2D_KS_PPL 2   // training points per lane (4: 44 VGPRs spill at 4 waves per SIMD, 3 % slower)
 #endif
 constexpr int OZ_KS_T = 64;   // training points per block
 constexpr int OZ_KS_P = 64;   // grid points per block
+constexpr int OZ_KS_PPL = GP2D_KS_PPL;
+static_assert(OZ_KS_PPL == 2 || OZ_KS_PPL == 4, "2 or 4 training points per lane");
+
+template <int PPL> struct packed_bytes;   // PPL residue bytes of one lane, stored at once
+template <> struct packed_bytes<2> { typedef uint16_t type; };
+template <> struct packed_bytes<4> { typedef uint32_t type; };
 
 __global__ __launch_bounds__(256, GP2D_KS_OCC) void ozaki_kstar_kernel(
     const double* __restrict__ xtr, int64_t ntr, int64_t npad, const double* __restrict__ xg, int64_t cv,
     int64_t cp, VecParams vp, const double* __restrict__ alpha, OzakiConsts oc, int8_t* __restrict__ bres,
     double* __restrict__ pm, uint8_t* __restrict__ flags) {
+  constexpr int PPL = OZ_KS_PPL, LG = 64 / PPL, RPW = 64 / LG, RPI = 4 * RPW;
+  typedef typename packed_bytes<PPL>::type pk_t;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int kg = lane & 15, r = lane >> 4;
-  const int64_t t0 = (int64_t)blockIdx.x * OZ_KS_T + 4 * kg;
+  const int kg = lane % LG, r = lane / LG;
+  const int64_t t0 = (int64_t)blockIdx.x * OZ_KS_T + PPL * kg;
   const int64_t n = 2 * npad, ncols = 2 * cp;
-  double a1[4], a2[4], x0[4], x1[4], x2[4];
-  bool tv[4];
+  double a1[PPL], a2[PPL], x0[PPL], x1[PPL], x2[PPL];
+  bool tv[PPL];
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
+  for (int u = 0; u < PPL; ++u) {
     const int64_t t = t0 + u;
     tv[u] = t < ntr;
     x0[u] = x1[u] = x2[u] = 0.0;
@@ -175,15 +188,15 @@ __global__ __launch_bounds__(256, GP2D_KS_OCC) void ozaki_kstar_kernel(
   const double scale = ldexp(1.0, oc.sB);
   bool nz = false;   // a nonzero scaled entry in this thread's part of the block
 #pragma unroll 1
-  for (int q = 0; q < OZ_KS_P / 16; ++q) {
-    const int64_t p = (int64_t)blockIdx.y * OZ_KS_P + 16 * q + 4 * wv + r;
+  for (int q = 0; q < OZ_KS_P / RPI; ++q) {
+    const int64_t p = (int64_t)blockIdx.y * OZ_KS_P + RPI * q + RPW * wv + r;
     const bool pv = p < cv;
     double g0 = 0.0, g1 = 0.0, g2 = 0.0;
     if (pv) vec_point(vp, xg, p, g0, g1, g2);
-    double k11[4], k12[4], k22[4];
+    double k11[PPL], k12[PPL], k22[PPL];
     double mu = 0.0, mv = 0.0;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < PPL; ++u) {
       if (pv && tv[u]) {
         vec_block_st(vp, x0[u] - g0, x1[u] - g1, x2[u] - g2, k11[u], k12[u], k22[u]);
       } else {
@@ -193,9 +206,9 @@ __global__ __launch_bounds__(256, GP2D_KS_OCC) void ozaki_kstar_kernel(
       mv += a1[u] * k12[u] + a2[u] * k22[u];   // row j = cp + p (v component)
     }
     if (pm != nullptr) {
-      // fixed-order reduction over the 16 lanes of this grid point (this block's 64 points)
+      // fixed-order reduction over the LG lanes of this grid point (this block's 64 points)
 #pragma unroll
-      for (int o = 8; o > 0; o >>= 1) {
+      for (int o = LG / 2; o > 0; o >>= 1) {
         mu += __shfl_xor(mu, o);
         mv += __shfl_xor(mv, o);
       }
@@ -204,12 +217,12 @@ __global__ __launch_bounds__(256, GP2D_KS_OCC) void ozaki_kstar_kernel(
         pm[(int64_t)blockIdx.x * ncols + cp + p] = mv;
       }
     }
-    if (p >= cp || t0 >= npad) continue;   // npad is a multiple of 64: whole 4-point groups
+    if (p >= cp || t0 >= npad) continue;   // npad is a multiple of 64: whole point groups
     // The (v,u) block equals the (u,v) block (k12 is symmetric in the 2×2 kernel block), so
     // only (u,u), (u,v) and (v,v) are stored: the GEMM reads (v,u) tiles from (u,v).
-    double xi[3][4];  // [entry: (u,u) (u,v) (v,v)][u]
+    double xi[3][PPL];  // [entry: (u,u) (u,v) (v,v)][u]
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < PPL; ++u) {
       xi[0][u] = rint(k11[u] * scale);
       xi[1][u] = rint(k12[u] * scale);
       xi[2][u] = rint(k22[u] * scale);
@@ -221,18 +234,18 @@ __global__ __launch_bounds__(256, GP2D_KS_OCC) void ozaki_kstar_kernel(
                   o_vv = slab_offset(cp + p, npad + t0, n);
     for (int l = 0; l < oc.nmod; ++l) {
       const double m = (double)oc.m[l], im = oc.inv_m[l];
-      uint32_t pk[3];
+      pk_t pk[3];
 #pragma unroll
       for (int e = 0; e < 3; ++e) {
         uint32_t w = 0;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) w |= residue_byte(xi[e][u], m, im) << (8 * u);   // |xi| < 2^pB
-        pk[e] = w;
+        for (int u = 0; u < PPL; ++u) w |= residue_byte(xi[e][u], m, im) << (8 * u);   // |xi| < 2^pB
+        pk[e] = (pk_t)w;
       }
       int8_t* plane = bres + (int64_t)l * ncols * n;
-      *reinterpret_cast<uint32_t*>(plane + o_uu) = pk[0];
-      *reinterpret_cast<uint32_t*>(plane + o_uv) = pk[1];
-      *reinterpret_cast<uint32_t*>(plane + o_vv) = pk[2];
+      *reinterpret_cast<pk_t*>(plane + o_uu) = pk[0];
+      *reinterpret_cast<pk_t*>(plane + o_uv) = pk[1];
+      *reinterpret_cast<pk_t*>(plane + o_vv) = pk[2];
     }
   }
   // block flag (grid block by, training block bx): 0 iff every stored residue is zero, so the
