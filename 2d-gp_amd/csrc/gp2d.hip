@@ -70,6 +70,18 @@ static int validate_kernel(const gp2d_kernel_t* k) {
   return 0;
 }
 
+// The Ozaki engine's scale bound |K*| ≤ max(1/ℓ_df², 1/ℓ_cf²) and its CRT range check
+// (|V| ≤ 4√kss) hold for the mixed kernel only when ratio ∈ [0, 1] (a convex combination of
+// the two parts; kss > 0).  GP_laser's free `rate` outside that range is still accepted by the
+// FP64 engine; the Ozaki entry points reject it.
+static int validate_ozaki_kernel(const gp2d_kernel_t* k) {
+  GP2D_CHECK(validate_kernel(k));
+  GP2D_REQUIRE(is_vector_family(k), "ozaki: vector families only");
+  if (k->kind == GP2D_KIND_MIXED)
+    GP2D_REQUIRE(k->ratio >= 0.0 && k->ratio <= 1.0, "ozaki: mixed-kernel ratio must be in [0, 1]");
+  return 0;
+}
+
 static int assemble_impl(const double* xa, int64_t na, int64_t na_pad, const double* xb, int64_t nb,
                          int64_t nb_pad, const gp2d_kernel_t* k, double diag_add, int symmetric, double* out,
                          int64_t ld, hipStream_t s) {
@@ -485,8 +497,7 @@ size_t gp2d_ozaki_wres_bytes(int64_t n) {
 
 int gp2d_ozaki_prepare(const double* W, int64_t n, int64_t ldw, const gp2d_kernel_t* k, int8_t* wres,
                        double* rowscale, int* nmod_out, void* stream) {
-  GP2D_CHECK(validate_kernel(k));
-  GP2D_REQUIRE(is_vector_family(k), "ozaki: vector families only");
+  GP2D_CHECK(validate_ozaki_kernel(k));
   GP2D_REQUIRE(n % IBM == 0 && n > 0, "ozaki: n must be a positive multiple of 256");
   GP2D_REQUIRE(nmod_out != nullptr, "ozaki: nmod_out is NULL");
   hipStream_t s = S(stream);
@@ -531,8 +542,7 @@ int gp2d_ozaki_prepare(const double* W, int64_t n, int64_t ldw, const gp2d_kerne
 
 int gp2d_ozaki_prepare_async(const double* W, int64_t n, int64_t ldw, const gp2d_kernel_t* k, double diag_add,
                              int8_t* wres, double* rowscale, int* nmod_out, void* stream) {
-  GP2D_CHECK(validate_kernel(k));
-  GP2D_REQUIRE(is_vector_family(k), "ozaki: vector families only");
+  GP2D_CHECK(validate_ozaki_kernel(k));
   GP2D_REQUIRE(n % IBM == 0 && n > 0, "ozaki: n must be a positive multiple of 256");
   GP2D_REQUIRE(nmod_out != nullptr, "ozaki: nmod_out is NULL");
   // the a-priori count bounds the data-driven one for any fit with this K_y diagonal (no host
@@ -663,8 +673,7 @@ int gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int nmod, int
                        int64_t ntr, int64_t ntr_pad, const double* xg, int64_t m, const gp2d_kernel_t* k,
                        int var_mode, double noise, int compute_var, double* mean, double* var, int64_t chunk,
                        void* work, size_t work_bytes, void* stream) {
-  GP2D_CHECK(validate_kernel(k));
-  GP2D_REQUIRE(is_vector_family(k), "ozaki: vector families only");
+  GP2D_CHECK(validate_ozaki_kernel(k));
   GP2D_REQUIRE(n == 2 * ntr_pad && n % IBM == 0, "ozaki: n must equal 2·ntr_pad and be a multiple of 256");
   GP2D_REQUIRE(chunk > 0 && chunk % (IBN / 2) == 0, "ozaki: chunk must be a positive multiple of 128");
   GP2D_REQUIRE(work != nullptr && work_bytes >= gp2d_predict_ozaki_workspace(n, chunk), "ozaki: workspace too small");
@@ -691,7 +700,7 @@ int gp2d_ozaki_nmod_apriori(int64_t n, const gp2d_kernel_t* k, double diag_add) 
   // and s_i = p−1−⌊log2 max|W_i|⌋ ≤ s_max.  (1 − 2^-40) absorbs the rounding of L_ii; the
   // identity rows of padded points take bound (a) = 1.01·2^{2p−2}.  prepare's data-driven
   // count never exceeds this one.
-  if (validate_kernel(k) != 0 || !is_vector_family(k) || n <= 0) return -1;
+  if (validate_ozaki_kernel(k) != 0 || n <= 0) return -1;
   const double kss = gp2d_kernel_diag(k);
   const double dmin = (1.0 - std::ldexp(1.0, -40)) / std::sqrt(kss + diag_add);
   const int smax = OZ_PW - 1 - (int)std::floor(std::log2(dmin));
@@ -713,8 +722,7 @@ size_t gp2d_ozaki_kstar_bytes(int64_t n, int64_t m, int64_t chunk, int nmod) {
 int gp2d_ozaki_kstar(const double* xtr, int64_t ntr, int64_t ntr_pad, const double* xg, int64_t m,
                      const gp2d_kernel_t* k, int nmod, int64_t chunk, int8_t* bres, size_t bres_bytes,
                      void* stream) {
-  GP2D_CHECK(validate_kernel(k));
-  GP2D_REQUIRE(is_vector_family(k), "ozaki: vector families only");
+  GP2D_CHECK(validate_ozaki_kernel(k));
   const int64_t n = 2 * ntr_pad;
   GP2D_REQUIRE(ntr_pad > 0 && n % IBM == 0 && ntr <= ntr_pad, "ozaki_kstar: 2·ntr_pad must be a multiple of 256");
   GP2D_REQUIRE(chunk > 0 && chunk % (IBN / 2) == 0, "ozaki_kstar: chunk must be a positive multiple of 128");
@@ -755,8 +763,7 @@ int gp2d_predict_ozaki_planes(const int8_t* wres, const double* rowscale, int nm
                               const gp2d_kernel_t* k, int var_mode, double noise, const int8_t* bres, int nmod_b,
                               double* mean, double* var, int64_t chunk, void* work, size_t work_bytes,
                               void* stream) {
-  GP2D_CHECK(validate_kernel(k));
-  GP2D_REQUIRE(is_vector_family(k), "ozaki: vector families only");
+  GP2D_CHECK(validate_ozaki_kernel(k));
   GP2D_REQUIRE(n == 2 * ntr_pad && n % IBM == 0, "ozaki: n must equal 2·ntr_pad and be a multiple of 256");
   GP2D_REQUIRE(chunk > 0 && chunk % (IBN / 2) == 0, "ozaki: chunk must be a positive multiple of 128");
   GP2D_REQUIRE(work != nullptr && work_bytes >= gp2d_predict_ozaki_planes_workspace(n, chunk),
@@ -913,6 +920,31 @@ int gp2d_kernel_grad(const double* xa, int64_t na, const double* xb, int64_t nb,
 }
 
 // ------------------------------------------------------------------ instrumentation
+// ---- dense helpers of the GP_scripts functional API (getMean / getCov on explicit matrices)
+int gp2d_gemm(int transb, int64_t m, int64_t n, int64_t k, double alpha, const double* A, int64_t lda,
+              const double* B, int64_t ldb, double beta, double* C, int64_t ldc, void* stream) {
+  GP2D_REQUIRE(A && B && C, "gemm: NULL argument");
+  GP2D_REQUIRE(m % NB == 0 && n % NB == 0 && k % 16 == 0 && m >= 0 && n >= 0 && k >= 0,
+               "gemm: m, n must be multiples of 128 and k of 16");
+  GP2D_REQUIRE(lda >= k && ldc >= n && ldb >= (transb ? k : n), "gemm: leading dimensions too small");
+  GP2D_REQUIRE(m <= INT32_MAX && n <= INT32_MAX && k <= INT32_MAX, "gemm: sizes exceed int32");
+  GemmParams p = gemm_params();
+  p.A = A; p.lda = lda;
+  p.B = B; p.ldb = ldb;
+  p.C = C; p.ldc = ldc;
+  p.M = (int)m; p.N = (int)n; p.K = (int)k;
+  p.alpha = alpha; p.beta = beta;   // k = 0: C = beta·C (the K loop runs no slab)
+  return transb ? launch_gemm<true, EPI_STORE>(p, 1, S(stream)) : launch_gemm<false, EPI_STORE>(p, 1, S(stream));
+}
+
+int gp2d_transpose(const double* A, int64_t n, int64_t lda, double* At, void* stream) {
+  GP2D_REQUIRE(A && At, "transpose: NULL argument");
+  GP2D_REQUIRE(n % 64 == 0 && n >= 0 && lda >= n, "transpose: n must be a multiple of 64, lda >= n");
+  if (n == 0) return 0;
+  transpose_kernel<<<dim3((unsigned)(n / 64), (unsigned)(n / 64)), 256, 0, S(stream)>>>(A, n, lda, At);
+  return check_launch("transpose_kernel");
+}
+
 void gp2d_timing_enable(int on) {
   std::lock_guard<std::mutex> lk(g_timing.mu);
   g_timing.on = (on != 0);

@@ -555,6 +555,81 @@ def kernel_grad(kernel: KernelSpec, xa, dL_dK, xb=None, device=None) -> np.ndarr
     return g.cpu().numpy()
 
 
+# ------------------------------------------------------------------ dense helpers
+def _as_matrix(a, device) -> torch.Tensor:
+    if isinstance(a, torch.Tensor):
+        t = a.to(device=device, dtype=torch.float64)
+    else:
+        t = torch.as_tensor(np.ascontiguousarray(np.asarray(a, dtype=np.float64)), device=device)
+    return t.reshape(t.shape[0], -1) if t.dim() != 2 else t
+
+
+def _padded(t: torch.Tensor, rows: int, cols: int) -> torch.Tensor:
+    if tuple(t.shape) == (rows, cols) and t.is_contiguous():
+        return t
+    out = torch.zeros((rows, cols), dtype=torch.float64, device=t.device)
+    out[:t.shape[0], :t.shape[1]] = t
+    return out
+
+
+def _up(v: int, m: int) -> int:
+    return max(m, (v + m - 1) // m * m)
+
+
+def gemm(A, B, transb: bool = False, alpha: float = 1.0, C=None, beta: float = 0.0, device=None) -> torch.Tensor:
+    """alpha·A·op(B) + beta·C on the FP64 MFMA GEMM core (gp2d_gemm); op(B) = Bᵀ if transb.
+    Operands of any shape are zero-padded to the kernel's 128/128/16 tiles (the padding adds
+    exact zeros to every sum).  The dense product of GP_scripts.getMean / getCov."""
+    dev = _require_device(device)
+    A = _as_matrix(A, dev)
+    B = _as_matrix(B, dev)
+    m, k = A.shape
+    n = B.shape[0] if transb else B.shape[1]
+    if (B.shape[1] if transb else B.shape[0]) != k:
+        raise ValueError(f"gemm: inner dimensions differ ({tuple(A.shape)} x {tuple(B.shape)}, transb={transb})")
+    mp, np_, kp = _up(m, NB), _up(n, NB), _up(k, 16)
+    Ap = _padded(A, mp, kp)
+    Bp = _padded(B, np_, kp) if transb else _padded(B, kp, np_)
+    Cp = torch.zeros((mp, np_), dtype=torch.float64, device=dev)
+    if C is not None and beta != 0.0:
+        Cp[:m, :n] = _as_matrix(C, dev)
+    N.check(N.lib().gp2d_gemm(int(bool(transb)), mp, np_, kp, float(alpha), _ptr(Ap), kp, _ptr(Bp), Bp.shape[1],
+                              float(beta), _ptr(Cp), np_, _stream_handle(dev)), "gp2d_gemm")
+    return Cp[:m, :n]
+
+
+def spd_inverse(K, device=None, return_factor: bool = False):
+    """K⁻¹ of a symmetric positive-definite matrix through the engine's factor:
+    L = chol(K) (gp2d_potrf), W = L⁻¹ (gp2d_trtri), K⁻¹ = WᵀW (gp2d_transpose + gp2d_gemm).
+    Stands in for np.linalg.inv(K) (GP_scripts.py:50, GP_laser.py:118) on the matrices those
+    call sites build; raises numpy.linalg.LinAlgError when K is not positive definite (where
+    np.linalg.inv raises only for an exactly singular K).  K is padded to a multiple of 128
+    with an identity block, which the block-diagonal inverse leaves decoupled."""
+    dev = _require_device(device)
+    K = _as_matrix(K, dev)
+    n0 = K.shape[0]
+    if K.shape[1] != n0:
+        raise ValueError("spd_inverse: K must be square")
+    L = N.lib()
+    n = _up(n0, NB)
+    A = torch.eye(n, dtype=torch.float64, device=dev)
+    A[:n0, :n0] = K
+    s = _stream_handle(dev)
+    dinv = torch.empty((n // NB, NB, NB), dtype=torch.float64, device=dev)
+    info = torch.zeros(1, dtype=torch.int32, device=dev)
+    N.check(L.gp2d_potrf(_ptr(A), n, n, _ptr(dinv), _ptr(info), None, 0, s), "gp2d_potrf")
+    wbytes = int(L.gp2d_trtri_workspace(n))
+    work = torch.empty(wbytes // 8 + 1, dtype=torch.float64, device=dev)
+    N.check(L.gp2d_trtri(_ptr(A), n, n, _ptr(dinv), _ptr(work), wbytes, s), "gp2d_trtri")
+    _raise_fit_errors(int(info.item()), None)
+    Wt = torch.empty((n, n), dtype=torch.float64, device=dev)
+    N.check(L.gp2d_transpose(_ptr(A), n, n, _ptr(Wt), s), "gp2d_transpose")
+    Ki = torch.empty((n, n), dtype=torch.float64, device=dev)
+    N.check(L.gp2d_gemm(1, n, n, n, 1.0, _ptr(Wt), n, _ptr(Wt), n, 0.0, _ptr(Ki), n, s), "gp2d_gemm")
+    Ki = Ki[:n0, :n0]
+    return (Ki, A[:n0, :n0]) if return_factor else Ki
+
+
 def timing_enable(on: bool = True):
     N.lib().gp2d_timing_enable(int(bool(on)))
 

@@ -5,10 +5,10 @@ Mirrors
     myKernel.py:12-57), ``nonDivK`` (div-free, :148-180), ``nonRotK`` (curl-free,
     :244-275) — constructor arguments, parameter names, ``K(X, X2)`` and
     ``Kdiag(X)``;
-  * the functional API of GP_scripts.py: ``myKernel`` (:6-42), ``nonDivK`` (:57-69),
-    ``compute_K`` (:74-95), ``compute_Ks`` (:97-123).  ``getMean``/``getCov`` on explicit
-    matrices (:44-54) are replaced by ``krig.Krig.predict`` (mean fused with the
-    K* generation, variance from the inverse Cholesky factor).
+  * the functional API of GP_scripts.py under the module's own names lives in
+    ``2d-gp_amd/GP_scripts.py`` (``myKernel``, ``getMean``, ``getCov``, ``nonDivK``,
+    ``compute_K``, ``compute_Ks``, ``sqExp``, ``rbf``); the helpers below (``vector_K``,
+    ``compute_K``, ``compute_Ks``, ``nonDivK_block``) are kept for existing callers.
 
 GPy itself is not a dependency: the classes expose the same methods and
 parameters without the paramz machinery.  Parameters are floats carrying a

@@ -82,8 +82,11 @@ class Krig:
 
     def __init__(self, kernel="df", l_df: float = 5.0, l_cf: float = 5.0, ratio: float = None,
                  noise: float = 0.0025, jitter: float = 0.0, var_mode: str = "latent", device=None,
-                 chunk: int = 8192):
+                 chunk: int = 8192, variance: str = "f64"):
         self.spec = self._make_spec(kernel, l_df, l_cf, ratio)
+        if variance not in E.VARIANCE_ENGINES:
+            raise ValueError(f"variance must be one of {E.VARIANCE_ENGINES}")
+        self.variance = variance
         self.noise = float(noise)
         self.jitter = float(jitter)
         self.var_mode = var_mode
@@ -114,7 +117,8 @@ class Krig:
         y = obs if isinstance(obs, torch.Tensor) else np.asarray(obs, dtype=np.float64)
         if bd == 2 and not isinstance(y, torch.Tensor) and y.ndim == 2 and y.shape[1] == 2:
             y = np.concatenate([y[:, 0], y[:, 1]])
-        self.gp = E.fit(self.spec, X, y, self.noise, jitter=self.jitter, device=self.device)
+        self.gp = E.fit(self.spec, X, y, self.noise, jitter=self.jitter, device=self.device,
+                        variance=self.variance)
         self._pred = E.Predictor(self.gp, self.chunk)
         self._X, self._y = X, y
         return self
@@ -195,7 +199,7 @@ class Krig:
                  l_cf=s.l_cf, ratio=s.ratio, variances=np.asarray(s.variances, dtype=np.float64),
                  lengthscales=np.asarray(s.lengthscales, dtype=np.float64), var_t=s.var_t, l_t=s.l_t,
                  noise=self.noise, jitter=self.jitter,
-                 var_mode=self.var_mode)
+                 var_mode=self.var_mode, variance=self.variance, chunk=self.chunk)
         if with_factor:
             d["W"] = _to_numpy(self.gp.W)
             d["alpha"] = _to_numpy(self.gp.alpha)
@@ -205,6 +209,11 @@ class Krig:
 
     @classmethod
     def load(cls, path: str, device=None, refit: bool = True):
+        """Restore a checkpoint written by save(): GPy.load / pickle.load of a fitted model
+        (krig.py:478-483).  A checkpoint with the factor (save(with_factor=True)) is restored
+        without refitting — W, α and the training order go back to the device as saved, so
+        predictions are bit-identical to the saved model's; without it the model is refitted
+        from the stored inputs (refit=False then returns an unfitted model)."""
         z = np.load(path, allow_pickle=False)
         fam = str(z["family"])
         if fam == "ard":
@@ -214,11 +223,44 @@ class Krig:
             st = dict(var_t=float(z["var_t"]), l_t=float(z["l_t"])) if "var_t" in z.files else {}
             spec = E.KernelSpec(family=fam, kind=str(z["kind"]), l_df=float(z["l_df"]), l_cf=float(z["l_cf"]),
                                 ratio=float(z["ratio"]), **st)
+        extra = {}
+        if "variance" in z.files:
+            extra = dict(variance=str(z["variance"]), chunk=int(z["chunk"]))
         k = cls(spec, noise=float(z["noise"]), jitter=float(z["jitter"]), var_mode=str(z["var_mode"]),
-                device=device)
-        if refit:
+                device=device, **extra)
+        if "W" in z.files:
+            k._restore(z["X"], z["y"], z["W"], z["alpha"], z["perm"] if "perm" in z.files else None)
+        elif refit:
             k.fit(z["X"], z["y"])
         return k
+
+    def _restore(self, X, y, W, alpha, perm):
+        """Rebuild the device fit from a saved factor (no assembly, no factorisation)."""
+        dev = E._require_device(self.device)
+        spec = self.spec
+        bd, d = spec.block_dim, spec.input_dim
+        Xd = torch.as_tensor(np.ascontiguousarray(np.asarray(X, dtype=np.float64).reshape(-1, d)), device=dev)
+        ntr = Xd.shape[0]
+        npad, n = E.fit_layout(spec, ntr, self.variance)
+        if W.shape != (n, n) or alpha.shape != (n,):
+            raise ValueError(f"saved factor has shape {W.shape}, the fit layout needs ({n}, {n})")
+        pm = None
+        if perm is not None:
+            pm = torch.as_tensor(np.asarray(perm, dtype=np.int64), device=dev)
+            Xd = Xd[pm].contiguous()
+        Y = E._pad_obs(y, ntr, npad, bd, dev)
+        if pm is not None:
+            for c in range(bd):
+                Y[c * npad:c * npad + ntr] = Y[c * npad:c * npad + ntr][pm]
+        gp = E.GPFit(kernel=spec, noise=self.noise, x=Xd, n_train=ntr, n_pad=npad,
+                     W=torch.as_tensor(np.ascontiguousarray(W), device=dev),
+                     alpha=torch.as_tensor(np.ascontiguousarray(alpha), device=dev), device=dev, y=Y, perm=pm)
+        if self.variance == "ozaki":
+            E.ozaki_prepare(gp, diag_add=self.noise + self.jitter)
+        self.gp = gp
+        self._pred = E.Predictor(gp, self.chunk)
+        self._X, self._y = X, y
+        return self
 
 
 # ===================================================================== module functions

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define GP2D_ABI_VERSION 2
+#define GP2D_ABI_VERSION 3
 
 /* kernel families */
 #define GP2D_FAMILY_VECTOR2D 0   /* 2×2 matrix-valued SE kernels on (x1, x2)          */
@@ -127,7 +127,7 @@ int gp2d_predict(const double* W, int64_t n, int64_t ldw, const double* alpha,
 /* ---- predict, FP64-accurate variance on the INT8 matrix cores (Ozaki scheme II) -----
  * Same results contract as gp2d_predict (1e-10 relative parity gate) for the vector2d
  * family; the variance contraction ‖W k*‖² runs as nmod exact int8 GEMMs
- * (v_mfma_i32_32x32x32_i8) on residues modulo pairwise-coprime m_l ≤ 256, followed by
+ * (v_mfma_i32_16x16x64_i8) on residues modulo pairwise-coprime m_l ≤ 256, followed by
  * a Chinese-remainder reconstruction in fp64.  Requires n % 256 == 0.
  * gp2d_ozaki_prepare: once per fit, W → residue planes wres (≤ gp2d_ozaki_wres_bytes(n)
  * bytes) and per-row scales rowscale (n doubles); *nmod_out receives the number of moduli
@@ -216,6 +216,17 @@ size_t gp2d_kernel_grad_workspace(int64_t na, int64_t nb);
 int    gp2d_kernel_grad(const double* xa, int64_t na, const double* xb, int64_t nb,
                         const gp2d_kernel_t* k, const double* dL_dK, int64_t ld,
                         double* grad_dev, void* work, size_t work_bytes, void* stream);
+
+/* ---- dense helpers (the GP_scripts functional API on explicit matrices) ------------
+ * gp2d_gemm: C = alpha·A·op(B) + beta·C on the FP64 MFMA GEMM core; op(B) = B (transb = 0,
+ *   B is k×n) or Bᵀ (transb = 1, B is n×k); row-major; m, n multiples of 128, k of 16 (the
+ *   Python layer pads).  Replaces the np.dot chains of GP_scripts.getMean (GP_scripts.py:44-46)
+ *   and getCov (GP_scripts.py:48-54, Ks·Ki·Ksᵀ).
+ * gp2d_transpose: At = Aᵀ for an n×n matrix (n a multiple of 64, At with leading dim n).
+ *   Forms K⁻¹ = WᵀW from W = L⁻¹ in place of np.linalg.inv (GP_scripts.py:50).           */
+int gp2d_gemm(int transb, int64_t m, int64_t n, int64_t k, double alpha, const double* A, int64_t lda,
+              const double* B, int64_t ldb, double beta, double* C, int64_t ldc, void* stream);
+int gp2d_transpose(const double* A, int64_t n, int64_t lda, double* At, void* stream);
 
 /* ---- instrumentation ------------------------------------------------------------
  * When enabled, every launch of the predict variance kernel (the dominant

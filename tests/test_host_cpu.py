@@ -24,7 +24,7 @@ def test_library_exports_every_header_symbol():
     for s in syms:
         assert hasattr(L, s), s
     assert set(syms) == set(_native.EXPORTS)
-    assert L.gp2d_abi_version() == _native.ABI_VERSION == 2
+    assert L.gp2d_abi_version() == _native.ABI_VERSION == 3
     assert L.gp2d_padded_points(1) == 64 and L.gp2d_padded_points(64) == 64 and L.gp2d_padded_points(65) == 128
 
 
@@ -50,6 +50,28 @@ def test_argument_errors_are_reported():
     assert rc < 0 and b"l_df" in L.gp2d_last_error()
     rc = L.gp2d_potrf(None, 100, 100, None, None, None, 0, None)
     assert rc < 0 and b"multiple of 128" in L.gp2d_last_error()
+    one = ctypes.c_void_p(1)   # never dereferenced: the argument checks fail first
+    rc = L.gp2d_gemm(0, 100, 128, 16, 1.0, one, 16, one, 128, 0.0, one, 128, None)
+    assert rc < 0 and b"multiples of 128" in L.gp2d_last_error()
+    rc = L.gp2d_transpose(one, 100, 100, one, None)
+    assert rc < 0 and b"multiple of 64" in L.gp2d_last_error()
+
+
+def test_ozaki_rejects_ratio_outside_unit_interval():
+    """The Ozaki scale bound and CRT range check assume a convex mixed kernel:
+    ratio outside [0, 1] is refused by every ozaki entry point, before any device work."""
+    import ctypes
+    from gp2d import _native as N
+    L = N.lib()
+    for r in (-0.25, 1.5):
+        k = N.vector_kernel_desc(N.KIND_MIXED, 5.0, 5.0, r)
+        assert L.gp2d_ozaki_nmod_apriori(8192, ctypes.byref(k), 0.0025) == -1
+        nm = ctypes.c_int(0)
+        one = ctypes.c_void_p(1)
+        rc = L.gp2d_ozaki_prepare_async(one, 512, 512, ctypes.byref(k), 0.0025, one, one, ctypes.byref(nm), None)
+        assert rc < 0 and b"ratio" in L.gp2d_last_error()
+    k = N.vector_kernel_desc(N.KIND_MIXED, 5.0, 5.0, 0.5)
+    assert L.gp2d_ozaki_nmod_apriori(8192, ctypes.byref(k), 0.0025) > 0
 
 
 def test_no_cpu_fallback():
