@@ -23,17 +23,32 @@ def world():
     return 1, 0
 
 
-def broadcast_fit(gp: E.GPFit | None, spec: E.KernelSpec, noise: float, x, device, src: int = 0) -> E.GPFit:
+def broadcast_fit(gp: E.GPFit | None, spec: E.KernelSpec, noise: float, x, device, src: int = 0,
+                  error: Exception | None = None) -> E.GPFit:
     """Broadcast W, α and the training points from `src` to every rank (RCCL
-    ncclBroadcast under the 'nccl' backend).  Ranks other than `src` pass gp=None."""
+    ncclBroadcast under the 'nccl' backend).  Ranks other than `src` pass gp=None.
+    If the fit failed on `src` (`error`, e.g. a non-positive-definite K_y) the status word of
+    the metadata broadcast carries it and EVERY rank raises (numpy.linalg.LinAlgError for a
+    failed factor) instead of waiting for a factor that never comes."""
     ws, rank = world()
     if ws == 1:
+        if error is not None:
+            raise error
         return gp
-    meta = torch.zeros(3, dtype=torch.int64, device=device)
+    meta = torch.zeros(4, dtype=torch.int64, device=device)
     if rank == src:
-        meta[0], meta[1], meta[2] = gp.n, gp.n_train, gp.n_pad
+        if error is None:
+            meta[0], meta[1], meta[2] = gp.n, gp.n_train, gp.n_pad
+        else:
+            meta[3] = 1 if isinstance(error, np.linalg.LinAlgError) else 2
     dist.broadcast(meta, src)
-    n, ntr, npad = (int(v) for v in meta.tolist())
+    n, ntr, npad, status = (int(v) for v in meta.tolist())
+    if status != 0:
+        if rank == src:
+            raise error
+        if status == 1:
+            raise np.linalg.LinAlgError(f"the fit on rank {src} failed: K_y is not positive definite")
+        raise RuntimeError(f"the fit on rank {src} failed")
     blocks = packed_blocks(n)
     packed = torch.empty(blocks[-1][2], dtype=torch.float64, device=device)
     if rank != src:
@@ -82,8 +97,13 @@ def fit_sharded(spec: E.KernelSpec, x, y, noise: float, device, mode: str = "bca
     ws, rank = world()
     if ws == 1 or mode == "replicate":
         return E.fit(spec, x, y, noise, jitter=jitter, device=device, variance=variance, check=check)
-    gp = E.fit(spec, x, y, noise, jitter=jitter, device=device, variance=variance) if rank == 0 else None
-    gp = broadcast_fit(gp, spec, noise, x, device)
+    gp, err = None, None
+    if rank == 0:
+        try:
+            gp = E.fit(spec, x, y, noise, jitter=jitter, device=device, variance=variance)
+        except Exception as e:   # noqa: BLE001 — re-raised on every rank by broadcast_fit
+            err = e
+    gp = broadcast_fit(gp, spec, noise, x, device, error=err)
     if variance == "ozaki" and "ozaki" not in gp.extra:
         E.ozaki_prepare(gp, diag_add=float(noise + jitter))   # a-priori moduli count: no host sync
     return gp
@@ -99,12 +119,16 @@ def predict_shard(pred: E.Predictor, xg_all, var_mode: str = "latent", compute_v
     return lo, hi, mean, var
 
 
-def gather_shards(m: int, bd: int, lo: int, hi: int, mean, var, device):
-    """All-gather the shards and reassemble the full [u(M)..., v(M)...] vectors in rank order."""
+def gather_shards(m: int, bd: int, lo: int, hi: int, mean, var, device, align: int = 64):
+    """All-gather the shards and reassemble the full [u(M)..., v(M)...] vectors in rank order.
+    `align` must be the one predict_shard used (checked against this rank's (lo, hi))."""
     ws, rank = world()
     if ws == 1:
         return mean, var
-    ranges = [D.shard_range(m, ws, r) for r in range(ws)]
+    ranges = [D.shard_range(m, ws, r, align) for r in range(ws)]
+    if ranges[rank] != (lo, hi):
+        raise ValueError(f"gather_shards: rank {rank} holds [{lo}, {hi}) but align={align} gives "
+                         f"{ranges[rank]}; pass predict_shard's align")
     maxlen = max(b - a for a, b in ranges)
     outs = []
     for t in (mean, var):

@@ -100,3 +100,42 @@ def test_packed_blocks_cover_the_lower_triangle():
         assert np.all(cover[np.tril_indices(n)] == 1)       # every lower entry once
         assert blocks[-1][2] == sum(GD.PACK_ROWS * c1 for _, c1, _ in blocks[:-1])
         assert blocks[-1][2] <= n * n // 2 + n * GD.PACK_ROWS
+
+
+def _fail_worker(rank, world, port, out_dir):
+    """Rank 0's fit fails (non-PD K_y): every rank must raise, none may hang in the broadcast."""
+    import sys
+    for p in (ROOT, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from gp2d import distributed as GD
+    from gp2d import engine as E
+    spec = E.KernelSpec(kind="df", l_df=5.0)
+    err = np.linalg.LinAlgError("K_y is not positive definite (leading minor of order 3)") if rank == 0 else None
+    raised = "none"
+    try:
+        GD.broadcast_fit(None, spec, -1e-3, None, "cpu", error=err)
+    except np.linalg.LinAlgError:
+        raised = "LinAlgError"
+    # gather_shards refuses a range that does not match its align
+    bad = "none"
+    try:
+        lo, hi = GD.D.shard_range(1100, world, rank, 128)   # 640 | 576 with align 64
+        GD.gather_shards(1100, 2, lo, hi, torch.zeros(2 * (hi - lo)), torch.zeros(2 * (hi - lo)), "cpu", align=64)
+    except ValueError:
+        bad = "ValueError"
+    with open(os.path.join(out_dir, f"fail{rank}.txt"), "w") as f:
+        f.write(f"{raised} {bad}")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bcast_fit_failure_raises_on_every_rank(tmp_path):
+    world = 2
+    mp.spawn(_fail_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    for i in range(world):
+        raised, bad = open(os.path.join(tmp_path, f"fail{i}.txt")).read().split()
+        assert raised == "LinAlgError", i
+        assert bad == "ValueError", i
