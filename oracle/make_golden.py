@@ -233,6 +233,81 @@ def gen_mykernel(gs, out):
                         x=x, y=y, u=u, v=v, xg=xg, l_df=l_df, noise=noise, mean=f, var=var)
 
 
+def config_subsample(xa, xg, n_near=256, n_rand=256, seed=5):
+    """512 grid indices for the BASELINE-size fixtures: the n_near grid points closest to a
+    training point (where var ≪ kss and the cancellation kss − ‖W k*‖² is worst) plus
+    n_rand seeded uniform draws from the rest.  Sorted, unique."""
+    from scipy.spatial import cKDTree
+    d, _ = cKDTree(xa).query(xg)
+    near = np.argsort(d, kind="stable")[:n_near]
+    rest = np.setdiff1d(np.arange(xg.shape[0]), near)
+    rnd = np.random.default_rng(seed).choice(rest, n_rand, replace=False)
+    return np.unique(np.concatenate([near, rnd]))
+
+
+def _refined_posterior(K, ks, kss, obs):
+    """Posterior mean / variance at the fixture points, accurate well past fp64 working
+    precision: Cholesky solve of K z = ks, one step of iterative refinement with the residual
+    in extended precision (x87 long double), then kss − ks·z and ks·α summed in long
+    double.  This is the yardstick for the ELEMENTWISE variance gate, which the reference's
+    own np.linalg.inv product cannot serve (its rounding is of the same order)."""
+    import scipy.linalg as sla
+    ld = np.longdouble
+    c = sla.cho_factor(K, lower=True)
+    rhs = np.concatenate([ks.T, obs[:, None]], 1)       # (n, 2m + 1)
+    z = sla.cho_solve(c, rhs)
+    Kl = K.astype(ld)
+    r = rhs.astype(ld) - Kl @ z.astype(ld)
+    z = z.astype(ld) + sla.cho_solve(c, r.astype(np.float64)).astype(ld)
+    ksl = ks.astype(ld)
+    var = kss.astype(ld) - np.einsum("ij,ji->i", ksl, z[:, :-1])
+    mean = ksl @ z[:, -1]
+    return mean.astype(np.float64), var.astype(np.float64)
+
+
+def gen_configs(gs, out):
+    """BASELINE.json configs at full size: the bench's seeded inputs
+    (gp2d.data.synthetic_tracks(4096, seed=2016), bbox_grid(…, 256, pad=5)) through the
+    reference's own GP_laser.py:113-134 recipe with its vectorised myKernel
+    (GP_scripts.py:6-46) and np.linalg.inv, evaluated at a 512-point grid subsample
+    (config_subsample).  Cases: the headline (div-free, α = 1) and config C (mixed, α = ½);
+    ℓ_df = ℓ_cf = 5 km, noise 0.0025, as bench.py.  Also stored: the refined posterior
+    (_refined_posterior) for the elementwise variance gate."""
+    x, y, u, v = synthetic_tracks(4096)
+    xa = np.stack([x, y], 1)
+    gx = np.linspace(x.min() - 5, x.max() + 5, 256)      # = gp2d.data.bbox_grid(x, y, 256, pad=5)
+    gy = np.linspace(y.min() - 5, y.max() + 5, 256)
+    GX, GY = np.meshgrid(gx, gy)
+    xg_all = np.stack([GX.reshape(-1), GY.reshape(-1)], 1)
+    idx = config_subsample(xa, xg_all)
+    xg = xg_all[idx]
+    m = xg.shape[0]
+    obs = np.concatenate([u, v])
+    d = dict(x=x, y=y, u=u, v=v, idx=idx, xg=xg, l_df=5.0, l_cf=5.0, noise=0.0025)
+    for name, rate in (("df", 1.0), ("mixed", 0.5)):
+        t0 = time.time()
+        K = gs["myKernel"](xa, xa, 5.0, 5.0, rate)
+        K = K + np.identity(K.shape[0]) * 0.0025         # GP_laser.py:114-115
+        Ki = np.linalg.inv(K)                            # GP_laser.py:118
+        Ks = gs["myKernel"](xg, xa, 5.0, 5.0, rate)      # GP_laser.py:122 (vectorised form)
+        f = gs["getMean"](Ks, Ki, obs[:, None])          # GP_laser.py:134
+        kss = np.diag(gs["myKernel"](xg, xg, 5.0, 5.0, rate))
+        var = kss - np.einsum("ij,ij->i", Ks, Ks @ Ki)   # diag of GP_laser.py:129
+        del Ki
+        mr, vr = _refined_posterior(K, Ks, kss, obs)
+        print(f"  config {name}: N=4096, {m} points, {time.time() - t0:.1f}s; inv recipe vs refined: "
+              f"mean {np.max(np.abs(f - mr)) / np.max(np.abs(mr)):.1e}, var elementwise "
+              f"{np.max(np.abs(var - vr) / vr):.1e}, min var/kss {np.min(vr / kss):.1e}")
+        d[f"{name}_rate"] = rate
+        d[f"{name}_mean"] = f
+        d[f"{name}_var"] = var
+        d[f"{name}_mean_refined"] = mr
+        d[f"{name}_var_refined"] = vr
+        d[f"{name}_kss"] = kss
+        d[f"{name}_K_rowsum"] = K.sum(1)
+    np.savez_compressed(os.path.join(out, "configs_N4096.npz"), **d)
+
+
 def gen_sklearn(out):
     """Config A: krig.scikit_prior's model (krig.py:174-194) on 3-D (T,Y,X) inputs, N=128,
     32×32 grid at one time slice."""
@@ -517,7 +592,8 @@ def main():
                 mykernel=lambda: gen_mykernel(gs, a.out), sklearn=lambda: gen_sklearn(a.out),
                 indices=lambda: gen_indices(a.out), grids=lambda: gen_grids(a.out),
                 lml=lambda: gen_lml(gs, a.out), st=lambda: gen_st(gs, a.out),
-                prep=lambda: gen_prep(a.out), window=lambda: gen_prior_window(a.out))
+                prep=lambda: gen_prep(a.out), window=lambda: gen_prior_window(a.out),
+                configs=lambda: gen_configs(gs, a.out))
     for name, fn in jobs.items():
         if a.only and name not in a.only.split(","):
             continue

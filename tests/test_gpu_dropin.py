@@ -80,8 +80,10 @@ def test_getcov_golden(golden, kind):
 def test_getcov_non_pd_raises():
     x = np.array([0.0, 0.0, 1.0])
     y = np.array([0.0, 0.0, 1.0])   # a repeated point: K is singular without noise
+    # sigma = 0.5 makes K_ii = 1/sigma^2 = 4 a perfect square, so the second pivot is
+    # 4 - (4/2)^2 = 0 exactly (with another sigma it rounds to a tiny value of either sign)
     with pytest.raises(np.linalg.LinAlgError):
-        GS.getCov(x, y, x, y, 0.7, 1)
+        GS.getCov(x, y, x, y, 0.5, 1)
 
 
 def test_laser_recipe_through_module(golden):
