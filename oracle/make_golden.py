@@ -308,6 +308,111 @@ def gen_configs(gs, out):
     np.savez_compressed(os.path.join(out, "configs_N4096.npz"), **d)
 
 
+def gen_config_d(gs, out):
+    """BASELINE config D on rank 0's shard: mixed (α = ½, ℓ = 5), N_train = 16384 (a 32768²
+    K), the 512 × 512 bbox grid cut into 8 shards (gp2d.data.shard_range) — rank 0 holds the
+    first 32768 points.  K is built from the reference's myKernel (GP_scripts.py:6-42) in
+    row chunks (one call on 16384² pairs would need ~40 GB of temporaries); at this size the
+    fixture factors K_y by Cholesky (scipy) instead of np.linalg.inv, and evaluates the
+    posterior at 256 points of the shard (128 nearest to a training point + 128 seeded)."""
+    import scipy.linalg as sla
+    N, rate = 16384, 0.5
+    x, y, u, v = synthetic_tracks(N)
+    xa = np.stack([x, y], 1)
+    gx = np.linspace(x.min() - 5, x.max() + 5, 512)
+    gy = np.linspace(y.min() - 5, y.max() + 5, 512)
+    GX, GY = np.meshgrid(gx, gy)
+    xg_all = np.stack([GX.reshape(-1), GY.reshape(-1)], 1)
+    shard = xg_all[:32768]                                # shard_range(262144, 8, 0) = [0, 32768)
+    idx = config_subsample(xa, shard, 128, 128)
+    xg = shard[idx]
+    t0 = time.time()
+    K = np.empty((2 * N, 2 * N))
+    c = 1024
+    for r0 in range(0, N, c):
+        blk = gs["myKernel"](xa[r0:r0 + c], xa, 5.0, 5.0, rate)   # rows [u(r0:r0+c); v(r0:r0+c)]
+        K[r0:r0 + c] = blk[:c]
+        K[N + r0:N + r0 + c] = blk[c:]
+        del blk
+    K[np.diag_indices(2 * N)] += 0.0025
+    rowsum = K.sum(1)
+    Ks = gs["myKernel"](xg, xa, 5.0, 5.0, rate)
+    kss = np.diag(gs["myKernel"](xg, xg, 5.0, 5.0, rate))
+    obs = np.concatenate([u, v])
+    # scipy's and numpy's Cholesky both segfault at n = 32768 in this container (OpenBLAS), so
+    # the factor is blocked here (4096-wide blocks, LAPACK on the blocks).  Only the forward
+    # solve is needed: with Z = L⁻¹[Ksᵀ, y], var = kss − ‖Z_j‖² and
+    # mean = Z_jᵀ Z_y.
+    bs = 4096
+    L = K                                                 # blocked right-looking Cholesky in place
+    for k0 in range(0, 2 * N, bs):
+        k1 = k0 + bs
+        L[k0:k1, k0:k1] = np.linalg.cholesky(L[k0:k1, k0:k1])
+        if k1 < 2 * N:
+            L[k1:, k0:k1] = sla.solve_triangular(L[k0:k1, k0:k1], L[k1:, k0:k1].T, lower=True,
+                                                 check_finite=False).T
+            for j0 in range(k1, 2 * N, bs):
+                L[j0:, j0:j0 + bs] -= L[j0:, k0:k1] @ L[j0:j0 + bs, k0:k1].T
+    B = np.concatenate([Ks.T, obs[:, None]], 1)
+    Z = np.empty_like(B)
+    for i0 in range(0, 2 * N, bs):
+        r = B[i0:i0 + bs] - L[i0:i0 + bs, :i0] @ Z[:i0]
+        Z[i0:i0 + bs] = sla.solve_triangular(L[i0:i0 + bs, i0:i0 + bs], r, lower=True, check_finite=False)
+    mean = Z[:, :-1].T @ Z[:, -1]     # (blocked forward substitution above, 4096-row blocks)
+    var = kss - np.einsum("ij,ij->j", Z[:, :-1], Z[:, :-1])
+    print(f"  config D rank-0 shard: N={N}, {xg.shape[0]} points, {time.time() - t0:.1f}s, "
+          f"min var/kss {np.min(var / kss):.1e}")
+    np.savez_compressed(os.path.join(out, "config_d_rank0.npz"), idx=idx, xg=xg, rate=rate, l=5.0, noise=0.0025,
+                        mean=mean, var=var, kss=kss, K_rowsum=rowsum, x_sum=np.array([x.sum(), y.sum()]))
+
+
+def config_e_settings():
+    """BASELINE config E's 64 hyperparameter settings: ℓ_df on 8 log-spaced values in
+    [2, 12] km × noise σ² on 8 log-spaced values in [1e-3, 5e-2] (div-free kernel)."""
+    return [dict(l_df=float(l), noise=float(nz)) for l in np.geomspace(2.0, 12.0, 8)
+            for nz in np.geomspace(1e-3, 5e-2, 8)]
+
+
+def gen_config_e(gs, out):
+    """BASELINE config E, rank 0's share of the 64-setting sweep over 8 GPUs (settings 0, 8,
+    …, 56 — gp2d.hyper.sweep deals them round-robin) at N_train = 4096 (seeded tracks): the
+    log marginal likelihood of each, with K from the reference's myKernel (GP_scripts.py:6-42)
+    and a Cholesky factor; for two of them also the gradient in (ℓ_df, noise): ∂/∂ℓ_df by a
+    4-point central difference of that LML, ∂/∂noise = ½(αᵀα − tr K_y⁻¹) exactly."""
+    import scipy.linalg as sla
+    x, y, u, v = synthetic_tracks(4096)
+    xa = np.stack([x, y], 1)
+    obs = np.concatenate([u, v])
+    S = config_e_settings()
+    share = list(range(0, 64, 8))
+
+    def lml(l, nz, want=False):
+        K = gs["myKernel"](xa, xa, l, l, 1.0)
+        K[np.diag_indices_from(K)] += nz
+        L = np.linalg.cholesky(K)
+        a = sla.cho_solve((L, True), obs)
+        val = -0.5 * obs @ a - np.sum(np.log(np.diag(L))) - 0.5 * obs.size * np.log(2 * np.pi)
+        return (val, L, a) if want else val
+
+    t0 = time.time()
+    vals = np.array([lml(S[i]["l_df"], S[i]["noise"]) for i in share])
+    grads = []
+    gidx = [share[2], share[5]]
+    for i in gidx:
+        l, nz = S[i]["l_df"], S[i]["noise"]
+        h = 1e-4 * l
+        f = [lml(l + t * h, nz) for t in (-2, -1, 1, 2)]
+        gl = (f[0] - 8 * f[1] + 8 * f[2] - f[3]) / (12 * h)
+        _, L, a = lml(l, nz, want=True)
+        Li = sla.solve_triangular(L, np.identity(L.shape[0]), lower=True)
+        gn = 0.5 * (a @ a - np.sum(Li * Li))
+        grads.append([gl, gn])
+    print(f"  config E share: 8 settings x N=4096, {time.time() - t0:.1f}s")
+    np.savez_compressed(os.path.join(out, "config_e_share.npz"), share=np.array(share),
+                        l_df=np.array([S[i]["l_df"] for i in share]), noise=np.array([S[i]["noise"] for i in share]),
+                        lml=vals, grad_idx=np.array(gidx), grad=np.array(grads))
+
+
 def gen_sklearn(out):
     """Config A: krig.scikit_prior's model (krig.py:174-194) on 3-D (T,Y,X) inputs, N=128,
     32×32 grid at one time slice."""
@@ -593,7 +698,8 @@ def main():
                 indices=lambda: gen_indices(a.out), grids=lambda: gen_grids(a.out),
                 lml=lambda: gen_lml(gs, a.out), st=lambda: gen_st(gs, a.out),
                 prep=lambda: gen_prep(a.out), window=lambda: gen_prior_window(a.out),
-                configs=lambda: gen_configs(gs, a.out))
+                configs=lambda: gen_configs(gs, a.out), config_d=lambda: gen_config_d(gs, a.out),
+                config_e=lambda: gen_config_e(gs, a.out))
     for name, fn in jobs.items():
         if a.only and name not in a.only.split(","):
             continue

@@ -1,0 +1,140 @@
+"""BASELINE.json configs at their real size through the HIP engine (the bench path).
+
+Fixtures (oracle/make_golden.py, generated from the reference's own code in the build
+container; /root/reference is not read here):
+  * configs_N4096.npz — the headline (div-free) and config C (mixed ½/½): the bench's seeded
+    N_train = 4096 tracks, the full 256 × 256 grid predicted on the GPU, checked at 512 grid
+    points (the 256 nearest to an observation + 256 seeded).  `mean`/`var` are the
+    reference's GP_laser.py:113-134 recipe (myKernel + np.linalg.inv); `*_refined` is the
+    same posterior with an extended-precision refinement step (make_golden._refined_posterior).
+  * config_d_rank0.npz — config D's rank-0 shard (N_train = 16384, 32768 of the 512² points).
+  * config_e_share.npz — rank 0's share of config E's 64-setting sweep at N_train = 4096.
+
+Gates (north_star: fp64 posterior mean / variance within 1e-10 relative):
+  * normwise: max|a − b| / max|b| ≤ 1e-10 per output vector, against the reference recipe;
+  * elementwise variance: max_j |var_j − ref_j| / ref_j ≤ 1e-10 against the refined
+    posterior.  The reference's own inv recipe is 1.7e-10 (div-free) / 6.6e-11 (mixed)
+    elementwise from the refined one at these points (its rounding is not smaller than the
+    gate), so the elementwise gate is taken against the refined values;
+  * elementwise mean: |Δmean_j| ≤ 1e-10 · max(|mean_j|, 1e-2 · max|mean|) (the mean crosses
+    zero, so a pure ratio is undefined at the crossings).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("no HIP device", allow_module_level=True)
+
+from gp2d import data as D  # noqa: E402
+from gp2d import engine as E  # noqa: E402
+from gp2d import hyper as H  # noqa: E402
+
+GATE = 1e-10
+
+
+def rel(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    return float(np.max(np.abs(a - b)) / np.max(np.abs(b)))
+
+
+def elem_var(a, b):
+    return float(np.max(np.abs(a - b) / b))
+
+
+def elem_mean(a, b):
+    floor = 1e-2 * np.max(np.abs(b))
+    return float(np.max(np.abs(a - b) / np.maximum(np.abs(b), floor)))
+
+
+def _at(t, idx, m):
+    a = t.cpu().numpy()
+    return np.concatenate([a[idx], a[m + idx]])
+
+
+@pytest.fixture(scope="module")
+def n4096(golden):
+    g = golden("configs_N4096.npz")
+    x1, x2, u, v = D.synthetic_tracks(4096, seed=2016)
+    assert np.array_equal(x1, g["x"]) and np.array_equal(u, g["u"]) and np.array_equal(v, g["v"])
+    _, _, xg = D.bbox_grid(x1, x2, 256, pad=5.0)
+    assert np.array_equal(xg[g["idx"]], g["xg"])
+    return g, np.stack([x1, x2], 1), np.concatenate([u, v]), xg
+
+
+@pytest.mark.parametrize("variance", ["ozaki", "f64"])
+@pytest.mark.parametrize("name", ["df", "mixed"])
+def test_config_n4096_full_grid(n4096, name, variance):
+    """Headline (df) and config C (mixed) exactly as bench.py runs them: fit on the device,
+    predict all 65,536 grid points in 8192-point chunks (Morton order and zero-slab skipping
+    active on the Ozaki engine), then the 512 fixture points."""
+    g, x, y, xg = n4096
+    rate = float(g[f"{name}_rate"])
+    ks = E.KernelSpec(kind=name, l_df=5.0, l_cf=5.0, ratio=rate)
+    gp = E.fit(ks, torch.tensor(x, device="cuda"), torch.tensor(y, device="cuda"), noise=0.0025, variance=variance)
+    assert (variance == "ozaki") == ("ozaki" in gp.extra)
+    mu, var = E.Predictor(gp, 8192)(torch.tensor(xg, device="cuda"))
+    m = xg.shape[0]
+    idx = g["idx"]
+    mu_s, var_s = _at(mu, idx, m), _at(var, idx, m)
+    assert np.all(np.isfinite(var.cpu().numpy())) and np.all(var.cpu().numpy() > 0)
+    M = idx.size
+    for c in (slice(0, M), slice(M, 2 * M)):        # u and v components separately
+        assert rel(mu_s[c], g[f"{name}_mean"][c]) < GATE
+        assert rel(var_s[c], g[f"{name}_var"][c]) < GATE
+    ev = elem_var(var_s, g[f"{name}_var_refined"])
+    em = elem_mean(mu_s, g[f"{name}_mean_refined"])
+    print(f"{name}/{variance}: var elementwise {ev:.2e}, mean elementwise {em:.2e}, "
+          f"var normwise {rel(var_s, g[f'{name}_var']):.2e}")
+    assert ev < GATE and em < GATE
+    # the nearest-to-observation half is where the cancellation kss − ‖W k*‖² bites
+    kss = g[f"{name}_kss"]
+    assert np.min(g[f"{name}_var_refined"] / kss) < 1e-2
+
+
+def test_config_d_rank0_shard(golden):
+    """Config D: N_train = 16384 (32768² K_y), rank 0's shard of the 512² grid — the
+    per-rank work of the 8-GPU run — on the Ozaki engine, at the fixture's 256 points."""
+    g = golden("config_d_rank0.npz")
+    x1, x2, u, v = D.synthetic_tracks(16384, seed=2016)
+    assert np.allclose([x1.sum(), x2.sum()], g["x_sum"], rtol=0, atol=0)
+    _, _, xg_all = D.bbox_grid(x1, x2, 512, pad=5.0)
+    lo, hi = D.shard_range(xg_all.shape[0], 8, 0)
+    assert (lo, hi) == (0, 32768)
+    shard = xg_all[lo:hi]
+    assert np.array_equal(shard[g["idx"]], g["xg"])
+    ks = E.KernelSpec(kind="mixed", l_df=5.0, l_cf=5.0, ratio=float(g["rate"]))
+    gp = E.fit(ks, torch.tensor(np.stack([x1, x2], 1), device="cuda"),
+               torch.tensor(np.concatenate([u, v]), device="cuda"), noise=0.0025, variance="ozaki")
+    mu, var = E.Predictor(gp, 8192)(torch.tensor(shard, device="cuda"))
+    m = shard.shape[0]
+    mu_s, var_s = _at(mu, g["idx"], m), _at(var, g["idx"], m)
+    del gp
+    torch.cuda.empty_cache()
+    ev = elem_var(var_s, g["var"])
+    print(f"D: mean {rel(mu_s, g['mean']):.2e} var {rel(var_s, g['var']):.2e} var elementwise {ev:.2e}")
+    assert rel(mu_s, g["mean"]) < GATE and rel(var_s, g["var"]) < GATE
+    assert ev < GATE
+    assert elem_mean(mu_s, g["mean"]) < GATE
+
+
+def test_config_e_sweep_share(golden):
+    """Config E: one rank's 8 of the 64 settings at N_train = 4096 through hyper.sweep (the
+    call each of the 8 ranks makes): LML of all 8, gradient of 2, against the reference-
+    myKernel fixture."""
+    g = golden("config_e_share.npz")
+    x1, x2, u, v = D.synthetic_tracks(4096, seed=2016)
+    x, y = np.stack([x1, x2], 1), np.concatenate([u, v])
+    settings = [dict(l_df=float(l), noise=float(nz)) for l, nz in zip(g["l_df"], g["noise"])]
+    ks = E.KernelSpec(kind="df", l_df=5.0)
+    vals, grads = H.sweep(ks, x, y, settings, noise=0.0025, eval_gradient=True)
+    assert np.max(np.abs(vals - g["lml"]) / np.abs(g["lml"])) < GATE
+    names = list(H.get_params(ks, 0.0025))
+    il, inz = names.index("l_df"), names.index("noise")
+    for k, gi in enumerate(g["grad_idx"]):
+        j = list(g["share"]).index(gi)
+        ref = g["grad"][k]
+        # ∂/∂ℓ: the fixture's central difference is good to ~1e-8 relative; ∂/∂noise is exact
+        assert abs(grads[j, il] - ref[0]) < 1e-6 * abs(ref[0])
+        assert abs(grads[j, inz] - ref[1]) < 1e-9 * abs(ref[1])
