@@ -1,0 +1,96 @@
+"""The multi-GPU path end to end on the GPU: two fresh rank processes (gloo process group,
+both on the one card of the test box — the 8-GPU node is the driver's) run
+fit_sharded(mode='bcast', variance='ozaki' / 'f64') → predict_shard → gather_shards, and the
+gathered posterior must be bit-identical to the one-process fit + predict.
+
+Rank 0 fits and broadcasts the packed W = L⁻¹, α and the (Morton-ordered) training points;
+rank 1 derives its own INT8 residue planes from the received factor (a-priori moduli count,
+as engine.fit does), so both ranks predict from identical operands.  The children are started
+with the 'spawn' method (a new interpreter each), never by exec'ing this process.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("no HIP device", allow_module_level=True)
+
+import torch.multiprocessing as mp  # noqa: E402
+
+from conftest import PKG, ROOT  # noqa: E402
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _problem():
+    rng = np.random.default_rng(1024)
+    n, G = 1024, 96
+    x = np.stack([rng.uniform(0, 60, n), rng.uniform(0, 45, n)], 1)
+    y = np.concatenate([np.sin(x[:, 1] / 7), np.cos(x[:, 0] / 9)]) + rng.normal(0, 0.05, 2 * n)
+    gx, gy = np.linspace(-5, 65, G), np.linspace(-5, 50, G + 7)
+    GX, GY = np.meshgrid(gx, gy)
+    return x, y, np.stack([GX.reshape(-1), GY.reshape(-1)], 1)
+
+
+def _worker(rank, world, port, out_dir, variance, kind):
+    for p in (ROOT, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from gp2d import distributed as GD
+    from gp2d import engine as E
+    x, y, xg = _problem()
+    dev = torch.device("cuda", 0)
+    spec = E.KernelSpec(kind=kind, l_df=5.0, l_cf=4.0, ratio=0.5 if kind == "mixed" else 1.0)
+    gp = GD.fit_sharded(spec, torch.tensor(x, device=dev), torch.tensor(y, device=dev), 0.0025, dev,
+                        mode="bcast", variance=variance)
+    pred = E.Predictor(gp, 1024)
+    lo, hi, mean, var = GD.predict_shard(pred, torch.tensor(xg, device=dev))
+    fm, fv = GD.gather_shards(xg.shape[0], 2, lo, hi, mean, var, dev)
+    torch.cuda.synchronize()
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), mean=fm.cpu().numpy(), var=fv.cpu().numpy(), lo=lo, hi=hi,
+             nmod=int(gp.extra["ozaki"][2]) if "ozaki" in gp.extra else 0)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("variance,kind", [("ozaki", "df"), ("ozaki", "mixed"), ("f64", "df")])
+def test_bcast_fit_two_ranks_bit_identical(tmp_path, variance, kind):
+    from gp2d import engine as E
+    world = 2
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, str(tmp_path), variance, kind)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    codes = [p.exitcode for p in procs]
+    for p in procs:
+        if p.is_alive():  # pragma: no cover — a hung rank: end it, then fail
+            p.kill()
+    assert codes == [0, 0], codes
+    x, y, xg = _problem()
+    spec = E.KernelSpec(kind=kind, l_df=5.0, l_cf=4.0, ratio=0.5 if kind == "mixed" else 1.0)
+    gp = E.fit(spec, x, y, 0.0025, variance=variance)
+    mu, var = (t.cpu().numpy() for t in E.Predictor(gp, 1024)(xg))
+    r = [np.load(os.path.join(tmp_path, f"rank{i}.npz")) for i in range(world)]
+    assert int(r[0]["lo"]) == 0 and int(r[0]["hi"]) == int(r[1]["lo"]) and int(r[1]["hi"]) == xg.shape[0]
+    assert int(r[0]["nmod"]) == int(r[1]["nmod"])
+    for i in range(world):
+        assert np.array_equal(r[i]["mean"], mu), i
+        assert np.array_equal(r[i]["var"], var), i
