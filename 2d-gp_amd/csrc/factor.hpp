@@ -256,8 +256,11 @@ __device__ __forceinline__ void tile4x4_store(double* __restrict__ S, int r, int
   }
 }
 
+// inv_in_place (the fused factor + inverse, gp2d_potrf_inv): A's diagonal block receives
+// W_kk = L_kk⁻¹ instead of L_kk (nothing reads L_kk from A after this kernel: the panel TRSM
+// uses dinv), which is TRTRI's level 0.
 __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A, int64_t lda, int k0,
-                                                         double* __restrict__ dinv, int* info) {
+                                                         double* __restrict__ dinv, int* info, int inv_in_place) {
   __shared__ __attribute__((aligned(16))) double S[NB * DP];
   __shared__ __attribute__((aligned(16))) double colbuf[32];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -338,7 +341,7 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
   GP2D_STAMP(2);
   // ---- store L (zero strict upper)
 #pragma unroll 1
-  for (int e = 0; e < (NB * NB / 2) / 256; ++e) {
+  for (int e = 0; e < (inv_in_place ? 0 : (NB * NB / 2) / 256); ++e) {
     const int idx = tid + 256 * e, r = idx >> 6, c = 2 * (idx & 63);
     const d2 v = *reinterpret_cast<const d2*>(S + dsw(r, c));
     *reinterpret_cast<d2*>(Ab + (int64_t)r * lda + c) = d2{(c <= r) ? v.x : 0.0, (c + 1 <= r) ? v.y : 0.0};
@@ -406,7 +409,9 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
   for (int e = 0; e < (NB * NB / 2) / 256; ++e) {
     const int idx = tid + 256 * e, r = idx >> 6, c = 2 * (idx & 63);
     const d2 v = *reinterpret_cast<const d2*>(S + dsw(r, c));
-    *reinterpret_cast<d2*>(D + (int64_t)r * NB + c) = d2{(c <= r) ? v.x : 0.0, (c + 1 <= r) ? v.y : 0.0};
+    const d2 w = d2{(c <= r) ? v.x : 0.0, (c + 1 <= r) ? v.y : 0.0};
+    *reinterpret_cast<d2*>(D + (int64_t)r * NB + c) = w;
+    if (inv_in_place) *reinterpret_cast<d2*>(Ab + (int64_t)r * lda + c) = w;
   }
 }
 

@@ -202,45 +202,64 @@ int gp2d_assemble(const double* xa, int64_t na, int64_t na_pad, const double* xb
   return assemble_impl(xa, na, na_pad, xb, nb, nb_pad, k, diag_add, symmetric, out, ld, S(stream));
 }
 
-// ------------------------------------------------------------------------ POTRF
-size_t gp2d_potrf_workspace(int64_t) { return 0; }
+}  // extern "C"
 
+// ------------------------------------------------------------------------ POTRF
 namespace {
 // POTRF streams (one set per device, created lazily): `crit` carries the critical path
 // (block-column updates, diagonal block, panel TRSM) at the highest priority, `bulk` the
-// trailing SYRK.  (Hardware CU masks splitting the CUs between the two were measured slower
-// at every split)
+// trailing SYRK, `inv` (low priority) the triangular inverse of the fused factor
+// (gp2d_potrf_inv).  (Hardware CU masks splitting the CUs between the streams were measured
+// slower at every split)  One factorisation at a time per device.
 struct FactorStreams {
   std::mutex mu;
-  std::vector<hipStream_t> crit, bulk, aux;   // indexed by device
-  std::vector<std::vector<hipEvent_t>> ev;
+  std::vector<hipStream_t> crit, bulk, aux, inv;   // indexed by device
+  std::vector<std::vector<hipEvent_t>> ev;         // 5 fixed events
+  std::vector<std::vector<hipEvent_t>> blk;        // one per block column (fused inverse)
 };
 FactorStreams g_fs;
 
-int factor_streams(hipStream_t* crit, hipStream_t* bulk, hipStream_t* aux, std::vector<hipEvent_t>** evs) {
+struct FactorCtx {
+  hipStream_t crit, bulk, aux, inv;
+  std::vector<hipEvent_t>* ev;
+  std::vector<hipEvent_t>* blk;
+};
+
+int factor_streams(FactorCtx& c, int nblk) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) { set_error("hipGetDevice failed"); return -1; }
   std::lock_guard<std::mutex> lk(g_fs.mu);
   if ((int)g_fs.crit.size() <= dev) {
     g_fs.crit.resize(dev + 1, nullptr); g_fs.bulk.resize(dev + 1, nullptr); g_fs.aux.resize(dev + 1, nullptr);
+    g_fs.inv.resize(dev + 1, nullptr);
     g_fs.ev.resize(dev + 1);
+    g_fs.blk.resize(dev + 1);
   }
   if (!g_fs.crit[dev]) {
     int lo = 0, hi = 0;
     if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) { lo = 0; hi = 0; }
     if (hipStreamCreateWithPriority(&g_fs.crit[dev], hipStreamNonBlocking, hi) != hipSuccess ||
         hipStreamCreateWithPriority(&g_fs.bulk[dev], hipStreamNonBlocking, lo) != hipSuccess ||
-        hipStreamCreateWithPriority(&g_fs.aux[dev], hipStreamNonBlocking, hi) != hipSuccess) {
+        hipStreamCreateWithPriority(&g_fs.aux[dev], hipStreamNonBlocking, hi) != hipSuccess ||
+        hipStreamCreateWithPriority(&g_fs.inv[dev], hipStreamNonBlocking, lo) != hipSuccess) {
       set_error("hipStreamCreate failed"); return -1;
     }
     g_fs.ev[dev].resize(5);
     for (auto& e : g_fs.ev[dev])
       if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) { set_error("hipEventCreate failed"); return -1; }
   }
-  *crit = g_fs.crit[dev];
-  *bulk = g_fs.bulk[dev];
-  *aux = g_fs.aux[dev];
-  *evs = &g_fs.ev[dev];
+  auto& b = g_fs.blk[dev];
+  while ((int)b.size() < nblk) {
+    hipEvent_t e;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) { set_error("hipEventCreate failed"); return -1; }
+    b.push_back(e);
+  }
+  c.crit = g_fs.crit[dev];
+  c.bulk = g_fs.bulk[dev];
+  c.aux = g_fs.aux[dev];
+  c.inv = g_fs.inv[dev];
+  c.ev = &g_fs.ev[dev];
+  c.blk = &g_fs.blk[dev];
   return 0;
 }
 
@@ -254,9 +273,80 @@ int launch_panel(double* A, int64_t lda, int k, int64_t n, const double* dinv, h
                                                                 1.0, 0.0);
   return check_launch("gemm_f64_panel_kernel");
 }
+
+// ---- TRTRI by recursive doubling over 128-blocks (in place; the diagonal blocks already hold
+// W_kk = L_kk⁻¹): at level g every pair (left = [s·2g, s·2g+g), right = [s·2g+g, s·2g+2g))
+// forms T = L[R, left]·W[left, left], then W[R, left] = −W[R, R]·T — one batched launch per
+// level and product.  T needs (nbk·128/2 + 128)² doubles.
+int trtri_levels(double* A, int64_t lda, int nbk, double* T, hipStream_t s) {
+  for (int g = 1; g < nbk; g *= 2) {
+    const int full = nbk / (2 * g);                // pairs whose right part has g blocks
+    const int rem = nbk - full * 2 * g;            // trailing blocks
+    struct Pair { int Ls, Rs, Rn, count; };
+    std::vector<Pair> launches;
+    if (full > 0) launches.push_back({0, g, g, full});
+    if (rem > g) launches.push_back({full * 2 * g, full * 2 * g + g, rem - g, 1});
+    for (const Pair& pr : launches) {
+      const int64_t Lo = (int64_t)pr.Ls * NB, Ro = (int64_t)pr.Rs * NB;
+      const int bw = g * NB, rh = pr.Rn * NB;
+      const int64_t stride = (int64_t)2 * g * NB * (lda + 1);  // next pair's diagonal offset
+      // T = C · WA      C = A[R, L] (rh × bw), WA = A[L, L] (bw × bw lower)
+      GemmParams p = gemm_params();
+      p.A = A + Ro * lda + Lo; p.lda = lda; p.sA = stride;
+      p.B = A + Lo * lda + Lo; p.ldb = lda; p.sB = stride;
+      p.C = T; p.ldc = bw; p.sC = (int64_t)rh * bw;
+      p.M = rh; p.N = bw; p.K = bw; p.b_lower = 1;
+      p.cols_first = 1;   // column block j needs k ≥ j: long-K tiles first
+      GP2D_CHECK((launch_gemm<false, EPI_STORE>(p, pr.count, s)));
+      // A[R, L] = −WD · T     WD = A[R, R] (rh × rh lower)
+      GemmParams q = gemm_params();
+      q.A = A + Ro * lda + Ro; q.lda = lda; q.sA = stride;
+      q.B = T; q.ldb = bw; q.sB = (int64_t)rh * bw;
+      q.C = A + Ro * lda + Lo; q.ldc = lda; q.sC = stride;
+      q.M = rh; q.N = bw; q.K = rh; q.a_lower = 1; q.alpha = -1.0;
+      q.rev_rows = 1;     // row block i needs k ≤ i: long-K tiles first
+      GP2D_CHECK((launch_gemm<false, EPI_STORE>(q, pr.count, s)));
+    }
+  }
+  return 0;
+}
+
+size_t trtri_t_doubles(int64_t nbk) { return (size_t)(nbk * NB / 2 + NB) * (size_t)(nbk * NB / 2 + NB); }
+
+// The fused inverse splits the top level of the recursive doubling at h (the largest power of
+// two below nb, i.e. the TRTRI's own top-level split): once block column h−1 is factored,
+// W[0:h, 0:h] (every lower level inside the left half) and the top product T = L[h:, 0:h]·W11
+// depend on final data only, so they run on `inv` under the second half of the factorisation;
+// after the last block only W22 = L22⁻¹ and W21 = −W22·T remain.  The same GEMMs on the same
+// operands as trtri_levels over all nb blocks, so the result is bit-identical to
+// gp2d_potrf + gp2d_trtri.
+int inv_top_split(int nb) { int h = 1; while (2 * h < nb) h *= 2; return h; }
+
+int inv_top_gemm(int kind, double* A, int64_t lda, int nb, double* T2, hipStream_t st) {
+  const int h = inv_top_split(nb);
+  const int64_t Ro = (int64_t)h * NB;
+  const int bw = h * NB, rh = (nb - h) * NB;
+  GemmParams p = gemm_params();
+  if (kind == 0) {   // T2 = L[R, left] · W[left, left]
+    p.A = A + Ro * lda; p.lda = lda;
+    p.B = A; p.ldb = lda;
+    p.C = T2; p.ldc = bw;
+    p.M = rh; p.N = bw; p.K = bw; p.b_lower = 1;
+    p.cols_first = 1;
+  } else {           // W[R, left] = −W[R, R] · T2
+    p.A = A + Ro * lda + Ro; p.lda = lda;
+    p.B = T2; p.ldb = bw;
+    p.C = A + Ro * lda; p.ldc = lda;
+    p.M = rh; p.N = bw; p.K = rh; p.a_lower = 1; p.alpha = -1.0;
+    p.rev_rows = 1;
+  }
+  return launch_gemm<false, EPI_STORE>(p, 1, st);
+}
 }  // namespace
 
-// Right-looking blocked Cholesky (NB = 128) with look-ahead on two internal streams and the
+#define GP2D_EV(call) do { if ((call) != hipSuccess) { set_error(#call " failed"); return -1; } } while (0)
+
+// Right-looking blocked Cholesky (NB = 128) with look-ahead on internal streams and the
 // trailing update delayed over pairs of panels:
 //   crit: for pair (k, k+1): block column k+1 ← panel k, factor k+1; block column k+2 ←
 //         panels k and k+1, factor k+2 (diagonal block + panel TRSM each),
@@ -264,20 +354,27 @@ int launch_panel(double* A, int64_t lda, int k, int64_t n, const double* dinv, h
 // so the single-workgroup diagonal kernel hides under the chip-wide SYRK.  Data regions are
 // disjoint (block columns k+1, k+2 vs ≥ k+3); bulk waits for panel k+1, crit waits for the
 // pair's SYRK before it updates block column k+3.  The caller's stream is joined at both ends.
-#define GP2D_EV(call) do { if ((call) != hipSuccess) { set_error(#call " failed"); return -1; } } while (0)
-int gp2d_potrf(double* A, int64_t n, int64_t lda, double* dinv, int* info_dev, void*, size_t, void* stream) {
+// With Tws != NULL the factor is inverted in place on the way (gp2d_potrf_inv, inv_top_split):
+// the diagonal kernels store W_kk, the left half of the inverse and the top-level product
+// T = L21·W11 run on `inv` under the second half of the factorisation, W22 and W21 after it.
+static int potrf_impl(double* A, int64_t n, int64_t lda, double* dinv, int* info_dev, hipStream_t s, double* Tws) {
   GP2D_REQUIRE(n % NB == 0 && n > 0, "potrf: n must be a positive multiple of 128");
   GP2D_REQUIRE(lda >= n && lda % 2 == 0, "potrf: lda must be >= n and even");
   GP2D_REQUIRE(dinv != nullptr, "potrf: dinv buffer is required");
-  hipStream_t s = S(stream);
   const int nb = (int)(n / NB);
-  hipStream_t sc, sb, sa;
-  std::vector<hipEvent_t>* ev;
-  GP2D_CHECK(factor_streams(&sc, &sb, &sa, &ev));
-  hipEvent_t e_pan = (*ev)[0], e_syrk = (*ev)[1], e_join = (*ev)[2], e_start = (*ev)[3], e_aux = (*ev)[4];
+  const bool fused = Tws != nullptr;
+  FactorCtx fc;
+  GP2D_CHECK(factor_streams(fc, fused ? 1 : 0));
+  hipStream_t sc = fc.crit, sb = fc.bulk, sa = fc.aux, si = fc.inv;
+  std::vector<hipEvent_t>& ev = *fc.ev;
+  hipEvent_t e_pan = ev[0], e_syrk = ev[1], e_join = ev[2], e_start = ev[3], e_aux = ev[4];
   GP2D_EV(hipEventRecord(e_join, s));
   GP2D_EV(hipStreamWaitEvent(sc, e_join, 0));
   GP2D_EV(hipStreamWaitEvent(sb, e_join, 0));
+  if (fused) GP2D_EV(hipStreamWaitEvent(si, e_join, 0));
+  const int h = fused ? inv_top_split(nb) : 0;
+  double* T1 = Tws;                                   // lower levels (one half at a time)
+  double* T2 = fused ? Tws + trtri_t_doubles(h) : nullptr;   // top-level T, (nb−h)·128 × h·128
   // A[j.., j] −= L[j.., p] · L[j, p]ᵀ: block column j receives panel p (skinny K = 128 GEMM,
   // B = the NB rows of block j of the panel)
   auto colupdate = [&](int j, int p, hipStream_t st) -> int {
@@ -287,11 +384,19 @@ int gp2d_potrf(double* A, int64_t n, int64_t lda, double* dinv, int* info_dev, v
                                                                          -1.0, 1.0);
     return check_launch("gemm_f64_panel_kernel");
   };
-  // diagonal block j (Cholesky + inverse) and its panel TRSM
+  // diagonal block j (Cholesky + inverse) and its panel TRSM; then (fused) the inverse's
+  // GEMMs whose inputs block column j completes
   auto factor = [&](int j) -> int {
-    potrf_diag_kernel<<<1, 256, 0, sc>>>(A, lda, j * NB, dinv, info_dev);
+    potrf_diag_kernel<<<1, 256, 0, sc>>>(A, lda, j * NB, dinv, info_dev, fused ? 1 : 0);
     GP2D_CHECK(check_launch("potrf_diag_kernel"));
-    return launch_panel(A, lda, j, n, dinv, sc);
+    GP2D_CHECK(launch_panel(A, lda, j, n, dinv, sc));
+    if (fused && nb > 1 && j == h - 1) {   // left half final: W11 and T = L21·W11 under the rest
+      GP2D_EV(hipEventRecord((*fc.blk)[0], sc));
+      GP2D_EV(hipStreamWaitEvent(si, (*fc.blk)[0], 0));
+      GP2D_CHECK(trtri_levels(A, lda, h, T1, si));
+      GP2D_CHECK(inv_top_gemm(0, A, lda, nb, T2, si));
+    }
+    return 0;
   };
   GP2D_CHECK(factor(0));
   // Delayed trailing updates: panels are consumed in pairs, so the bulk SYRK runs with K = 256
@@ -336,11 +441,42 @@ int gp2d_potrf(double* A, int64_t n, int64_t lda, double* dinv, int* info_dev, v
   }
   GP2D_EV(hipEventRecord(e_join, sb));
   GP2D_EV(hipStreamWaitEvent(sc, e_join, 0));
+  if (fused && nb > 1) {   // W22 = L22⁻¹ (its lower levels) and the top level's W21 = −W22·T
+    GP2D_EV(hipEventRecord(e_join, sc));
+    GP2D_EV(hipStreamWaitEvent(si, e_join, 0));
+    double* A22 = A + (int64_t)h * NB * (lda + 1);
+    GP2D_CHECK(trtri_levels(A22, lda, nb - h, T1, si));
+    GP2D_CHECK(inv_top_gemm(1, A, lda, nb, T2, si));
+    GP2D_EV(hipEventRecord(e_join, si));
+    GP2D_EV(hipStreamWaitEvent(sc, e_join, 0));
+  }
   GP2D_EV(hipEventRecord(e_join, sc));
   GP2D_EV(hipStreamWaitEvent(s, e_join, 0));
   dim3 zg((unsigned)((n / 2 + 255) / 256), (unsigned)n);
   zero_upper_kernel<<<zg, 256, 0, s>>>(A, n, lda);
   return check_launch("zero_upper_kernel");
+}
+
+extern "C" {
+size_t gp2d_potrf_workspace(int64_t) { return 0; }
+
+int gp2d_potrf(double* A, int64_t n, int64_t lda, double* dinv, int* info_dev, void*, size_t, void* stream) {
+  return potrf_impl(A, n, lda, dinv, info_dev, S(stream), nullptr);
+}
+
+size_t gp2d_potrf_inv_workspace(int64_t n) {
+  const int nb = (int)(n / NB);
+  if (nb <= 1) return 0;
+  const int h = inv_top_split(nb);
+  return (trtri_t_doubles(h) + (size_t)(nb - h) * NB * (size_t)h * NB) * sizeof(double);
+}
+
+int gp2d_potrf_inv(double* A, int64_t n, int64_t lda, double* dinv, int* info_dev, void* work, size_t work_bytes,
+                   void* stream) {
+  GP2D_REQUIRE(n % NB == 0 && n > 0, "potrf_inv: n must be a positive multiple of 128");
+  if (n == NB) return potrf_impl(A, n, lda, dinv, info_dev, S(stream), A);   // no inverse GEMMs: W = dinv
+  GP2D_REQUIRE(work != nullptr && work_bytes >= gp2d_potrf_inv_workspace(n), "potrf_inv: workspace too small");
+  return potrf_impl(A, n, lda, dinv, info_dev, S(stream), reinterpret_cast<double*>(work));
 }
 
 // ------------------------------------------------------------------------ TRTRI
@@ -365,37 +501,7 @@ int gp2d_trtri(double* A, int64_t n, int64_t lda, const double* dinv, void* work
   }
   put_diag_blocks_kernel<<<dim3(NB * NB / 256, nb), 256, 0, s>>>(A, lda, dinv);
   GP2D_CHECK(check_launch("put_diag_blocks_kernel"));
-  for (int g = 1; g < nb; g *= 2) {
-    // pairs (left = [s·2g, s·2g+g), right = [s·2g+g, min(s·2g+2g, nb))) in 128-blocks
-    const int full = nb / (2 * g);                 // pairs whose right part has g blocks
-    const int rem = nb - full * 2 * g;             // trailing blocks
-    struct Pair { int Ls, Rs, Rn, count; };
-    std::vector<Pair> launches;
-    if (full > 0) launches.push_back({0, g, g, full});
-    if (rem > g) launches.push_back({full * 2 * g, full * 2 * g + g, rem - g, 1});
-    for (const Pair& pr : launches) {
-      const int64_t Lo = (int64_t)pr.Ls * NB, Ro = (int64_t)pr.Rs * NB;
-      const int bw = g * NB, rh = pr.Rn * NB;
-      const int64_t stride = (int64_t)2 * g * NB * (lda + 1);  // next pair's diagonal offset
-      // T = C · WA      C = A[R, L] (rh × bw), WA = A[L, L] (bw × bw lower)
-      GemmParams p = gemm_params();
-      p.A = A + Ro * lda + Lo; p.lda = lda; p.sA = stride;
-      p.B = A + Lo * lda + Lo; p.ldb = lda; p.sB = stride;
-      p.C = T; p.ldc = bw; p.sC = (int64_t)rh * bw;
-      p.M = rh; p.N = bw; p.K = bw; p.b_lower = 1;
-      p.cols_first = 1;   // column block j needs k ≥ j: long-K tiles first
-      GP2D_CHECK((launch_gemm<false, EPI_STORE>(p, pr.count, s)));
-      // A[R, L] = −WD · T     WD = A[R, R] (rh × rh lower)
-      GemmParams q = gemm_params();
-      q.A = A + Ro * lda + Ro; q.lda = lda; q.sA = stride;
-      q.B = T; q.ldb = bw; q.sB = (int64_t)rh * bw;
-      q.C = A + Ro * lda + Lo; q.ldc = lda; q.sC = stride;
-      q.M = rh; q.N = bw; q.K = rh; q.a_lower = 1; q.alpha = -1.0;
-      q.rev_rows = 1;     // row block i needs k ≤ i: long-K tiles first
-      GP2D_CHECK((launch_gemm<false, EPI_STORE>(q, pr.count, s)));
-    }
-  }
-  return 0;
+  return trtri_levels(A, lda, nb, T, s);
 }
 
 // ------------------------------------------------------------------------ POTRS

@@ -174,6 +174,16 @@ class GPFit:
             _raise_fit_errors(inf, err)
         return self
 
+    def record_stream(self, stream) -> "GPFit":
+        """Mark the fit's device tensors as in use on `stream` — for a fit made on one stream
+        and predicted on another: the caching allocator then keeps their memory until the
+        work queued on `stream` when they are freed has finished."""
+        oz = self.extra.get("ozaki", ())
+        for t in (self.x, self.W, self.alpha, self.y, self.perm, *oz[:2]):
+            if isinstance(t, torch.Tensor) and t.is_cuda:
+                t.record_stream(stream)
+        return self
+
     @property
     def n(self) -> int:
         return self.W.shape[0]
@@ -193,6 +203,12 @@ def _pad_obs(y, n_train: int, n_pad: int, bd: int, device) -> torch.Tensor:
 
 
 VARIANCE_ENGINES = ("f64", "ozaki")
+
+# fit: the two-call gp2d_potrf + gp2d_trtri sequence, or gp2d_potrf_inv (the left half of the
+# inverse and the top-level T = L21·W11 issued under the second half of the factorisation).
+# Bit-identical results; measured a wash at N = 4096 (the concurrent GEMMs slow the POTRF
+# critical path by what they save: 13.5 ms either way), so off by default.
+FUSED_INVERSE = False
 
 
 def fit_layout(kernel: KernelSpec, n_train: int, variance: str = "f64"):
@@ -258,19 +274,24 @@ def fit(kernel: KernelSpec, x, y, noise: float, jitter: float = 0.0, device=None
                             _ptr(A), n, s), "gp2d_assemble")
     dinv = torch.empty((n // NB, NB, NB), dtype=torch.float64, device=dev)
     info = torch.zeros(1, dtype=torch.int32, device=dev)
-    N.check(L.gp2d_potrf(_ptr(A), n, n, _ptr(dinv), _ptr(info), None, 0, s), "gp2d_potrf")
+    if FUSED_INVERSE:   # factor and inverse in one call, the TRTRI GEMMs overlapped with POTRF
+        wbytes = int(L.gp2d_potrf_inv_workspace(n))
+        work = torch.empty(wbytes // 8 + 1, dtype=torch.float64, device=dev)
+        N.check(L.gp2d_potrf_inv(_ptr(A), n, n, _ptr(dinv), _ptr(info), _ptr(work), wbytes, s), "gp2d_potrf_inv")
+    else:
+        N.check(L.gp2d_potrf(_ptr(A), n, n, _ptr(dinv), _ptr(info), None, 0, s), "gp2d_potrf")
+        wbytes = int(L.gp2d_trtri_workspace(n))
+        work = torch.empty(wbytes // 8 + 1, dtype=torch.float64, device=dev)
+        N.check(L.gp2d_trtri(_ptr(A), n, n, _ptr(dinv), _ptr(work), wbytes, s), "gp2d_trtri")
+    del work, dinv
     info_host = ev = None
     if not check:
+        # α (and the ozaki preparation) are enqueued before `info` is read (one host sync per
+        # fit); a failed factor raises in GPFit.check()
         info_host = _PINNED_INFO.pop() if _PINNED_INFO else torch.empty(1, dtype=torch.int32, pin_memory=True)
         info_host.copy_(info, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(dev))
-    # TRTRI and α are enqueued behind POTRF before `info` is read (one host sync per fit,
-    # no bubble between the factor and the inverse); a failed factor raises below
-    wbytes = int(L.gp2d_trtri_workspace(n))
-    work = torch.empty(wbytes // 8 + 1, dtype=torch.float64, device=dev)
-    N.check(L.gp2d_trtri(_ptr(A), n, n, _ptr(dinv), _ptr(work), wbytes, s), "gp2d_trtri")
-    del work, dinv
     Y = _pad_obs(y, ntr, npad, bd, dev)
     if perm is not None:
         for c in range(bd):

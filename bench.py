@@ -61,6 +61,10 @@ def parse():
                          "non-root ranks wait for the factor broadcast (N>1, bcast)")
     ap.add_argument("--oz-skip", type=int, default=1,
                     help="ozaki: skip the all-zero K* slabs in the int8 GEMMs (exact; 0 = dense, for A/B)")
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="issue each job's fit on a second stream, so job i+1's fit runs while job i's predict "
+                         "does (the steps are independent fit+predict jobs, like the reference's per-time-window "
+                         "krig.kriging loop); 0 = strictly one job after the other")
     ap.add_argument("--cpu-baseline", type=int, default=-1,
                     help="time the numpy oracle on the host cores (N=1 only); -1 = only when N_train <= 4096")
     ap.add_argument("--cpu-sample-points", type=int, default=2048)
@@ -149,7 +153,9 @@ def main():
     var = torch.empty(2 * m, dtype=torch.float64, device=dev)
     pred_cache = {}
     side = torch.cuda.Stream(dev) if args.variance == "ozaki" else None
-    cfg = {"mode": args.fit_mode if ws > 1 else "local", "ahead": False}
+    cfg = {"mode": args.fit_mode if ws > 1 else "local", "ahead": False,
+           "pipeline": bool(args.pipeline) and ws == 1 or (bool(args.pipeline) and args.fit_mode == "replicate"),
+           "first": True}
 
     def set_mode(mode):
         cfg["mode"] = mode
@@ -163,12 +169,27 @@ def main():
             last[0].check()
             last[0] = None
 
+    fit_stream = torch.cuda.Stream(dev)
+    main_stream = torch.cuda.current_stream(dev)
+
+    def do_fit():
+        if not cfg["pipeline"]:
+            return GD.fit_sharded(spec, xt, yt, noise, dev, mode=cfg["mode"], variance=args.variance, check=False)
+        # job i+1's fit is queued on its own stream behind job i's fit only, so it runs while
+        # job i's predict (main stream) does; the predict waits for its own fit's event
+        fit_stream.wait_stream(main_stream) if cfg["first"] else None
+        cfg["first"] = False
+        with torch.cuda.stream(fit_stream):
+            gp = GD.fit_sharded(spec, xt, yt, noise, dev, mode=cfg["mode"], variance=args.variance, check=False)
+        main_stream.wait_stream(fit_stream)
+        return gp.record_stream(main_stream)
+
     def step():
         planes = None
         if cfg["ahead"]:   # K* planes depend on (X_train, grid, kernel) only: overlap them with the fit
             planes = E.kstar_planes(spec, xt, xg, noise, chunk=args.chunk, stream=side, out=pred_cache.get("k"))
             pred_cache["k"] = planes
-        gp = GD.fit_sharded(spec, xt, yt, noise, dev, mode=cfg["mode"], variance=args.variance, check=False)
+        gp = do_fit()
         pr = pred_cache.get("p")
         if pr is None or pr.gp.n != gp.n or pr.ozaki != ("ozaki" in gp.extra):
             pr = E.Predictor(gp, args.chunk)
@@ -215,6 +236,22 @@ def main():
     elapsed = float(dt.item())
     ms_per_step = 1e3 * elapsed / args.steps
     value = m_all * args.steps / elapsed
+
+    # the same jobs strictly one after the other (secondary: the unpipelined rate)
+    serial = None
+    if cfg["pipeline"]:
+        cfg["pipeline"] = False
+        barrier(ws)
+        ts0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        check_last()
+        barrier(ws)
+        dts = torch.tensor([time.perf_counter() - ts0], dtype=torch.float64, device=dev)
+        if ws > 1:
+            dist.all_reduce(dts, op=dist.ReduceOp.MAX)
+        serial = {"value": m_all * args.steps / float(dts.item()), "ms_per_step": 1e3 * float(dts.item()) / args.steps}
+        cfg["pipeline"] = True
 
     # mean-only throughput (secondary, same fit)
     barrier(ws)
@@ -289,6 +326,8 @@ def main():
                                   (" (RCCL broadcast of packed W)" if ws > 1 and cfg["mode"] == "bcast" else ""),
                    "fit_mode_probe_ms_per_step": probe or None, "kstar_ahead": cfg["ahead"]},
         "roofline": roof,
+        "pipelined": cfg["pipeline"],
+        "serial": serial,
         "mean_only_value": mean_only,
     }
     if ws == 1 and (args.cpu_baseline > 0 or (args.cpu_baseline < 0 and args.ntrain <= 4096)):

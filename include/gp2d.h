@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define GP2D_ABI_VERSION 3
+#define GP2D_ABI_VERSION 4
 
 /* kernel families */
 #define GP2D_FAMILY_VECTOR2D 0   /* 2×2 matrix-valued SE kernels on (x1, x2)          */
@@ -99,6 +99,16 @@ int gp2d_potrf(double* A, int64_t n, int64_t lda, double* dinv, int* info_dev,
 size_t gp2d_trtri_workspace(int64_t n);
 int gp2d_trtri(double* A, int64_t n, int64_t lda, const double* dinv,
                void* work, size_t work_bytes, void* stream);
+
+/* gp2d_potrf_inv: the fit's factor in one call — A (SPD, n a multiple of 128) is
+ * replaced by W = L⁻¹ (lower, strict upper zero), the result of gp2d_potrf followed
+ * by gp2d_trtri, with the inverse's GEMMs overlapped with the factorisation (each is
+ * issued as soon as the block column that finalises its inputs is factored).
+ * Replaces np.linalg.inv(K) (GP_laser.py:118) on the fit path.  dinv (n/128 blocks of
+ * 128×128) receives the diagonal-block inverses; *info_dev as LAPACK potrf.        */
+size_t gp2d_potrf_inv_workspace(int64_t n);
+int gp2d_potrf_inv(double* A, int64_t n, int64_t lda, double* dinv, int* info_dev,
+                   void* work, size_t work_bytes, void* stream);
 
 /* gp2d_potrs_inv: alpha = Wᵀ (W y) = K_y⁻¹ y given W = L⁻¹.  Replaces
  * np.dot(Ki, y) (GP_scripts.py:45) / cho_solve (_gpr.py:360).                    */

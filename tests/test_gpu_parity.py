@@ -120,6 +120,36 @@ def test_potrf_trtri_potrs_abi(n):
     assert rel(A2.cpu().numpy(), np.linalg.inv(Lref)) < 1e-12
 
 
+@pytest.mark.parametrize("n", [128, 384, 1152, 2560, 8192])
+def test_potrf_inv_matches_two_calls(n):
+    """gp2d_potrf_inv (TRTRI GEMMs overlapped with the factorisation) is bit-identical to
+    gp2d_potrf + gp2d_trtri: the same GEMMs on the same operands, only issued earlier.  Sizes
+    cover power-of-two and ragged block counts (3, 9, 20 blocks) and the bench's n = 8192."""
+    import ctypes
+    from gp2d import _native as N
+    L_ = N.lib()
+    K = _spd(n, n + 1)
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    A1 = torch.tensor(K, device="cuda")
+    A2 = A1.clone()
+    d1 = torch.empty((n // 128, 128, 128), dtype=torch.float64, device="cuda")
+    d2 = torch.empty_like(d1)
+    i1 = torch.zeros(1, dtype=torch.int32, device="cuda")
+    i2 = torch.zeros(1, dtype=torch.int32, device="cuda")
+    N.check(L_.gp2d_potrf(P(A1), n, n, P(d1), P(i1), None, 0, s), "potrf")
+    wb = int(L_.gp2d_trtri_workspace(n))
+    work = torch.empty(wb // 8 + 1, dtype=torch.float64, device="cuda")
+    N.check(L_.gp2d_trtri(P(A1), n, n, P(d1), P(work), wb, s), "trtri")
+    wb2 = int(L_.gp2d_potrf_inv_workspace(n))
+    work2 = torch.full((wb2 // 8 + 1,), float("nan"), dtype=torch.float64, device="cuda")
+    N.check(L_.gp2d_potrf_inv(P(A2), n, n, P(d2), P(i2), P(work2), wb2, s), "potrf_inv")
+    assert int(i1.item()) == 0 and int(i2.item()) == 0
+    assert torch.equal(A1, A2) and torch.equal(d1, d2)
+    if n <= 2560:
+        assert rel(A2.cpu().numpy(), np.linalg.inv(np.linalg.cholesky(K))) < 1e-12
+
+
 @pytest.mark.parametrize("variance", ["f64", "ozaki"])
 def test_not_positive_definite_raises(variance):
     """Non-SPD K_y → LAPACK-style info → numpy.linalg.LinAlgError (np.linalg.inv / sklearn paths),

@@ -143,14 +143,14 @@ int main() {
   timeit("potrf_diag_reg (chol+inv)", [&] { hipMemcpyAsync(A, A0, n * n * 8, hipMemcpyDeviceToDevice); potrf_diag_reg_kernel<<<1, 256>>>(A, n, 0, D, info); });
   std::vector<double> Lr(n * n), Dr(n * n), Lb(n * n), Db(n * n);
   hipMemcpy(Lr.data(), A, n * n * 8, hipMemcpyDeviceToHost); hipMemcpy(Dr.data(), D, n * n * 8, hipMemcpyDeviceToHost);
-  timeit("potrf_diag blocked (chol+inv)", [&] { hipMemcpyAsync(A, A0, n * n * 8, hipMemcpyDeviceToDevice); potrf_diag_kernel<<<1, 256>>>(A, n, 0, D, info); });
+  timeit("potrf_diag blocked (chol+inv)", [&] { hipMemcpyAsync(A, A0, n * n * 8, hipMemcpyDeviceToDevice); potrf_diag_kernel<<<1, 256>>>(A, n, 0, D, info, 0); });
   hipMemcpy(Lb.data(), A, n * n * 8, hipMemcpyDeviceToHost); hipMemcpy(Db.data(), D, n * n * 8, hipMemcpyDeviceToHost);
   double eL = 0, eD = 0, mL = 0, mD = 0;
   for (int i = 0; i < n * n; ++i) { eL = std::max(eL, std::abs(Lr[i] - Lb[i])); eD = std::max(eD, std::abs(Dr[i] - Db[i])); mL = std::max(mL, std::abs(Lr[i])); mD = std::max(mD, std::abs(Dr[i])); }
   printf("blocked vs reg: L max rel diff %.2e, inv max rel diff %.2e\n", eL / mL, eD / mD);
   timeit("memcpy only", [&] { hipMemcpyAsync(A, A0, n * n * 8, hipMemcpyDeviceToDevice); });
   timeit("trti2_diag (inv only)", [&] { trti2_diag_kernel<<<1, 256>>>(A, n, D); });
-  potrf_diag_kernel<<<1, 256>>>(A, n, 0, D, info); (void)hipDeviceSynchronize();
+  potrf_diag_kernel<<<1, 256>>>(A, n, 0, D, info, 0); (void)hipDeviceSynchronize();
   unsigned long long st[16]; (void)hipMemcpyFromSymbol(st, HIP_SYMBOL(g_stamps), sizeof(st));
   printf("phases (cycles): load %llu, chol %llu, store L %llu, rdiag %llu, diag-inv %llu, offdiag-inv %llu\n", st[1]-st[0], st[2]-st[1], st[3]-st[2], st[5]-st[3], st[6]-st[5], st[4]-st[6]);
   printf("panels/trailing (cycles):"); for (int p = 0; p < 4; ++p) printf(" p%d %llu/%llu", p, st[8 + 2 * p] - (p ? st[7 + 2 * p] : st[1]), st[9 + 2 * p] - st[8 + 2 * p]); printf("\n");

@@ -1,6 +1,6 @@
 """Per-step kernel timeline from a rocprofv3 --kernel-trace CSV (dev tool).
 
-usage: python tools/timeline.py kernel_trace.csv [first_kernel_substring] [step_index]
+usage: python tools/timeline.py kernel_trace.csv|results.db [first_kernel_substring] [step_index]
 Splits the trace at every launch of the step's first kernel (default assemble_vec_kernel),
 takes step `step_index` (default −2: the last complete one) and prints, per kernel family: launches, first start, last end
 (ms from the step start) and summed duration — i.e. what overlapped with what."""
@@ -18,10 +18,16 @@ def short(name):
 
 def main(path, first="assemble_vec_kernel", index="-2"):
     rows = []
-    with open(path) as f:
-        for r in csv.DictReader(f):
-            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]),
-                         r.get("Queue_Id", r.get("Stream_Id", "?"))))
+    if path.endswith(".db"):   # rocpd SQLite output (rocprofv3's default format)
+        import sqlite3
+        c = sqlite3.connect(path)
+        for s, e, n, q in c.execute("select start, end, name, queue_id from kernels"):
+            rows.append((int(s), int(e), short(n), str(q)))
+    else:
+        with open(path) as f:
+            for r in csv.DictReader(f):
+                rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]),
+                             r.get("Queue_Id", r.get("Stream_Id", "?"))))
     rows.sort()
     starts = [i for i, r in enumerate(rows) if first in r[2]]
     if len(starts) < 2:
