@@ -312,11 +312,7 @@ __global__ __launch_bounds__(64) void ozaki_slab_list_kernel(const uint8_t* __re
 constexpr int IBM = 256, IBN = 256, IBK = 64;
 constexpr int I_OP = IBM * IBK;        // bytes per operand per stage (16 KB) = one layout tile
 constexpr int I_STAGE = 2 * I_OP;      // A then B
-#ifndef GP2D_IGEMM_NSTAGE
-#define GP2D_IGEMM_NSTAGE 4
-#endif
-constexpr int I_NSTAGE = GP2D_IGEMM_NSTAGE;   // ring stages; I_NSTAGE − 1 slabs in flight
-static_assert(I_NSTAGE == 4 || I_NSTAGE == 5, "ring depth 4 or 5 (the tail is written out for both)");
+constexpr int I_NSTAGE = 4;        // ring stages of the 256-wide shape (I_NSTAGE − 1 slabs in flight)
 
 typedef int i4v __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -327,59 +323,68 @@ __device__ __forceinline__ int swz16(int row, int chunk) {
   return chunk ^ g;
 }
 
-// s_waitcnt vmcnt(4·W) + lgkmcnt(0) + s_barrier: this wave's LDS-DMA pieces of all but the
-// W youngest slabs (4 pieces per slab per wave) have landed, then the workgroup syncs.
-template <int W>
+// s_waitcnt vmcnt(P·W) + lgkmcnt(0) + s_barrier: this wave's LDS-DMA pieces of all but the
+// W youngest slabs (P pieces per slab per wave) have landed, then the workgroup syncs.
+template <int P, int W>
 __device__ __forceinline__ void vmwait_barrier(std::integral_constant<int, W>) {
-#if defined(GP2D_IGEMM_NO_DMA) && defined(GP2D_IGEMM_NO_BARRIER)
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#else
-  if constexpr (W == 0) asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  else if constexpr (W == 1) asm volatile("s_waitcnt vmcnt(4)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  else if constexpr (W == 2) asm volatile("s_waitcnt vmcnt(8)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  else if constexpr (W == 3) asm volatile("s_waitcnt vmcnt(12)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#endif
+  static_assert(P * W < 64, "vmcnt field");
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(P * W) : "memory");
 }
 
-
 // A: M×K plane, B: N×K plane (both slab-blocked); C: column-major N×M bytes (ldc ≥ M).
-// B tiles (row block rb ≥ alias_rb, k slab s < alias_ks) are read from (rb − alias_rb,
-// s + alias_ks): the K* planes store the (v,u) block only as its equal (u,v) block.
-// alias_rb = INT_MAX disables the aliasing.
-// slist / scnt (optional, ozaki_slab_list_kernel): the K loop of B tile bj runs over the listed
-// slabs only — the others have an all-zero K* tile and add exactly nothing.  A tile whose list
-// is shorter than the ring's prologue (1 or 2 slabs) runs dense.
-__global__ __launch_bounds__(512, 1) void igemm_nt_mod_kernel(const int8_t* __restrict__ A,
-                                                              const int8_t* __restrict__ B,
-                                                              uint8_t* __restrict__ C, int64_t ldc, int M, int N,
-                                                              int K, int a_lower, int modulus, double inv_mod,
-                                                              int alias_rb, int alias_ks,
-                                                              const int* __restrict__ slist,
-                                                              const int* __restrict__ scnt) {
-  __shared__ __attribute__((aligned(16))) int8_t smem[I_NSTAGE * I_STAGE];
+// B tiles (256-row layout block rb ≥ alias_rb, k slab s < alias_ks) are read from
+// (rb − alias_rb, s + alias_ks): the K* planes store the (v,u) block only as its equal (u,v)
+// block.  alias_rb = INT_MAX disables the aliasing.
+// slist / scnt (optional, ozaki_slab_list_kernel, per 256-row B block): the K loop runs over
+// the listed slabs only — the others have an all-zero K* tile and add exactly nothing.  A tile
+// whose list is shorter than the ring's prologue runs dense.
+//
+// Two shapes (TBN = output columns per workgroup; rows are always 256 = IBM):
+//   TBN = 256: 512 threads, 8 waves as 2×4, one workgroup per CU, 4-stage ring (128 KB).
+//   TBN = 128: (alternative, measured slower — see igemm_tile_width in gp2d.hip)
+//              256 threads, 4 waves as 2×2, TWO workgroups per CU, 3-stage ring of 24 KB
+//              stages (72 KB each).  Every wave computes the same 128×64 register tile as in
+//              the 256 shape and a SIMD still holds two waves, but they belong to different
+//              workgroups, so one workgroup's epilogue (modular reduction, LDS transpose,
+//              64 KB of stores) and its successor's prologue run under the other's MFMAs
+//              instead of idling the matrix cores (the epilogue alone is ≈ 17 % of a launch
+//              on random residues, tools/microbench ablation).  Costs: 1.5× the LDS-DMA
+//              pieces per MAC (the A slab is fetched by both column halves).
+template <int TBN, int NST>
+__global__ __launch_bounds__(TBN * 2, (TBN == 256) ? 1 : 2) void igemm_nt_mod_kernel(
+    const int8_t* __restrict__ A, const int8_t* __restrict__ B, uint8_t* __restrict__ C, int64_t ldc, int M, int N,
+    int K, int a_lower, int modulus, double inv_mod, int alias_rb, int alias_ks, const int* __restrict__ slist,
+    const int* __restrict__ scnt) {
+  static_assert(TBN == 256 || TBN == 128, "tile width");
+  static_assert(NST >= 3 && NST <= 5, "ring depth 3..5 (the tail is written out for these)");
+  constexpr int NW = TBN / 32;                 // waves: 8 or 4
+  constexpr int WC = TBN / 64;                 // wave columns: 4 or 2
+  constexpr int B_OP = TBN * IBK;              // B bytes per stage
+  constexpr int STG = I_OP + B_OP;             // stage bytes: A then B
+  constexpr int AP = IBM / NW / 16;            // A pieces (16 rows × 64 B) per wave per slab: 2 or 4
+  constexpr int BPW = TBN / NW / 16;           // B pieces per wave per slab: 2
+  constexpr int PPW = AP + BPW;                // DMA pieces per wave per slab
+  __shared__ __attribute__((aligned(16))) int8_t smem[NST * STG];
   const int bj = blockIdx.x;
   const int bi = (int)(gridDim.y - 1 - blockIdx.y);   // heavy (long-K) row blocks first
-  const int i0 = bi * IBM, j0 = bj * IBN;
+  const int i0 = bi * IBM, j0 = bj * TBN;
+  const int jb = j0 / IBN, jr = j0 % IBN;             // 256-row B layout block, row offset in it
   const int ke = a_lower ? min(K, i0 + IBM) : K;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = wid >> 2, wc = wid & 3;
+  const int wr = wid / WC, wc = wid % WC;
   const int l16 = lane & 15, lq = lane >> 4;
   const int64_t kslabs = K / IBK;
   const int8_t* Ap = A + (int64_t)bi * kslabs * I_OP;   // this row block's slab tiles
-  const bool alias = bj >= alias_rb;
-  const int8_t* Bp = B + (int64_t)bj * kslabs * I_OP;
-  const int8_t* Bq = B + ((int64_t)(alias ? bj - alias_rb : 0) * kslabs + alias_ks) * I_OP;
-#ifdef GP2D_IGEMM_EPI_ONLY
-  int nsl = 0;
-#else
+  const bool alias = jb >= alias_rb;
+  const int8_t* Bp = B + (int64_t)jb * kslabs * I_OP + jr * IBK;
+  const int8_t* Bq = B + ((int64_t)(alias ? jb - alias_rb : 0) * kslabs + alias_ks) * I_OP + jr * IBK;
   int nsl = ke / IBK;
-#endif
-  const int* sl = nullptr;   // slab list of this B tile (nullptr: dense K loop)
+  const int* sl = nullptr;   // slab list of this B block (nullptr: dense K loop)
   if (slist != nullptr) {
-    const int c = scnt[(int64_t)bj * (kslabs / 4 + 1) + ke / IBM];
-    if (c == 0 || c >= I_NSTAGE - 1) {
+    const int c = scnt[(int64_t)jb * (kslabs / 4 + 1) + ke / IBM];
+    if (c == 0 || c >= NST - 1) {
       nsl = c;
-      sl = slist + (int64_t)bj * kslabs;
+      sl = slist + (int64_t)jb * kslabs;
     }
   }
 
@@ -389,31 +394,30 @@ __global__ __launch_bounds__(512, 1) void igemm_nt_mod_kernel(const int8_t* __re
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = i4v{0, 0, 0, 0};
 
-  // wave w moves rows [32w, 32w+32) of both operands: 2 contiguous 1 KB pieces each
+  // wave w moves A rows [16·AP·w, +16·AP) and B rows [32w, 32w+32): contiguous 1 KB pieces
   const int drow = lane >> 2, dchunk = lane & 3;
   // ks: the K slab (already mapped through the list) loaded into ring stage st
   auto issue = [&](int ks, int st) {
-#ifdef GP2D_IGEMM_NO_DMA
-    return;
-#endif
-    int8_t* As = smem + st * I_STAGE;
+    int8_t* As = smem + st * STG;
     int8_t* Bs = As + I_OP;
     const int8_t* Ag = Ap + (int64_t)ks * I_OP;
     const int8_t* Bg = ((alias && ks < alias_ks) ? Bq : Bp) + (int64_t)ks * I_OP;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int row = wid * 32 + h * 16 + drow;
-      const int off = row * IBK + 16 * swz16(row, dchunk);
-      __builtin_amdgcn_global_load_lds((const void*)(Ag + off), (lds_ptr_t)(As + (wid * 32 + h * 16) * IBK), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(Bg + off), (lds_ptr_t)(Bs + (wid * 32 + h * 16) * IBK), 16, 0, 0);
+    for (int h = 0; h < AP; ++h) {
+      const int row = (wid * AP + h) * 16 + drow;
+      __builtin_amdgcn_global_load_lds((const void*)(Ag + row * IBK + 16 * swz16(row, dchunk)),
+                                       (lds_ptr_t)(As + (wid * AP + h) * 16 * IBK), 16, 0, 0);
+    }
+#pragma unroll
+    for (int h = 0; h < BPW; ++h) {
+      const int row = (wid * BPW + h) * 16 + drow;   // swizzle by the row within the 256 block
+      __builtin_amdgcn_global_load_lds((const void*)(Bg + row * IBK + 16 * swz16(jr + row, dchunk)),
+                                       (lds_ptr_t)(Bs + (wid * BPW + h) * 16 * IBK), 16, 0, 0);
     }
   };
   const uint32_t lds_base = (uint32_t)(size_t)(lds_ptr_t)smem;
   auto reada = [&](int st, int half, i4v (&a)[4]) {  // A fragments mi = 4·half .. 4·half+3
-#ifdef GP2D_IGEMM_NO_LDSREAD
-    return;
-#endif
-    const uint32_t As = lds_base + st * I_STAGE;
+    const uint32_t As = lds_base + st * STG;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int row = wr * 128 + (4 * half + u) * 16 + l16;
@@ -422,22 +426,15 @@ __global__ __launch_bounds__(512, 1) void igemm_nt_mod_kernel(const int8_t* __re
     }
   };
   auto readb = [&](int st, i4v (&b)[4]) {
-#ifdef GP2D_IGEMM_NO_LDSREAD
-    return;
-#endif
-    const uint32_t Bs = lds_base + st * I_STAGE + I_OP;
+    const uint32_t Bs = lds_base + st * STG + I_OP;
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) {
       const int row = wc * 64 + ni * 16 + l16;
-      const uint32_t ad = Bs + row * IBK + 16 * swz16(row, lq);
+      const uint32_t ad = Bs + row * IBK + 16 * swz16(jr + row, lq);
       asm volatile("ds_read_b128 %0, %1" : "=v"(b[ni]) : "v"(ad) : "memory");
     }
   };
   auto mfmas = [&](int half, const i4v (&a)[4], const i4v (&b)[4]) {
-#ifdef GP2D_IGEMM_NO_MFMA
-    acc[0][0][0] += a[0][0] ^ b[0][0];
-    return;
-#endif
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
@@ -451,34 +448,30 @@ __global__ __launch_bounds__(512, 1) void igemm_nt_mod_kernel(const int8_t* __re
   auto slab = [&](int s) -> int { return sl ? ((const_int_ptr)sl)[min(s, nsl - 1)] : s; };
   if (nsl > 0) {
 #pragma unroll
-    for (int q = 0; q < I_NSTAGE - 1; ++q) issue(slab(q), q);
-    int knext = slab(I_NSTAGE - 1);
-    vmwait_barrier(std::integral_constant<int, I_NSTAGE - 2>{});   // slab 0 landed (nsl ≥ 4 ≥ I_NSTAGE − 1)
+    for (int q = 0; q < NST - 1; ++q) issue(slab(q), q);
+    int knext = slab(NST - 1);
+    vmwait_barrier<PPW>(std::integral_constant<int, NST - 2>{});   // slab 0 landed (nsl ≥ NST − 1)
     // Per slab: MFMA half 0 (A rows 0-63 of the wave) → barrier publishing slab s+1 → reads
     // of slab s+1's B and A-half-0 fragments into the other register set → MFMA half 1.
-    // Both waves of a SIMD leave the barrier together, so the next slab's first fragments
-    // must already be in flight behind half 1's 16 MFMAs rather than be read after it.
+    // Both waves of a workgroup on a SIMD leave the barrier together, so the next slab's first
+    // fragments must already be in flight behind half 1's 16 MFMAs rather than be read after it.
     i4v bA[4], a0A[4], bB[4], a0B[4], a1[4];
-#ifdef GP2D_IGEMM_NO_LDSREAD
-#pragma unroll
-    for (int u = 0; u < 4; ++u) bA[u] = a0A[u] = bB[u] = a0B[u] = a1[u] = i4v{lane, u, wid, 1};
-#endif
     readb(0, bA);
     reada(0, 0, a0A);
     __builtin_amdgcn_sched_barrier(0);
-    // Step kinds: FULL steps issue slab s + I_NSTAGE − 1 and publish s+1 leaving the younger
-    // I_NSTAGE − 2 slabs in flight; the tail steps issue nothing and leave W = I_NSTAGE−3 .. 0
-    // slabs in flight; the LAST step has no barrier.  The steady-state loop runs only FULL
-    // steps, unrolled by two for the register ping-pong, so it carries no per-slab branches.
+    // Step kinds: FULL steps issue slab s + NST − 1 and publish s+1 leaving the younger
+    // NST − 2 slabs in flight; the tail steps issue nothing and leave W = NST−3 .. 0 slabs in
+    // flight; the LAST step has no barrier.  The steady-state loop runs only FULL steps,
+    // unrolled by two for the register ping-pong, so it carries no per-slab branches.
     constexpr int LAST = -1;
     auto step = [&](auto dma_c, auto w_c, int s, i4v (&b)[4], i4v (&a0)[4], i4v (&bn)[4], i4v (&a0n)[4]) {
       constexpr bool dma = decltype(dma_c)::value;
       constexpr int w = decltype(w_c)::value;
-      const int st = s % I_NSTAGE;
+      const int st = s % NST;
       // the stage written is slab s−1's: nobody reads it after the previous barrier
       if constexpr (dma) {
-        issue(knext, (s + I_NSTAGE - 1) % I_NSTAGE);
-        knext = slab(s + I_NSTAGE);
+        issue(knext, (s + NST - 1) % NST);
+        knext = slab(s + NST);
       }
       reada(st, 1, a1);
       asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");  // b, a0 landed
@@ -486,8 +479,8 @@ __global__ __launch_bounds__(512, 1) void igemm_nt_mod_kernel(const int8_t* __re
       mfmas(0, a0, b);
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (w != LAST) {
-        vmwait_barrier(w_c);   // publish slab s+1 (lgkmcnt(0) inside: a1 landed)
-        const int st1 = (s + 1) % I_NSTAGE;
+        vmwait_barrier<PPW>(w_c);   // publish slab s+1 (lgkmcnt(0) inside: a1 landed)
+        const int st1 = (s + 1) % NST;
         readb(st1, bn);
         reada(st1, 0, a0n);
         asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");  // nothing older than the 8 new reads
@@ -500,8 +493,8 @@ __global__ __launch_bounds__(512, 1) void igemm_nt_mod_kernel(const int8_t* __re
     };
     using T_ = std::true_type;
     using F_ = std::false_type;
-    using W_FULL = std::integral_constant<int, I_NSTAGE - 2>;
-    const int m = nsl - (I_NSTAGE - 1);   // FULL steps
+    using W_FULL = std::integral_constant<int, NST - 2>;
+    const int m = nsl - (NST - 1);   // FULL steps
     int s = 0;
     for (; s + 1 < m; s += 2) {
       step(T_{}, W_FULL{}, s, bA, a0A, bB, a0B);
@@ -516,25 +509,34 @@ __global__ __launch_bounds__(512, 1) void igemm_nt_mod_kernel(const int8_t* __re
         a0A[u] = a0B[u];
       }
     }
-    // tail: I_NSTAGE − 1 steps, W = I_NSTAGE−3, ..., 0, then LAST
-    if constexpr (I_NSTAGE == 5) {
+    // tail: NST − 1 steps, W = NST−3, ..., 0, then LAST
+    if constexpr (NST == 5) {
       step(F_{}, std::integral_constant<int, 2>{}, s, bA, a0A, bB, a0B);
       step(F_{}, std::integral_constant<int, 1>{}, s + 1, bB, a0B, bA, a0A);
       step(F_{}, std::integral_constant<int, 0>{}, s + 2, bA, a0A, bB, a0B);
       step(F_{}, std::integral_constant<int, LAST>{}, s + 3, bB, a0B, bA, a0A);
-    } else {
+    } else if constexpr (NST == 4) {
       step(F_{}, std::integral_constant<int, 1>{}, s, bA, a0A, bB, a0B);
       step(F_{}, std::integral_constant<int, 0>{}, s + 1, bB, a0B, bA, a0A);
       step(F_{}, std::integral_constant<int, LAST>{}, s + 2, bA, a0A, bB, a0B);
+    } else {
+      step(F_{}, std::integral_constant<int, 0>{}, s, bA, a0A, bB, a0B);
+      step(F_{}, std::integral_constant<int, LAST>{}, s + 1, bB, a0B, bA, a0A);
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
-  // Epilogue: residues mod m (fp32 quotient estimate, exact int correction), packed 4 rows
-  // per dword into an LDS image of Cᵀ [col][row] (pitch 272 B), then written out as
-  // coalesced 16-B row runs of the column-major residue plane.
+  // Epilogue: residues mod m, packed 4 rows per dword into an LDS image of Cᵀ [col][row]
+  // (pitch 272 B), then written out as coalesced 16-B row runs of the column-major residue
+  // plane.  Full-rate VALU only (no v_mul_lo_u32): v = vh·2^16 + vl with vl ∈ [0, 2^16), so
+  // v ≡ y = vh·(2^16 mod m) + vl with |y| < 2^23 + 2^16 (|vh| < 2^15 for any int32 v): y is
+  // exact in fp32 and both products fit the 24-bit multiplier; q = ⌊y/m⌋ from the fp32
+  // quotient is off by at most one, so r = y − q·m ∈ [−m, 2m) and two unsigned-min steps
+  // (r < 0 → r + m, then r ≥ m → r − m) finish the reduction.
   uint8_t* T = reinterpret_cast<uint8_t*>(smem);
   constexpr int TP = IBM + 16;
+  static_assert(TBN * TP <= NST * STG, "epilogue image fits the ring");
   const float fim = (float)inv_mod;
+  const int c16 = 65536 % modulus;
 #pragma unroll
   for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
@@ -543,11 +545,14 @@ __global__ __launch_bounds__(512, 1) void igemm_nt_mod_kernel(const int8_t* __re
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int v = acc[mi][ni][u];
-        const int q = (int)floorf((float)v * fim);     // off by at most one
-        int res = v - q * modulus;
-        res += (res < 0) ? modulus : 0;
-        res -= (res >= modulus) ? modulus : 0;
-        pk |= (uint32_t)res << (8 * u);
+        int y, q, r;
+        asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(y) : "v"(v >> 16), "s"(c16), "v"(v & 0xffff));
+        asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(q) : "v"((float)y * fim));
+        asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(q), "s"(-modulus), "v"(y));
+        const uint32_t r0 = (uint32_t)r;
+        const uint32_t r1 = min(r0, r0 + (uint32_t)modulus);
+        const uint32_t res = min(r1, r1 - (uint32_t)modulus);
+        pk |= res << (8 * u);
       }
       const int rloc = wr * 128 + mi * 16 + 4 * lq;
       const int cloc = wc * 64 + ni * 16 + l16;
@@ -555,8 +560,8 @@ __global__ __launch_bounds__(512, 1) void igemm_nt_mod_kernel(const int8_t* __re
     }
   __syncthreads();
 #pragma unroll
-  for (int p = 0; p < (IBM * IBN / 16) / 512; ++p) {
-    const int id = tid + 512 * p;
+  for (int p = 0; p < (IBM * TBN / 16) / (TBN * 2); ++p) {
+    const int id = tid + TBN * 2 * p;
     const int cloc = id >> 4, ch = id & 15;
     const uint4 v = *reinterpret_cast<const uint4*>(T + cloc * TP + 16 * ch);
     *reinterpret_cast<uint4*>(C + (int64_t)(j0 + cloc) * ldc + i0 + 16 * ch) = v;

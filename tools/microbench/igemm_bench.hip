@@ -1,8 +1,8 @@
 // The int8 NT GEMM of ozaki.hpp in isolation on random residues (dev tool): time per
 // 8192×16384×8192 lower-triangular launch, and 4096 sampled outputs checked against a
-// CPU dot product.  Build variants with -DGP2D_IGEMM_NO_DMA / -DGP2D_IGEMM_NO_MFMA.
-#include "../../2d-gp_amd/csrc/ozaki.hpp"
-#include "igemm_v2.hpp"
+// CPU dot product.  FULL = the product kernel; the ablation variants build the dev copy
+// (igemm_ablate.hpp) with -DGP2D_IGEMM_NO_DMA / NO_MFMA / NO_LDSREAD / EPI_ONLY.
+#include "igemm_ablate.hpp"
 #include <cstdio>
 #include <random>
 #include <vector>
@@ -10,8 +10,14 @@
 #include <cstdlib>
 namespace gp2d { void set_error(const std::string&) {} }
 using namespace gp2d;
+#ifndef IG_TBN
+#define IG_TBN 256
+#endif
+#ifndef IG_NST
+#define IG_NST 4
+#endif
 #ifndef IGEMM_KERNEL
-#define IGEMM_KERNEL igemm_nt_mod_kernel
+#define IGEMM_KERNEL igemm_nt_mod_kernel<IG_TBN, IG_NST>
 #define IGEMM_EXTRA , nullptr, nullptr   // dense K loop (no slab list)
 #endif
 #ifndef IGEMM_EXTRA
@@ -34,8 +40,8 @@ int main() {
   (void)hipMemcpy(dA, Ab.data(), A.size(), hipMemcpyHostToDevice);
   (void)hipMemcpy(dB, Bb.data(), B.size(), hipMemcpyHostToDevice);
   hipEvent_t e0, e1; (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
-  const dim3 g(nc / IBN, n / IBM);
-  auto launch = [&]() { IGEMM_KERNEL<<<g, 512>>>(dA, dB, dC, n, n, nc, n, 1, mod, 1.0 / mod, 1 << 30, 0 IGEMM_EXTRA); };
+  const dim3 g(nc / IG_TBN, n / IBM);
+  auto launch = [&]() { IGEMM_KERNEL<<<g, 2 * IG_TBN>>>(dA, dB, dC, n, n, nc, n, 1, mod, 1.0 / mod, 1 << 30, 0 IGEMM_EXTRA); };
   for (int w = 0; w < 3; ++w) launch();
   (void)hipDeviceSynchronize();
   (void)hipEventRecord(e0);
