@@ -90,7 +90,7 @@ def test_lml_grad_deterministic():
 
 
 def test_lml_grad_full_size_fd():
-    """Config B size (N=4096, div-free): the analytic gradient against a central difference of
+    """Headline / config C size (N=4096, div-free): the analytic gradient against a central difference of
     the GPU LML itself (size-independent property; step 1e-5 relative)."""
     x, y = tracks(4096, seed=11)
     noise = 0.0025
