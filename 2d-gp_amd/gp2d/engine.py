@@ -241,8 +241,14 @@ def _raise_fit_errors(inf: int, err):
 
 
 def fit(kernel: KernelSpec, x, y, noise: float, jitter: float = 0.0, device=None, variance: str = "f64",
-        check: bool = True) -> GPFit:
+        check: bool = True, jitchol: int = 0) -> GPFit:
     """K_y = K(x,x) + (noise+jitter)·I → L = chol(K_y) → W = L⁻¹ → α = Wᵀ W y.
+
+    jitchol = k > 0: GPy's jitchol retry (GPy.util.linalg.jitchol, maxtries = k; GPy is not
+    installed here, so this follows its published algorithm and is parity-unpinned): if K_y is
+    not positive definite, refit with an extra diagonal jitter of mean(diag K_y)·1e-6, ten times
+    larger on each further try, up to k tries, then raise LinAlgError.  The jitter that succeeded
+    is gp.extra['jitchol'] (0.0 when the first factorisation did).  Implies check=True.
 
     variance: 'f64'   — predictive variance by the FP64-MFMA contraction;
               'ozaki' — the same contraction emulated exactly on the INT8 matrix cores
@@ -251,6 +257,26 @@ def fit(kernel: KernelSpec, x, y, noise: float, jitter: float = 0.0, device=None
     reference's np.linalg.inv / GPy jitchol / sklearn error paths).  check=False returns
     without waiting for the factor (no host sync); the error is raised by GPFit.check().
     """
+    if jitchol:
+        try:
+            gp = fit(kernel, x, y, noise, jitter=jitter, device=device, variance=variance)
+            gp.extra["jitchol"] = 0.0
+            return gp
+        except np.linalg.LinAlgError:
+            diag = float(N.lib().gp2d_kernel_diag(ctypes.byref(kernel.desc()))) + noise + jitter
+            if not diag > 0.0:
+                raise np.linalg.LinAlgError("not pd: non-positive diagonal elements") from None
+            jit = diag * 1e-6
+            for _ in range(int(jitchol)):
+                if not np.isfinite(jit):
+                    break
+                try:
+                    gp = fit(kernel, x, y, noise, jitter=jitter + jit, device=device, variance=variance)
+                    gp.extra["jitchol"] = jit
+                    return gp
+                except np.linalg.LinAlgError:
+                    jit *= 10.0
+            raise np.linalg.LinAlgError("not positive definite, even with jitter.") from None
     if variance not in VARIANCE_ENGINES:
         raise ValueError(f"variance must be one of {VARIANCE_ENGINES}")
     if variance == "ozaki" and not kernel.is_vector:

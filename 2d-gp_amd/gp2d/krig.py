@@ -27,6 +27,7 @@ from __future__ import annotations
 import os
 import time
 from dataclasses import dataclass
+from datetime import datetime, timedelta
 
 import numpy as np
 import torch
@@ -82,8 +83,9 @@ class Krig:
 
     def __init__(self, kernel="df", l_df: float = 5.0, l_cf: float = 5.0, ratio: float = None,
                  noise: float = 0.0025, jitter: float = 0.0, var_mode: str = "latent", device=None,
-                 chunk: int = 8192, variance: str = "f64"):
+                 chunk: int = 8192, variance: str = "f64", jitchol: int = 0):
         self.spec = self._make_spec(kernel, l_df, l_cf, ratio)
+        self.jitchol = int(jitchol)   # GPy jitchol retries on a non-PD K_y (engine.fit)
         if variance not in E.VARIANCE_ENGINES:
             raise ValueError(f"variance must be one of {E.VARIANCE_ENGINES}")
         self.variance = variance
@@ -118,7 +120,7 @@ class Krig:
         if bd == 2 and not isinstance(y, torch.Tensor) and y.ndim == 2 and y.shape[1] == 2:
             y = np.concatenate([y[:, 0], y[:, 1]])
         self.gp = E.fit(self.spec, X, y, self.noise, jitter=self.jitter, device=self.device,
-                        variance=self.variance)
+                        variance=self.variance, jitchol=self.jitchol)
         self._pred = E.Predictor(self.gp, self.chunk)
         self._X, self._y = X, y
         return self
@@ -552,24 +554,51 @@ def _prior_window(fm, tcenter, tlim, xlim, xrange, varname):
     return XT, np.concatenate([obs[:, col], obst[:, col]])
 
 
+RADAR_T0 = datetime(2016, 1, 1)             # radar time origin (days), krig.py:110
+RADAR_T0D = datetime(2016, 2, 7, 2, 15)     # first time of Filtered_2016_2_7.pkl, krig.py:111
+
+
+def radar_grid(radar):
+    """The HF-radar grid branch of scikit_prior (krig.py:98-118): the radar NetCDF's image
+    origin (imageOriginPosition = lon, lat) projected and shifted to the drifter frame in km,
+    plus its xCoords / yCoords (m); the first radar time, counted in days from 2016-01-01,
+    becomes hours since the drifter data's first time.  Returns (X (M, 3) in T, Y, X order,
+    tcenter, yg, xg) with the meshgrid(yg, tg, xg) flattening of krig.py:114-118.
+    Reference quirk: that branch never sets `tcenter`, which krig.py:143 then reads (NameError);
+    the build takes the radar time tg as the window centre, the evident intent."""
+    R = NC.readNC(radar)
+    lon_r, lat_r = (float(v) for v in np.asarray(R["imageOriginPosition"], dtype=np.float64).reshape(-1)[:2])
+    x0, y0 = nad83(lon_r, lat_r)
+    x0 = (x0 - x_ori) / 1000.0
+    y0 = (y0 - y_ori) / 1000.0
+    xg = x0 + np.asarray(R["xCoords"], dtype=np.float64) / 1000.0
+    yg = y0 + np.asarray(R["yCoords"], dtype=np.float64) / 1000.0
+    tr = np.asarray(R["time"], dtype=np.float64).reshape(-1)
+    tg = np.array([(RADAR_T0 + timedelta(float(tr[0])) - RADAR_T0D).total_seconds() / 3600])
+    Yg, Tg, Xg = np.meshgrid(yg, tg, xg)
+    X = np.concatenate([Tg.reshape(-1, 1), Yg.reshape(-1, 1), Xg.reshape(-1, 1)], axis=1)
+    return X, tg, yg, xg
+
+
 def scikit_prior(filename0, varname="v", dt=0, tlim=6, radar="", xlim=(0, 0), ylim=(0, 0), dx=0, ind=0, xrange=3,
                  HP=None, device=None):
     """krig.scikit_prior (krig.py:88-207): fixed-hyperparameter scalar GP
     HP0·RBF([lt,ly,lx]) (+ HP4·RBF) + White(noise) on the windowed observations,
-    predicted at time dt on the getGrid window (xlim/ylim given) or on the grid of a
-    pre-existing filename0+'.nc' (krig.py:123-141).  Model inputs come from
+    predicted on a radar NetCDF's grid (radar=path, radar_grid, krig.py:98-118), at time dt
+    on the getGrid window (xlim/ylim given) or on the grid of a pre-existing
+    filename0+'.nc' (krig.py:123-141).  Model inputs come from
     filename0+'.npz' (written by kriging); HP = [var1, lt, ly, lx, (var2, lt, ly, lx,) noise]
     (the GPy param_array the reference loads at krig.py:159-161).
     Writes <filename>_<t>h_scikit_<ind>.nc (createNC if absent, then varname, varname+'var',
     hyperparam_<varname>, krig.py:197-206) and returns (U, Ustd²) reshaped [1, yg, xg]."""
-    if radar:
-        raise NotImplementedError("radar grids need the radar NetCDF files and the NAD83 projection "
-                                  "(pyproj), neither of which exists here")
     fm = np.load(filename0 + ".npz", allow_pickle=False)
     if HP is None:
         raise ValueError("HP (hyperparameters) is required: the reference reads them from a GPy pickle")
     HP = np.asarray(HP, dtype=np.float64)
-    if (xlim[1] > xlim[0]) and (ylim[1] > ylim[0]):
+    if radar:                                                         # krig.py:98-118
+        X, tcenter, yg, xg = radar_grid(radar)
+        filename = filename0 + "_radar"
+    elif (xlim[1] > xlim[0]) and (ylim[1] > ylim[0]):
         X, tcenter, yg, xg = getGrid([dt, dt + 1], ylim, xlim, 1, dx)   # krig.py:121
         filename = filename0 + "_cyc"
     else:                                                             # krig.py:123-141

@@ -1,4 +1,6 @@
 """The reference-compatible surface (krig / kern) on the GPU vs golden vectors and the oracle."""
+import os
+
 import numpy as np
 import pytest
 
@@ -158,3 +160,36 @@ def test_kriging_predict_pipeline(tmp_path):
     d = ncio.readNC(outf)
     assert np.array_equal(d["v"], U0.astype(np.float32)) and np.array_equal(d["vvar"], S0.astype(np.float32))
     assert np.array_equal(d["hyperparam_v"], HP.astype(np.float32))
+
+
+def test_scikit_prior_radar_branch(tmp_path):
+    """scikit_prior on an HF-radar grid (krig.py:98-118 + the fit/predict/NetCDF of 146-206):
+    the grid comes from a synthetic radar NetCDF written by gp2d.ncio; the posterior is checked
+    against the oracle ARD model on the same window and grid (1e-10)."""
+    from test_ncio_cpu import _write_radar
+    rng = np.random.default_rng(5)
+    xc = np.arange(0.0, 12000.0, 2000.0)
+    yc = np.arange(0.0, 10000.0, 2000.0)
+    radar = str(tmp_path / "radar.nc")
+    _write_radar(radar, -88.55, 28.85, xc, yc, 37.5)
+    Xr, tg, yg, xg = krig.radar_grid(radar)
+    n, m = 150, 40
+    Xo = np.stack([tg[0] + rng.uniform(-8, 8, n), rng.uniform(yg[0] - 3, yg[-1] + 3, n),
+                   rng.uniform(xg[0] - 3, xg[-1] + 3, n)], 1)
+    Xt = np.stack([tg[0] + rng.uniform(-8, 8, m), rng.uniform(yg[0], yg[-1], m), rng.uniform(xg[0], xg[-1], m)], 1)
+    obs = np.stack([np.sin(Xo[:, 1] / 4), np.cos(Xo[:, 2] / 5)], 1) + rng.normal(0, 0.05, (n, 2))
+    tp = np.stack([np.sin(Xt[:, 1] / 4), np.cos(Xt[:, 2] / 5)], 1)
+    f0 = str(tmp_path / "res" / "model")
+    os.makedirs(os.path.dirname(f0))
+    np.savez(f0 + ".npz", Xo=Xo, Xt=Xt, obs=obs, test_points=tp)
+    HP = np.array([0.5, 6.0, 3.0, 4.0, 0.004])
+    U, S = krig.scikit_prior(f0, varname="u", radar=radar, HP=HP, xrange=1000.0)
+    assert U.shape == (1, yg.size, xg.size)
+    sel = lambda T: np.where((T[:, 0] >= tg[0] - 6) & (T[:, 0] <= tg[0] + 6))[0]   # tlim 6, all x
+    XT = np.concatenate([Xo[sel(Xo)], Xt[sel(Xt)]])
+    u = np.concatenate([obs[sel(Xo), 1], tp[sel(Xt), 1]])
+    mo, so = O.ard_fit_predict(XT, u, Xr, [0.5], [(6.0, 3.0, 4.0)], 0.004, jitter=1e-10)
+    assert rel(U.reshape(-1), mo) < 1e-10 and rel(S.reshape(-1), so ** 2) < 1e-10
+    out = f0 + "_radar_" + str(np.round(tg[0], decimals=2)) + "h_scikit_0.nc"
+    d = ncio.readNC(out)
+    assert np.array_equal(d["u"], U.astype(np.float32)) and np.array_equal(d["uvar"], S.astype(np.float32))

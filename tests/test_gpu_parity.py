@@ -184,3 +184,31 @@ def test_sharded_predict_bit_identical():
         from gp2d.distributed import assemble_from_shards
         assert np.array_equal(assemble_from_shards(xg.shape[0], 2, shards_m), m_all)
         assert np.array_equal(assemble_from_shards(xg.shape[0], 2, shards_v), v_all)
+
+
+@pytest.mark.parametrize("variance", ["f64", "ozaki"])
+def test_jitchol_retry(variance):
+    """GPy jitchol semantics (GPy.util.linalg.jitchol; GPy absent here — parity unpinned, the
+    published algorithm): a singular K_y (repeated points, no noise) fails without the option;
+    with jitchol=5 the fit succeeds with jitter = mean(diag K_y)·1e-6·10^t for the first
+    try t that factors, and equals a plain fit with that jitter bit for bit."""
+    rng = np.random.default_rng(4)
+    x = rng.uniform(0, 20, (60, 2))
+    x = np.concatenate([x, x[:5]])   # five repeated points: K is singular
+    y = rng.normal(size=2 * x.shape[0])
+    ks = E.KernelSpec(kind="df", l_df=3.0)
+    with pytest.raises(np.linalg.LinAlgError):
+        E.fit(ks, x, y, noise=0.0, variance=variance)
+    gp = E.fit(ks, x, y, noise=0.0, variance=variance, jitchol=5)
+    jit = gp.extra["jitchol"]
+    base = (1.0 / 9.0) * 1e-6                       # mean(diag K_y) = 1/ℓ² for the div-free kernel
+    ratios = [jit / (base * 10 ** t) for t in range(5)]
+    assert any(abs(r - 1.0) < 1e-12 for r in ratios), jit
+    ref = E.fit(ks, x, y, noise=0.0, jitter=jit, variance=variance)
+    assert torch.equal(gp.W, ref.W) and torch.equal(gp.alpha, ref.alpha)
+    xg = rng.uniform(0, 20, (300, 2))
+    a, b = E.predict(gp, xg), E.predict(ref, xg)
+    assert torch.equal(a[0], b[0])
+    assert torch.equal(a[1], b[1]) or variance == "ozaki"   # (the ozaki CRT may poison both alike: NaN ≠ NaN)
+    # a well-posed fit reports no jitter
+    assert E.fit(ks, x[:60], y[:120], noise=0.01, variance=variance, jitchol=5).extra["jitchol"] == 0.0

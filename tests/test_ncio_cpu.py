@@ -109,3 +109,39 @@ def test_own_attributes_and_types_roundtrip(tmp_path):
         assert np.array_equal(f.variables["d"][:], [1.5, 2.5, 3.5])
         assert f.variables["d"].scale == 2.0
         assert np.array_equal(f.variables["s"][:], [[1, 2, 3], [4, 5, 6]])
+
+
+def _write_radar(path, lon, lat, xc, yc, t_days):
+    """A synthetic HF-radar file with the variables krig.scikit_prior reads (krig.py:99-108)."""
+    with ncio.NCFile(path, "w") as f:
+        f.createDimension("two", 2)
+        f.createDimension("x", xc.size)
+        f.createDimension("y", yc.size)
+        f.createDimension("time", None)
+        f.createVariable("imageOriginPosition", "f8", ("two",))[:] = np.array([lon, lat])
+        f.createVariable("xCoords", "f8", ("x",))[:] = xc
+        f.createVariable("yCoords", "f8", ("y",))[:] = yc
+        f.createVariable("time", "f8", ("time",))[:] = np.array([t_days])
+        f.createVariable("ux", "f4", ("time", "y", "x"))[:] = np.zeros((1, yc.size, xc.size), np.float32)
+        f.createVariable("uy", "f4", ("time", "y", "x"))[:] = np.zeros((1, yc.size, xc.size), np.float32)
+
+
+def test_radar_grid_branch(tmp_path):
+    """scikit_prior's radar grid (krig.py:98-118) from a radar NetCDF written here: origin
+    projected (the documented NAD83 stand-in) and shifted to the drifter frame in km, xCoords /
+    yCoords in m, time in days since 2016-01-01 → hours since 2016-02-07 02:15, meshgrid
+    (yg, tg, xg) flattening."""
+    import krig as K
+    from datetime import datetime, timedelta
+    p = str(tmp_path / "radar.nc")
+    xc = np.arange(0.0, 9000.0, 1500.0)
+    yc = np.arange(-2000.0, 4000.0, 1000.0)
+    _write_radar(p, -88.5, 28.9, xc, yc, 37.25)
+    X, tg, yg, xg = K.radar_grid(p)
+    x0, y0 = K.nad83(-88.5, 28.9)
+    assert np.allclose(xg, (x0 - K.x_ori) / 1000.0 + xc / 1000.0, rtol=0, atol=1e-12)
+    assert np.allclose(yg, (y0 - K.y_ori) / 1000.0 + yc / 1000.0, rtol=0, atol=1e-12)
+    hours = (datetime(2016, 1, 1) + timedelta(37.25) - datetime(2016, 2, 7, 2, 15)).total_seconds() / 3600
+    assert tg.shape == (1,) and tg[0] == hours
+    assert X.shape == (yg.size * xg.size, 3) and np.all(X[:, 0] == hours)
+    assert np.array_equal(X[:xg.size, 2], xg) and np.all(X[:xg.size, 1] == yg[0])
