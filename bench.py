@@ -223,8 +223,13 @@ def main():
     E.timing_read()
     barrier(ws)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    trace = os.environ.get("GP2D_BENCH_TRACE") == "1"   # per-step wall times on stderr (diagnostics)
+    for i in range(args.steps):
         step()
+        if trace:
+            torch.cuda.synchronize()
+            print(f"[rank {rank}] step {i}: {1e3 * (time.perf_counter() - t0):.1f} ms since start", file=sys.stderr,
+                  flush=True)
     check_last()
     barrier(ws)
     t1 = time.perf_counter()
@@ -279,7 +284,7 @@ def main():
     achieved = kflops / (kms * 1e-3) / 1e12 if kms > 0 else None
     traffic = None   # the committed PMC pass was taken at the headline workload only
     headline = (args.kind, args.ntrain, G, strong) == ("df", 4096, 256, False)
-    pmc_json = args.pmc_json or os.path.join(ROOT, "profiles", f"r01_pmc_traffic_{args.variance}.json")
+    pmc_json = args.pmc_json or os.path.join(ROOT, "profiles", f"r02_pmc_traffic_{args.variance}.json")
     try:
         with open(pmc_json) as f:
             pmc = json.load(f)
