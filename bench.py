@@ -242,31 +242,6 @@ def main():
     ms_per_step = 1e3 * elapsed / args.steps
     value = m_all * args.steps / elapsed
 
-    # the same jobs strictly one after the other (secondary: the unpipelined rate).  One rank
-    # only: with two ranks sharing one card (the rehearsal setup) this phase, run after the
-    # pipelined one, slowed to 1.5-2 s per step although either phase alone runs at the
-    # expected 2 x 63 ms
-    serial = None
-    if cfg["pipeline"] and ws == 1:
-        cfg["pipeline"] = False
-        barrier(ws)
-        E.timing_enable(True)
-        E.timing_read()
-        ts0 = time.perf_counter()
-        for _ in range(args.steps):
-            step()
-        check_last()
-        barrier(ws)
-        dts = torch.tensor([time.perf_counter() - ts0], dtype=torch.float64, device=dev)
-        skms, sklaunch, _ = E.timing_read()
-        E.timing_enable(False)
-        if ws > 1:
-            dist.all_reduce(dts, op=dist.ReduceOp.MAX)
-        # the dominant kernel's launch time without a concurrent fit (its roofline alone)
-        serial = {"value": m_all * args.steps / float(dts.item()), "ms_per_step": 1e3 * float(dts.item()) / args.steps,
-                  "dominant_kernel_ms": skms, "dominant_kernel_launches": sklaunch}
-        cfg["pipeline"] = True
-
     # mean-only throughput (secondary, same fit)
     barrier(ws)
     t2 = time.perf_counter()
@@ -311,10 +286,6 @@ def main():
                 "dense_equivalent_tops": achieved * nmod if achieved else None,
                 "fp64_equivalent_tflops": achieved, "fp64_equivalent_frac_of_fp64_peak":
                     (achieved / FP64_PEAK_TFLOPS) if achieved else None}
-        if serial and serial["dominant_kernel_ms"] > 0 and ex:
-            # the same launches in the unpipelined run (no fit competing for the CUs)
-            ex_serial = ex * (kms / klaunch) * (serial["dominant_kernel_launches"] / serial["dominant_kernel_ms"])
-            roof["frac_unpipelined"] = ex_serial / INT8_PEAK_TOPS
     else:
         roof = {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": (achieved / FP64_PEAK_TFLOPS) if achieved else None, "traffic": traffic,
@@ -345,7 +316,6 @@ def main():
                    "fit_mode_probe_ms_per_step": probe or None, "kstar_ahead": cfg["ahead"]},
         "roofline": roof,
         "pipelined": cfg["pipeline"],
-        "serial": serial,
         "mean_only_value": mean_only,
     }
     if ws == 1 and (args.cpu_baseline > 0 or (args.cpu_baseline < 0 and args.ntrain <= 4096)):
