@@ -37,7 +37,7 @@ INT8_PEAK_TOPS = 5000.0   # MI355X dense int8 MFMA (2x bf16 2.5 PF); measured 4.
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--ntrain", type=int, default=4096)
     ap.add_argument("--grid", type=int, default=256)
