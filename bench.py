@@ -65,6 +65,9 @@ def parse():
                     help="issue each job's fit on a second stream, so job i+1's fit runs while job i's predict "
                          "does (the steps are independent fit+predict jobs, like the reference's per-time-window "
                          "krig.kriging loop); 0 = strictly one job after the other")
+    ap.add_argument("--unpipelined-steps", type=int, default=20,
+                    help="with --pipeline 1 on one rank: first time this many jobs strictly one after another "
+                         "(reported under 'unpipelined', with the dominant kernel's roofline alone)")
     ap.add_argument("--cpu-baseline", type=int, default=-1,
                     help="time the numpy oracle on the host cores (N=1 only); -1 = only when N_train <= 4096")
     ap.add_argument("--cpu-sample-points", type=int, default=2048)
@@ -216,6 +219,29 @@ def main():
         set_mode(min(probe, key=probe.get))
     else:
         set_mode(cfg["mode"])
+    unpiped = None
+    if cfg["pipeline"] and ws == 1 and args.unpipelined_steps > 0:
+        # reference: the same jobs strictly one after another, measured BEFORE the timed region
+        # (the dominant kernel's launch time without a concurrent fit = its roofline alone)
+        cfg["pipeline"] = False
+        for _ in range(args.warmup):
+            step()
+        check_last()
+        barrier(ws)
+        E.timing_enable(True)
+        E.timing_read()
+        tu0 = time.perf_counter()
+        for _ in range(args.unpipelined_steps):
+            step()
+        check_last()
+        barrier(ws)
+        tu1 = time.perf_counter()
+        ukms, uklaunch, ukflops = E.timing_read()
+        E.timing_enable(False)
+        unpiped = {"value": m_all * args.unpipelined_steps / (tu1 - tu0),
+                   "ms_per_step": 1e3 * (tu1 - tu0) / args.unpipelined_steps, "steps": args.unpipelined_steps,
+                   "kernel_ms": ukms, "kernel_launches": uklaunch, "kernel_flops": ukflops}
+        cfg["pipeline"] = True
     for _ in range(args.warmup):
         step()
     barrier(ws)
@@ -286,6 +312,10 @@ def main():
                 "dense_equivalent_tops": achieved * nmod if achieved else None,
                 "fp64_equivalent_tflops": achieved, "fp64_equivalent_frac_of_fp64_peak":
                     (achieved / FP64_PEAK_TFLOPS) if achieved else None}
+        if unpiped and unpiped["kernel_ms"] > 0:
+            ua = unpiped["kernel_flops"] / (unpiped["kernel_ms"] * 1e-3) / 1e12 * nmod * efrac
+            unpiped["roofline_frac"] = ua / INT8_PEAK_TOPS
+            unpiped["avg_launch_ms"] = unpiped["kernel_ms"] / unpiped["kernel_launches"] / nmod
     else:
         roof = {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": (achieved / FP64_PEAK_TFLOPS) if achieved else None, "traffic": traffic,
@@ -316,6 +346,7 @@ def main():
                    "fit_mode_probe_ms_per_step": probe or None, "kstar_ahead": cfg["ahead"]},
         "roofline": roof,
         "pipelined": cfg["pipeline"],
+        "unpipelined": unpiped,
         "mean_only_value": mean_only,
     }
     if ws == 1 and (args.cpu_baseline > 0 or (args.cpu_baseline < 0 and args.ntrain <= 4096)):
