@@ -535,6 +535,47 @@ def predict(gp: GPFit, xg, var_mode: str = "latent", compute_var: bool = True, c
     return Predictor(gp, chunk)(xg, var_mode=var_mode, compute_var=compute_var)
 
 
+def krige_jobs(jobs, variance: str = "ozaki", chunk: int = 8192, var_mode: str = "latent",
+               compute_var: bool = True, jitter: float = 0.0, device=None):
+    """Independent kriging jobs (kernel, x, y, noise, xg), one after another — the reference's
+    runKrig.py:1-40 sweep (one GP_laser / krig.kriging fit + grid predict per setting or
+    time window) run in one process.  Yields (mean, var) per job, in order, on the current
+    stream; results are bit-identical to fit() + Predictor() called per job.
+
+    Job i+1's fit is queued on a side stream as soon as job i's predict is, so the factor
+    (latency-bound, a few hundred workgroups) runs on the CUs the predict's GEMMs leave idle
+    (bench.py --pipeline).  The fit of job i+1 waits for the work queued on the
+    current stream before it (so input tensors made there are ready); a non-SPD K_y of job i
+    raises numpy.linalg.LinAlgError when job i is yielded, as fit() would.  The predict
+    workspace is reused while consecutive jobs have the same padded size."""
+    dev = _require_device(device)
+    main = torch.cuda.current_stream(dev)
+    side = torch.cuda.Stream(dev)
+
+    def queue_fit(job):
+        kernel, x, y, noise, _ = job
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            return fit(kernel, x, y, noise, jitter=jitter, device=dev, variance=variance, check=False)
+
+    it = iter(jobs)
+    job = next(it, None)
+    gp = queue_fit(job) if job is not None else None
+    pred = None
+    while job is not None:
+        main.wait_stream(side)
+        gp.record_stream(main)
+        nxt = next(it, None)
+        gp_next = queue_fit(nxt) if nxt is not None else None
+        if pred is None or pred.gp.n != gp.n or pred.ozaki != ("ozaki" in gp.extra):
+            pred = Predictor(gp, chunk)
+        pred.gp = gp
+        out = pred(job[4], var_mode=var_mode, compute_var=compute_var)
+        gp.check()
+        yield out
+        job, gp = nxt, gp_next
+
+
 # ------------------------------------------------------------------ hyperparameters
 def param_names(kernel: KernelSpec) -> tuple:
     """Gradient / parameter order of log_marginal_likelihood: vector2d (l_df, l_cf, ratio, noise);

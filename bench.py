@@ -16,6 +16,8 @@ kernel: the variance contraction, timed live with HIP events on its stream) and
 from __future__ import annotations
 
 import argparse
+import functools
+import itertools
 import json
 import os
 import sys
@@ -242,8 +244,15 @@ def main():
                    "ms_per_step": 1e3 * (tu1 - tu0) / args.unpipelined_steps, "steps": args.unpipelined_steps,
                    "kernel_ms": ukms, "kernel_launches": uklaunch, "kernel_flops": ukflops}
         cfg["pipeline"] = True
+    run = step
+    if cfg["pipeline"] and cfg["mode"] in ("local", "replicate") and not cfg["ahead"]:
+        # the shipped API for a sweep of jobs: engine.krige_jobs (one generator over warmup +
+        # timed jobs, so no fit is queued past the last timed job and none is left unoverlapped)
+        jobs = E.krige_jobs(itertools.repeat((spec, xt, yt, noise, xg), args.warmup + args.steps),
+                            variance=args.variance, chunk=args.chunk)
+        run = functools.partial(next, jobs)
     for _ in range(args.warmup):
-        step()
+        run()
     barrier(ws)
     E.timing_enable(True)
     E.timing_read()
@@ -251,7 +260,7 @@ def main():
     t0 = time.perf_counter()
     trace = os.environ.get("GP2D_BENCH_TRACE") == "1"   # per-step wall times on stderr (diagnostics)
     for i in range(args.steps):
-        step()
+        run()
         if trace:
             torch.cuda.synchronize()
             print(f"[rank {rank}] step {i}: {1e3 * (time.perf_counter() - t0):.1f} ms since start", file=sys.stderr,
@@ -346,6 +355,7 @@ def main():
                    "fit_mode_probe_ms_per_step": probe or None, "kstar_ahead": cfg["ahead"]},
         "roofline": roof,
         "pipelined": cfg["pipeline"],
+        "api": "engine.krige_jobs" if run is not step else "engine.fit + Predictor",
         "unpipelined": unpiped,
         "mean_only_value": mean_only,
     }

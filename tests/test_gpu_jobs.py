@@ -1,0 +1,53 @@
+"""engine.krige_jobs — a sweep of independent kriging jobs with job i+1's fit on a side stream
+under job i's predict (the pattern bench.py --pipeline times) — must give, job by job, the
+same bits as fit() + Predictor() run one job at a time, and raise for a non-SPD job as fit()
+does.  The jobs mix sizes (workspace reuse and reallocation), kernel kinds and engines."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("no HIP device", allow_module_level=True)
+
+from gp2d import engine as E  # noqa: E402
+
+
+def _job(seed, n, G, kind, noise=0.0025):
+    rng = np.random.default_rng(seed)
+    x = np.stack([rng.uniform(0, 60, n), rng.uniform(0, 45, n)], 1)
+    y = np.concatenate([np.sin(x[:, 1] / 7), np.cos(x[:, 0] / 9)]) + rng.normal(0, 0.05, 2 * n)
+    gx, gy = np.linspace(-5, 65, G), np.linspace(-5, 50, G + 3)
+    GX, GY = np.meshgrid(gx, gy)
+    xg = np.stack([GX.reshape(-1), GY.reshape(-1)], 1)
+    spec = E.KernelSpec(kind=kind, l_df=4.0 + seed % 3, l_cf=3.0, ratio=0.5 if kind == "mixed" else 1.0)
+    return spec, torch.tensor(x, device="cuda"), torch.tensor(y, device="cuda"), noise, \
+        torch.tensor(xg, device="cuda")
+
+
+JOBS = [(1, 700, 60, "df"), (2, 700, 64, "mixed"), (3, 1500, 50, "df"), (4, 300, 40, "cf"),
+        (5, 1500, 72, "mixed"), (6, 1500, 72, "df")]
+
+
+@pytest.mark.parametrize("variance", ["ozaki", "f64"])
+def test_krige_jobs_bit_identical_to_sequential(variance):
+    jobs = [_job(*j) for j in JOBS]
+    got = [(m.clone(), v.clone()) for m, v in E.krige_jobs(jobs, variance=variance, chunk=2048)]
+    assert len(got) == len(jobs)
+    for (spec, x, y, noise, xg), (m, v) in zip(jobs, got):
+        gp = E.fit(spec, x, y, noise, variance=variance)
+        rm, rv = E.Predictor(gp, 2048)(xg)
+        assert torch.equal(m, rm) and torch.equal(v, rv)
+
+
+def test_krige_jobs_non_spd_raises_at_its_job():
+    jobs = [_job(1, 500, 40, "df"), _job(2, 500, 40, "df", noise=-100.0), _job(3, 500, 40, "df")]
+    gen = E.krige_jobs(jobs, variance="ozaki", chunk=1024)
+    m, v = next(gen)
+    assert torch.isfinite(v).all()
+    with pytest.raises(np.linalg.LinAlgError):
+        next(gen)
+
+
+def test_krige_jobs_empty():
+    assert list(E.krige_jobs([])) == []
