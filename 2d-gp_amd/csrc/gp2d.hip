@@ -736,6 +736,8 @@ static int predict_ozaki_impl(const int8_t* wres, const double* rowscale, int nm
   OzakiConsts oc;
   GP2D_CHECK(make_ozaki_consts(nmod, k, oc));
   const int nm = oc.nmod;
+  // the GEMM epilogue's biased sums (ozaki_mod_u31) stay below 2^31 for K = n < 2^16
+  GP2D_REQUIRE(n < 65536, "ozaki: the int8 GEMM epilogue needs n < 65536 (N_train < 32768)");
   const int64_t nmseg = (ntr_pad + OZ_KS_T - 1) / OZ_KS_T;
   const int64_t npseg = (n + OZ_CRT_ROWS - 1) / OZ_CRT_ROWS;
   const double kss = gp2d_kernel_diag(k);
@@ -779,11 +781,11 @@ static int predict_ozaki_impl(const int8_t* wres, const double* rowscale, int nm
         uint8_t* Cl = cres + (size_t)l * n * ncols;
         if (narrow)
           igemm_nt_mod_kernel<128, 3><<<ggrid, 256, 0, s>>>(Al, Bl, Cl, n, (int)n, (int)ncols, (int)n, 1, oc.m[l],
-                                                            oc.inv_m[l], (int)(cp / IBN), (int)(ntr_pad / IBK),
+                                                            (int)(cp / IBN), (int)(ntr_pad / IBK),
                                                             use_skip ? slist : nullptr, use_skip ? scnt : nullptr);
         else
           igemm_nt_mod_kernel<256, I_NSTAGE><<<ggrid, 512, 0, s>>>(Al, Bl, Cl, n, (int)n, (int)ncols, (int)n, 1,
-                                                                   oc.m[l], oc.inv_m[l], (int)(cp / IBN),
+                                                                   oc.m[l], (int)(cp / IBN),
                                                                    (int)(ntr_pad / IBK), use_skip ? slist : nullptr,
                                                                    use_skip ? scnt : nullptr);
         GP2D_CHECK(check_launch("igemm_nt_mod_kernel"));

@@ -4,7 +4,7 @@
 export TMPDIR=/tmp
 cd tools/microbench
 for v in "$@"; do
-  t=$(timeout -k 10 60 ./igemm_$v | head -n 1) || exit 1
+  t=$(timeout -k 10 60 ./igemm_$v > run_$v.txt && head -n 1 run_$v.txt && tail -n 1 run_$v.txt >&2) || exit 1
   timeout -s KILL 60 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES -f csv -d ../../gpurun_out/pmc_$v -o run -- ./igemm_$v > /dev/null 2>&1 || exit 1
   f=$(find ../../gpurun_out/pmc_$v -name "*counter_collection.csv" | head -n 1)
   python3 - "$f" "$t" <<'PY'
