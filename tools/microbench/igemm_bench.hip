@@ -44,7 +44,15 @@ int main() {
   (void)hipMemcpy(dB, Bb.data(), B.size(), hipMemcpyHostToDevice);
   hipEvent_t e0, e1; (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
   const dim3 g(nc / IG_TBN, n / IBM);
-  auto launch = [&]() { IGEMM_KERNEL<<<g, 2 * IG_TBN>>>(dA, dB, dC, n, n, nc, n, 1, mod IGEMM_INV, 1 << 30, 0 IGEMM_EXTRA); };
+  // IGEMM_K=k: dense (not triangular) launches with K = k on the same planes — per-tile vs
+  // per-slab cost (time = tiles·a + slabs·b); the sampled check then does not apply
+  const int kx = getenv("IGEMM_K") ? atoi(getenv("IGEMM_K")) : n, low = getenv("IGEMM_K") ? 0 : 1;
+#ifdef IGEMM_GRID
+  const dim3 gl(IGEMM_GRID);
+#else
+  const dim3 gl = g;
+#endif
+  auto launch = [&]() { IGEMM_KERNEL<<<gl, 2 * IG_TBN>>>(dA, dB, dC, n, n, nc, kx, low, mod IGEMM_INV, 1 << 30, 0 IGEMM_EXTRA); };
   for (int w = 0; w < 3; ++w) launch();
   (void)hipDeviceSynchronize();
   (void)hipEventRecord(e0);
@@ -52,6 +60,10 @@ int main() {
   (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
   float ms; (void)hipEventElapsedTime(&ms, e0, e1);
   const double ops = 2.0 * ((double)n * n / 2 + n * 128.0) * nc;
+  if (!low) {
+    printf("%s: K=%d dense: %.4f ms/launch\n", VARIANT, kx, ms / 20);
+    return 0;
+  }
   printf("%s: %.3f ms/launch, %.0f TOPs\n", VARIANT, ms / 20, ops / (ms / 20) / 1e9);
   std::vector<uint8_t> C((size_t)n * nc);
   (void)hipMemcpy(C.data(), dC, C.size(), hipMemcpyDeviceToHost);

@@ -14,7 +14,7 @@ import json
 import sys
 from collections import defaultdict
 
-PAT = "igemm_nt_mod_kernel"
+PAT = "igemm_nt_mod_"   # the persistent (default) and one-tile forms
 
 
 def per_dispatch(path):
