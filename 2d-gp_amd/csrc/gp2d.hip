@@ -12,6 +12,8 @@
 #include "lml.hpp"
 #include "../../include/gp2d.h"
 
+#include <dlfcn.h>
+
 #include <algorithm>
 #include <cstdlib>
 #include <cmath>
@@ -1089,6 +1091,49 @@ int gp2d_transpose(const double* A, int64_t n, int64_t lda, double* At, void* st
   if (n == 0) return 0;
   transpose_kernel<<<dim3((unsigned)(n / 64), (unsigned)(n / 64)), 256, 0, S(stream)>>>(A, n, lda, At);
   return check_launch("transpose_kernel");
+}
+
+// ------------------------------------------------------------- RCCL broadcast
+// ncclBroadcast of the caller's communicator, resolved at first use from the RCCL the process
+// already has loaded (RTLD_NOLOAD: the library that created `comm`), else librccl.so.1 from
+// the ROCm install — no link-time dependency, so the engine loads where RCCL is absent.
+}  // extern "C"
+namespace {
+typedef int (*rccl_bcast_fn)(const void*, void*, size_t, int, int, void*, hipStream_t);
+typedef const char* (*rccl_errstr_fn)(int);
+struct RcclSyms {
+  rccl_bcast_fn bcast = nullptr;
+  rccl_errstr_fn errstr = nullptr;
+};
+const RcclSyms& rccl_syms() {
+  static const RcclSyms r = [] {
+    RcclSyms x;
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+    if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (h) {
+      x.bcast = reinterpret_cast<rccl_bcast_fn>(dlsym(h, "ncclBroadcast"));
+      x.errstr = reinterpret_cast<rccl_errstr_fn>(dlsym(h, "ncclGetErrorString"));
+    }
+    return x;
+  }();
+  return r;
+}
+constexpr int kRcclUint8 = 1;   // ncclUint8
+}  // namespace
+extern "C" {
+
+int gp2d_bcast(void* buf, size_t bytes, int root, void* comm, void* stream) {
+  GP2D_REQUIRE(root >= 0, "bcast: root must be >= 0");
+  if (bytes == 0) return 0;
+  GP2D_REQUIRE(buf != nullptr && comm != nullptr, "bcast: NULL buffer or communicator");
+  const RcclSyms& r = rccl_syms();
+  GP2D_REQUIRE(r.bcast != nullptr, "bcast: RCCL (librccl.so.1, ncclBroadcast) not found");
+  const int rc = r.bcast(buf, buf, bytes, kRcclUint8, root, comm, S(stream));
+  if (rc != 0) {
+    set_error(std::string("bcast: ncclBroadcast failed: ") + (r.errstr ? r.errstr(rc) : "unknown RCCL error"));
+    return -100 - rc;
+  }
+  return 0;
 }
 
 void gp2d_timing_enable(int on) {

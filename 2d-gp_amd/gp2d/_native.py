@@ -12,7 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GP2D_LIB", os.path.join(_HERE, "libgp2d.so"))
-ABI_VERSION = 4          # GP2D_ABI_VERSION in include/gp2d.h
+ABI_VERSION = 5          # GP2D_ABI_VERSION in include/gp2d.h
 
 FAMILY_VECTOR2D, FAMILY_ARD_RBF, FAMILY_VECTOR_ST = 0, 1, 2
 KIND_SCALAR, KIND_DIVFREE, KIND_CURLFREE, KIND_MIXED = 0, 1, 2, 3
@@ -30,7 +30,7 @@ EXPORTS = (
     "gp2d_predict_ozaki_planes_workspace", "gp2d_predict_ozaki_planes", "gp2d_ozaki_set_skip", "gp2d_morton_codes", "gp2d_lml", "gp2d_lml_grad_count",
     "gp2d_lml_grad_workspace", "gp2d_lml_grad",
     "gp2d_kernel_grad_count", "gp2d_kernel_grad_workspace", "gp2d_kernel_grad",
-    "gp2d_gemm", "gp2d_transpose",
+    "gp2d_gemm", "gp2d_transpose", "gp2d_bcast",
     "gp2d_timing_enable", "gp2d_timing_read", "gp2d_last_error",
 )
 
@@ -107,6 +107,7 @@ _SIGS = {
     "gp2d_kernel_grad": (_I, [_P, _I64, _P, _I64, _KP, _P, _I64, _P, _P, _SZ, _P]),
     "gp2d_gemm": (_I, [_I, _I64, _I64, _I64, _D, _P, _I64, _P, _I64, _D, _P, _I64, _P]),
     "gp2d_transpose": (_I, [_P, _I64, _I64, _P, _P]),
+    "gp2d_bcast": (_I, [_P, _SZ, _I, _P, _P]),
     "gp2d_timing_enable": (None, [_I]),
     "gp2d_timing_read": (_I, [ctypes.POINTER(_D), ctypes.POINTER(_I64), ctypes.POINTER(_D)]),
     "gp2d_last_error": (ctypes.c_char_p, []),

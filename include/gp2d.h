@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define GP2D_ABI_VERSION 4
+#define GP2D_ABI_VERSION 5
 
 /* kernel families */
 #define GP2D_FAMILY_VECTOR2D 0   /* 2×2 matrix-valued SE kernels on (x1, x2)          */
@@ -237,6 +237,17 @@ int    gp2d_kernel_grad(const double* xa, int64_t na, const double* xb, int64_t 
 int gp2d_gemm(int transb, int64_t m, int64_t n, int64_t k, double alpha, const double* A, int64_t lda,
               const double* B, int64_t ldb, double beta, double* C, int64_t ldc, void* stream);
 int gp2d_transpose(const double* A, int64_t n, int64_t lda, double* At, void* stream);
+
+/* ---- multi-GPU: factor broadcast --------------------------------
+ * gp2d_bcast: in-place ncclBroadcast of `bytes` bytes of device memory from rank `root` over
+ *   the caller's RCCL communicator (`comm` is an ncclComm_t), on `stream`.  The fit of rank 0
+ *   (W = L⁻¹ packed, α, the Morton-ordered training points) goes out this way in the bcast
+ *   fit mode; a C/C++ host that owns its communicator calls it directly (the Python layer
+ *   uses torch.distributed's broadcast on the same RCCL, gp2d/distributed.py).  There is no
+ *   reference call it replaces — the reference is single-process.  RCCL is
+ *   resolved at first call (no link-time dependency).  Returns −100 − ncclResult_t on an RCCL
+ *   failure.                                                                             */
+int gp2d_bcast(void* buf, size_t bytes, int root, void* comm, void* stream);
 
 /* ---- instrumentation ------------------------------------------------------------
  * When enabled, every launch of the predict variance kernel (the dominant

@@ -152,6 +152,10 @@ int main() {
   double ms = -1, fl = -1;
   int64_t cnt = -1;
   EXPECT(gp2d_timing_read(&ms, &cnt, &fl) == 0 && cnt == 0 && ms == 0.0);
+  // ---- factor broadcast: argument checks run before RCCL is resolved
+  EXPECT(gp2d_bcast(nullptr, 0, 0, nullptr, nullptr) == 0);
+  EXPECT_ERR(gp2d_bcast(buf, 8, 0, nullptr, nullptr));
+  EXPECT_ERR(gp2d_bcast(buf, 8, -1, buf, nullptr));
   gp2d_timing_enable(0);
   gp2d_ozaki_set_skip(1);
   std::printf("%d checks, %d failed\n", g_checks, g_fail);

@@ -94,3 +94,28 @@ def test_bcast_fit_two_ranks_bit_identical(tmp_path, variance, kind):
     for i in range(world):
         assert np.array_equal(r[i]["mean"], mu), i
         assert np.array_equal(r[i]["var"], var), i
+
+
+def test_gp2d_bcast_native_rccl():
+    """gp2d_bcast (the C ABI's factor broadcast for C/C++ hosts) on a one-rank RCCL
+    communicator made with ncclCommInitAll: root 0 keeps its bytes, rc 0; a root outside the
+    communicator comes back as −100 − ncclInvalidArgument with RCCL's message."""
+    import ctypes
+    from gp2d import _native as N
+    L = N.lib()
+    rccl = ctypes.CDLL("librccl.so.1")
+    comm = ctypes.c_void_p()
+    devs = (ctypes.c_int * 1)(torch.cuda.current_device())
+    assert rccl.ncclCommInitAll(ctypes.byref(comm), 1, devs) == 0
+    try:
+        x = torch.arange(1 << 20, dtype=torch.float64, device="cuda")
+        ref = x.clone()
+        s = torch.cuda.current_stream()
+        rc = L.gp2d_bcast(ctypes.c_void_p(x.data_ptr()), x.numel() * 8, 0, comm, ctypes.c_void_p(s.cuda_stream))
+        assert rc == 0, L.gp2d_last_error()
+        torch.cuda.synchronize()
+        assert torch.equal(x, ref)
+        rc = L.gp2d_bcast(ctypes.c_void_p(x.data_ptr()), 8, 1, comm, ctypes.c_void_p(s.cuda_stream))
+        assert rc == -104 and b"ncclBroadcast" in L.gp2d_last_error(), (rc, L.gp2d_last_error())
+    finally:
+        rccl.ncclCommDestroy(comm)

@@ -24,7 +24,7 @@ def test_library_exports_every_header_symbol():
     for s in syms:
         assert hasattr(L, s), s
     assert set(syms) == set(_native.EXPORTS)
-    assert L.gp2d_abi_version() == _native.ABI_VERSION == 4
+    assert L.gp2d_abi_version() == _native.ABI_VERSION == 5
     assert L.gp2d_padded_points(1) == 64 and L.gp2d_padded_points(64) == 64 and L.gp2d_padded_points(65) == 128
 
 
@@ -55,6 +55,11 @@ def test_argument_errors_are_reported():
     assert rc < 0 and b"multiples of 128" in L.gp2d_last_error()
     rc = L.gp2d_transpose(one, 100, 100, one, None)
     assert rc < 0 and b"multiple of 64" in L.gp2d_last_error()
+    assert L.gp2d_bcast(None, 0, 0, None, None) == 0            # nothing to send
+    rc = L.gp2d_bcast(one, 8, 0, None, None)
+    assert rc < 0 and b"communicator" in L.gp2d_last_error()
+    rc = L.gp2d_bcast(one, 8, -1, one, None)
+    assert rc < 0 and b"root" in L.gp2d_last_error()
 
 
 def test_ozaki_rejects_ratio_outside_unit_interval():
