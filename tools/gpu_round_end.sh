@@ -1,5 +1,5 @@
 set -o pipefail
-R=${1:-r02_end}
+R=${1:-round_end}
 mkdir -p gpurun_out/$R
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/$R/gpu_tests.log 2>&1 && \
