@@ -9,6 +9,8 @@ single-GPU result.
 """
 from __future__ import annotations
 
+import collections
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -107,6 +109,85 @@ def fit_sharded(spec: E.KernelSpec, x, y, noise: float, device, mode: str = "bca
     if variance == "ozaki" and "ozaki" not in gp.extra:
         E.ozaki_prepare(gp, diag_add=float(noise + jitter))   # a-priori moduli count: no host sync
     return gp
+
+
+def krige_jobs_sharded(jobs, variance: str = "ozaki", chunk: int = 8192, var_mode: str = "latent",
+                       compute_var: bool = True, jitter: float = 0.0, device=None, align: int = 64):
+    """A stream of independent kriging jobs (kernel, x, y, noise, xg) — the reference's
+    runKrig.py sweep / per-window krig.kriging calls — spread over all ranks: job j is FITTED
+    by rank j mod world only (round robin, on a side stream, up to one job per rank ahead),
+    its factor W = L⁻¹, α and training points are broadcast from that rank (broadcast_fit,
+    RCCL under the 'nccl' backend), and EVERY rank predicts its tile-aligned shard of job j's
+    grid (predict_shard).  Yields (lo, hi, mean, var) per job, in job order, on every rank;
+    the shards are bit-identical to one process's fit + predict (fixed-order reductions).
+
+    Per job a rank does 1/world of a fit plus 1/world of the predict, so for a stream of jobs
+    the fit — the serial part of a one-job multi-GPU predict — is divided like the grid
+    (DESIGN.md §5).  Every rank must pass the same job sequence (x, y are read on the owner
+    only); a non-SPD K_y raises numpy.linalg.LinAlgError on every rank at that job."""
+    ws, rank = world()
+    dev = E._require_device(device)
+    if ws == 1:   # one rank: the single-GPU pipelined form (the next fit under this predict)
+        seen = collections.deque()
+
+        def feed():
+            for job in jobs:
+                seen.append(job)
+                yield job
+        for mean, var in E.krige_jobs(feed(), variance=variance, chunk=chunk, var_mode=var_mode,
+                                      compute_var=compute_var, jitter=jitter, device=dev):
+            xg = seen.popleft()[4]
+            yield 0, int(xg.shape[0]), mean, var
+        return
+    main = torch.cuda.current_stream(dev)
+    fit_stream = torch.cuda.Stream(dev)
+    it = iter(jobs)
+    window = collections.deque()   # (index, job) read ahead
+    own = {}                       # index → (gp, error, event) of this rank's fits in flight
+    count = 0
+    pred = None
+    while True:
+        while len(window) < ws:
+            job = next(it, None)
+            if job is None:
+                break
+            window.append((count, job))
+            count += 1
+        if not window:
+            return
+        for idx, job in window:   # this rank's fits among the next `world` jobs, issued ahead
+            if idx % ws == rank and idx not in own:
+                spec, x, y, noise, _ = job
+                fit_stream.wait_stream(main)
+                gp, err = None, None
+                with torch.cuda.stream(fit_stream):
+                    try:
+                        gp = E.fit(spec, x, y, noise, jitter=jitter, device=dev, variance=variance, check=False)
+                    except Exception as e:   # noqa: BLE001 — travels in broadcast_fit's status word
+                        err = e
+                    ev = torch.cuda.Event()
+                    ev.record(fit_stream)
+                own[idx] = (gp, err, ev)
+        idx, (spec, x, y, noise, xg) = window.popleft()
+        owner = idx % ws
+        gp, err = None, None
+        if owner == rank:
+            gp, err, ev = own.pop(idx)
+            if gp is not None:
+                main.wait_event(ev)
+                gp.record_stream(main)
+                try:
+                    gp.check()
+                except Exception as e:   # noqa: BLE001
+                    gp, err = None, e
+        gp = broadcast_fit(gp, spec, noise, x, dev, src=owner, error=err)
+        if variance == "ozaki" and "ozaki" not in gp.extra:
+            E.ozaki_prepare(gp, diag_add=float(noise + jitter))   # a-priori moduli count: no host sync
+        if pred is None or pred.gp.n != gp.n or pred.ozaki != ("ozaki" in gp.extra):
+            pred = E.Predictor(gp, chunk)
+        pred.gp = gp
+        yield predict_shard(pred, E._as_points(xg, spec.input_dim, dev), var_mode=var_mode,
+                            compute_var=compute_var, align=align)
 
 
 def predict_shard(pred: E.Predictor, xg_all, var_mode: str = "latent", compute_var: bool = True, align: int = 64):

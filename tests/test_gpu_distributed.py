@@ -119,3 +119,86 @@ def test_gp2d_bcast_native_rccl():
         assert rc == -104 and b"ncclBroadcast" in L.gp2d_last_error(), (rc, L.gp2d_last_error())
     finally:
         rccl.ncclCommDestroy(comm)
+
+
+def _jobs():
+    from gp2d import engine as E
+    out = []
+    for seed, n, G, kind in [(11, 700, 40, "df"), (12, 700, 44, "mixed"), (13, 900, 40, "df"), (14, 700, 36, "cf"),
+                             (15, 900, 48, "mixed")]:
+        rng = np.random.default_rng(seed)
+        x = np.stack([rng.uniform(0, 60, n), rng.uniform(0, 45, n)], 1)
+        y = np.concatenate([np.sin(x[:, 1] / 7), np.cos(x[:, 0] / 9)]) + rng.normal(0, 0.05, 2 * n)
+        GX, GY = np.meshgrid(np.linspace(-5, 65, G), np.linspace(-5, 50, G + 5))
+        xg = np.stack([GX.reshape(-1), GY.reshape(-1)], 1)
+        spec = E.KernelSpec(kind=kind, l_df=4.0 + seed % 3, l_cf=3.0, ratio=0.5 if kind == "mixed" else 1.0)
+        out.append((spec, x, y, 0.0025, xg))
+    return out
+
+
+def _rr_worker(rank, world, port, out_dir, variance, bad):
+    for p in (ROOT, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from gp2d import distributed as GD
+    jobs = _jobs()
+    if bad is not None:   # a non-SPD job (negative noise) owned by rank bad % world
+        s, x, y, _, xg = jobs[bad]
+        jobs[bad] = (s, x, y, -100.0, xg)
+    res, raised = {}, -1
+    try:
+        for j, (lo, hi, mean, var) in enumerate(GD.krige_jobs_sharded(jobs, variance=variance, chunk=1024)):
+            res[f"lo{j}"], res[f"hi{j}"] = lo, hi
+            res[f"mean{j}"], res[f"var{j}"] = mean.cpu().numpy(), var.cpu().numpy()
+    except np.linalg.LinAlgError:
+        raised = len([k for k in res if k.startswith("lo")])
+    np.savez(os.path.join(out_dir, f"rr{rank}.npz"), raised=raised, **res)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _spawn(target, world, *args):
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, *args)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    codes = [p.exitcode for p in procs]
+    for p in procs:
+        if p.is_alive():  # pragma: no cover — a hung rank: end it, then fail
+            p.kill()
+    assert codes == [0] * world, codes
+
+
+@pytest.mark.parametrize("variance", ["ozaki", "f64"])
+def test_round_robin_jobs_two_ranks_bit_identical(tmp_path, variance):
+    """krige_jobs_sharded: job j fitted on rank j mod 2 only, factor broadcast, every rank
+    predicts its shard; the assembled shards equal one process's fit + predict, bit for bit."""
+    from gp2d import distributed as GD
+    from gp2d import engine as E
+    world = 2
+    _spawn(_rr_worker, world, str(tmp_path), variance, None)
+    r = [np.load(os.path.join(tmp_path, f"rr{i}.npz")) for i in range(world)]
+    for j, (spec, x, y, noise, xg) in enumerate(_jobs()):
+        gp = E.fit(spec, x, y, noise, variance=variance)
+        mu, var = (t.cpu().numpy() for t in E.Predictor(gp, 1024)(xg))
+        m = xg.shape[0]
+        shards_m = [(int(r[i][f"lo{j}"]), int(r[i][f"hi{j}"]), r[i][f"mean{j}"]) for i in range(world)]
+        shards_v = [(int(r[i][f"lo{j}"]), int(r[i][f"hi{j}"]), r[i][f"var{j}"]) for i in range(world)]
+        assert np.array_equal(GD.assemble_from_shards(m, 2, shards_m), mu), j
+        assert np.array_equal(GD.assemble_from_shards(m, 2, shards_v), var), j
+
+
+def test_round_robin_jobs_non_spd_raises_on_every_rank(tmp_path):
+    """Job 3 (owned by rank 1) has a non-SPD K_y: both ranks raise LinAlgError after the
+    three jobs before it, none hangs."""
+    world = 2
+    _spawn(_rr_worker, world, str(tmp_path), "ozaki", 3)
+    for i in range(world):
+        assert int(np.load(os.path.join(tmp_path, f"rr{i}.npz"))["raised"]) == 3, i
