@@ -141,21 +141,21 @@ def krige_jobs_sharded(jobs, variance: str = "ozaki", chunk: int = 8192, var_mod
         return
     main = torch.cuda.current_stream(dev)
     fit_stream = torch.cuda.Stream(dev)
+    comm = torch.cuda.Stream(dev)   # broadcasts + the receivers' int8 preparation
     it = iter(jobs)
     window = collections.deque()   # (index, job) read ahead
     own = {}                       # index → (gp, error, event) of this rank's fits in flight
     count = 0
-    pred = None
-    while True:
-        while len(window) < ws:
+
+    def refill():
+        nonlocal count
+        while len(window) < ws + 1:
             job = next(it, None)
             if job is None:
                 break
             window.append((count, job))
             count += 1
-        if not window:
-            return
-        for idx, job in window:   # this rank's fits among the next `world` jobs, issued ahead
+        for idx, job in window:   # this rank's fits among the jobs read ahead
             if idx % ws == rank and idx not in own:
                 spec, x, y, noise, _ = job
                 fit_stream.wait_stream(main)
@@ -168,26 +168,54 @@ def krige_jobs_sharded(jobs, variance: str = "ozaki", chunk: int = 8192, var_mod
                     ev = torch.cuda.Event()
                     ev.record(fit_stream)
                 own[idx] = (gp, err, ev)
-        idx, (spec, x, y, noise, xg) = window.popleft()
+
+    def receive(idx, job):
+        """Job idx's factor from its owner, on the comm stream: (gp, ready event) or the
+        exception every rank raises for it (kept until the job's turn)."""
+        spec, x, _, noise, _ = job
         owner = idx % ws
         gp, err = None, None
         if owner == rank:
             gp, err, ev = own.pop(idx)
             if gp is not None:
-                main.wait_event(ev)
-                gp.record_stream(main)
+                comm.wait_event(ev)
+                gp.record_stream(comm)
                 try:
                     gp.check()
                 except Exception as e:   # noqa: BLE001
                     gp, err = None, e
-        gp = broadcast_fit(gp, spec, noise, x, dev, src=owner, error=err)
-        if variance == "ozaki" and "ozaki" not in gp.extra:
-            E.ozaki_prepare(gp, diag_add=float(noise + jitter))   # a-priori moduli count: no host sync
+        try:
+            with torch.cuda.stream(comm):
+                gp = broadcast_fit(gp, spec, noise, x, dev, src=owner, error=err)
+                if variance == "ozaki" and "ozaki" not in gp.extra:
+                    E.ozaki_prepare(gp, diag_add=float(noise + jitter))   # a-priori moduli count
+                ready = torch.cuda.Event()
+                ready.record(comm)
+        except Exception as e:   # noqa: BLE001
+            return e
+        return gp, ready
+
+    refill()
+    if not window:
+        return
+    cur = receive(*window[0])
+    pred = None
+    while window:
+        idx, (spec, x, y, noise, xg) = window.popleft()
+        if isinstance(cur, Exception):
+            raise cur
+        gp, ready = cur
+        main.wait_event(ready)
+        gp.record_stream(main)
         if pred is None or pred.gp.n != gp.n or pred.ozaki != ("ozaki" in gp.extra):
             pred = E.Predictor(gp, chunk)
         pred.gp = gp
-        yield predict_shard(pred, E._as_points(xg, spec.input_dim, dev), var_mode=var_mode,
+        out = predict_shard(pred, E._as_points(xg, spec.input_dim, dev), var_mode=var_mode,
                             compute_var=compute_var, align=align)
+        refill()
+        # the next job's factor travels (host may wait for its owner) while this predict runs
+        cur = receive(*window[0]) if window else None
+        yield out
 
 
 def predict_shard(pred: E.Predictor, xg_all, var_mode: str = "latent", compute_var: bool = True, align: int = 64):

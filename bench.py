@@ -1,10 +1,12 @@
 """Headline benchmark: posterior grid points/s (fit + predict), N_train = 4096,
 divergence-free 2-D SE vector kernel, 256×256 grid per GPU (BASELINE.json).
 
-One "step" = K_y assembly + POTRF + TRTRI + α (rank 0, W/α broadcast over RCCL
-when N > 1) + posterior mean AND variance at every point of this rank's grid
-shard.  Inputs are resident in HBM before the timed region.  Weak scaling: each
-GPU owns 65,536 points of a 256 × (256·N) global grid.
+One "step" = one complete job: K_y assembly + POTRF + TRTRI + α + posterior mean AND
+variance at every point of the job's grid.  Inputs are resident in HBM before the timed
+region.  N = 1: successive jobs pipelined (engine.krige_jobs).  N > 1 (default: strong
+scaling): the same 256×256 job grid sharded over the N ranks, job j fitted on rank j mod N
+and its factor broadcast over RCCL (distributed.krige_jobs_sharded); --scaling weak gives
+each rank its own 256×256 block with a replicated fit instead.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...
@@ -51,10 +53,16 @@ def parse():
                     help="BASELINE.json config preset: B = df N=1024 128^2, C = mixed N=4096 256^2, "
                          "D = mixed N=16384, one 512^2 grid sharded over the ranks (strong scaling)")
     ap.add_argument("--chunk", type=int, default=8192)
-    ap.add_argument("--fit-mode", default="replicate", choices=["auto", "bcast", "replicate"],
+    ap.add_argument("--scaling", default="auto", choices=["auto", "weak", "strong"],
+                    help="N>1: strong = the --grid x --grid job grid sharded over the ranks (auto's choice: "
+                         "jobs fitted round robin, factor broadcast); weak = a --grid x --grid block per rank "
+                         "(a --grid x (--grid·N) job grid)")
+    ap.add_argument("--fit-mode", default=None, choices=["auto", "bcast", "replicate", "rr"],
                     help="N>1: every rank fits, no data-path collective (replicate, default); rank 0 "
-                         "fits and W goes out by RCCL broadcast (bcast); or whichever of the two the "
-                         "warmup measured faster (auto)")
+                         "fits and W goes out by RCCL broadcast (bcast); whichever of the two the "
+                         "warmup measured faster (auto); or job j fitted on rank j mod N only and its "
+                         "factor broadcast, every rank predicting its shard of every job (rr, "
+                         "distributed.krige_jobs_sharded)")
     ap.add_argument("--variance", default="ozaki", choices=["ozaki", "f64"],
                     help="variance contraction: exact INT8 Ozaki-II emulation (default) or FP64 MFMA")
     ap.add_argument("--kstar-ahead", type=int, default=-1,
@@ -81,6 +89,11 @@ def parse():
         a.kind, a.ntrain, a.grid = "mixed", 4096, 256
     elif a.config == "D":
         a.kind, a.ntrain, a.grid_global = "mixed", 16384, 512
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    if a.grid_global == 0 and ws > 1 and a.scaling in ("auto", "strong"):
+        a.grid_global = a.grid   # N>1 default: one job grid sharded over the ranks
+    if a.fit_mode is None:
+        a.fit_mode = "rr" if (ws > 1 and a.grid_global > 0) else "replicate"
     return a
 
 
@@ -159,7 +172,8 @@ def main():
     pred_cache = {}
     side = torch.cuda.Stream(dev) if args.variance == "ozaki" else None
     cfg = {"mode": args.fit_mode if ws > 1 else "local", "ahead": False,
-           "pipeline": bool(args.pipeline) and ws == 1 or (bool(args.pipeline) and args.fit_mode == "replicate"),
+           "pipeline": bool(args.pipeline) and ws == 1 or (bool(args.pipeline) and args.fit_mode == "replicate")
+           or (ws > 1 and args.fit_mode == "rr"),
            "first": True}
 
     def set_mode(mode):
@@ -245,12 +259,21 @@ def main():
                    "kernel_ms": ukms, "kernel_launches": uklaunch, "kernel_flops": ukflops}
         cfg["pipeline"] = True
     run = step
-    if cfg["pipeline"] and cfg["mode"] in ("local", "replicate") and not cfg["ahead"]:
+    api = "engine.fit + Predictor"
+    if cfg["mode"] == "rr":
+        # the global grid on every rank; each job's fit on one rank, its shard predicted on all
+        xg_full = torch.tensor(xg_all, device=dev)
+        jobs = GD.krige_jobs_sharded(itertools.repeat((spec, xt, yt, noise, xg_full), args.warmup + args.steps),
+                                     variance=args.variance, chunk=args.chunk)
+        run = functools.partial(next, jobs)
+        api = "distributed.krige_jobs_sharded"
+    elif cfg["pipeline"] and cfg["mode"] in ("local", "replicate") and not cfg["ahead"]:
         # the shipped API for a sweep of jobs: engine.krige_jobs (one generator over warmup +
         # timed jobs, so no fit is queued past the last timed job and none is left unoverlapped)
         jobs = E.krige_jobs(itertools.repeat((spec, xt, yt, noise, xg), args.warmup + args.steps),
                             variance=args.variance, chunk=args.chunk)
         run = functools.partial(next, jobs)
+        api = "engine.krige_jobs"
     for _ in range(args.warmup):
         run()
     barrier(ws)
@@ -281,7 +304,10 @@ def main():
     barrier(ws)
     t2 = time.perf_counter()
     for _ in range(args.steps):
-        gp = GD.fit_sharded(spec, xt, yt, noise, dev, mode=cfg["mode"], variance=args.variance)
+        gp = GD.fit_sharded(spec, xt, yt, noise, dev, mode="replicate" if cfg["mode"] == "rr" else cfg["mode"],
+                            variance=args.variance)
+        if "p" not in pred_cache:   # the timed region ran through krige_jobs*: no Predictor yet
+            pred_cache["p"] = E.Predictor(gp, args.chunk)
         pred_cache["p"].gp = gp
         pred_cache["p"](xg, compute_var=False, out=(mean, var))
     barrier(ws)
@@ -350,12 +376,14 @@ def main():
                                ", fit+predict (mean+variance)" + (f" [BASELINE config {args.config}]" if args.config else ""),
                    "n_train": args.ntrain, ("grid_global" if strong else "grid_per_gpu"): f"{G}x{G}",
                    "points_total": m_all, "length_scale_km": 5.0, "noise": noise,
-                   "parallelism": f"grid-sharded x{ws}, factor {cfg['mode']}" +
-                                  (" (RCCL broadcast of packed W)" if ws > 1 and cfg["mode"] == "bcast" else ""),
+                   "parallelism": (f"grid-sharded x{ws}, job j fitted on rank j mod {ws}, factor broadcast "
+                                   "(RCCL, packed W)" if cfg["mode"] == "rr" else
+                                   f"grid-sharded x{ws}, factor {cfg['mode']}" +
+                                   (" (RCCL broadcast of packed W)" if ws > 1 and cfg["mode"] == "bcast" else "")),
                    "fit_mode_probe_ms_per_step": probe or None, "kstar_ahead": cfg["ahead"]},
         "roofline": roof,
         "pipelined": cfg["pipeline"],
-        "api": "engine.krige_jobs" if run is not step else "engine.fit + Predictor",
+        "api": api,
         "unpipelined": unpiped,
         "mean_only_value": mean_only,
     }

@@ -176,3 +176,23 @@ def test_prior_window_bit_exact(golden, case):
     fm = {k: g[k] for k in ("Xo", "Xt", "obs", "test_points")}
     XT, u = K._prior_window(fm, np.array([tc]), tlim, (x0, x1), xrange, "u" if comp else "v")
     assert np.array_equal(XT, g[f"c{case}_XT"]) and np.array_equal(u, g[f"c{case}_u"])
+
+
+def test_bench_scaling_defaults(monkeypatch):
+    """bench.py: N = 1 runs the headline job; N > 1 defaults to strong scaling over the same
+    256×256 job grid with round-robin fits; --scaling weak keeps a block per rank."""
+    import sys
+    import bench
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    monkeypatch.setattr(sys, "argv", ["bench.py"])
+    a = bench.parse()
+    assert (a.grid_global, a.fit_mode) == (0, "replicate")
+    monkeypatch.setenv("WORLD_SIZE", "8")
+    a = bench.parse()
+    assert (a.grid_global, a.fit_mode) == (256, "rr")
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--scaling", "weak"])
+    a = bench.parse()
+    assert (a.grid_global, a.fit_mode) == (0, "replicate")
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--fit-mode", "bcast"])
+    a = bench.parse()
+    assert (a.grid_global, a.fit_mode) == (256, "bcast")
