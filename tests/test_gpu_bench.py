@@ -35,3 +35,26 @@ def test_bench_json_contract(variance):
     assert r["bound"] == "mfma" and 0 < r["frac"] < 1 and abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-12
     c = d["cpu_baseline"]
     assert c["value"] > 0 and c["kind"] == "port" and c["cores"] >= 1 and c["sample"]
+
+
+def test_bench_two_ranks_default_contract():
+    """The N > 1 default (strong scaling, round-robin fits + factor broadcast) through
+    torch.distributed.run with two ranks on the one card (gloo: RCCL refuses two ranks per
+    device): one JSON line from rank 0, whole-job value over both ranks."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, GP2D_DIST_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2",
+           "--ntrain", "256", "--grid", "64", "--steps", "4", "--warmup", "1", "--chunk", "1024"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=200, cwd=ROOT, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["api"] == "distributed.krige_jobs_sharded"
+    assert abs(d["value"] - 64 * 64 / (d["ms_per_step"] * 1e-3)) / d["value"] < 1e-6
+    assert "cpu_baseline" not in d and d["roofline"]["frac"] > 0
