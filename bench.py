@@ -41,7 +41,7 @@ INT8_PEAK_TOPS = 5000.0   # MI355X dense int8 MFMA (2x bf16 2.5 PF); measured 4.
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--steps", type=int, default=None, help="timed jobs (default 100; --config D: 4, E: 2 sweeps)")
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--ntrain", type=int, default=4096)
     ap.add_argument("--grid", type=int, default=256)
@@ -49,9 +49,11 @@ def parse():
     ap.add_argument("--grid-global", type=int, default=0,
                     help="strong scaling: ONE fixed G x G grid sharded over the ranks (0 = weak scaling, "
                          "--grid x --grid points per rank)")
-    ap.add_argument("--config", default=None, choices=["B", "C", "D"],
+    ap.add_argument("--config", default=None, choices=["B", "C", "D", "E"],
                     help="BASELINE.json config preset: B = df N=1024 128^2, C = mixed N=4096 256^2, "
-                         "D = mixed N=16384, one 512^2 grid sharded over the ranks (strong scaling)")
+                         "D = mixed N=16384, one 512^2 grid sharded over the ranks (strong scaling), "
+                         "E = 64-setting (l_df, noise) sweep of LML + gradient at N=4096, settings dealt over "
+                         "the ranks (hyper.sweep)")
     ap.add_argument("--chunk", type=int, default=8192)
     ap.add_argument("--scaling", default="auto", choices=["auto", "weak", "strong"],
                     help="N>1: strong = the --grid x --grid job grid sharded over the ranks (auto's choice: "
@@ -89,6 +91,8 @@ def parse():
         a.kind, a.ntrain, a.grid = "mixed", 4096, 256
     elif a.config == "D":
         a.kind, a.ntrain, a.grid_global = "mixed", 16384, 512
+    if a.steps is None:
+        a.steps = {"D": 4, "E": 2}.get(a.config, 100)
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     if a.grid_global == 0 and ws > 1 and a.scaling in ("auto", "strong"):
         a.grid_global = a.grid   # N>1 default: one job grid sharded over the ranks
@@ -140,9 +144,70 @@ def cpu_baseline(x, y, xg, kind, l, noise, sample_pts):
                       f"grid points ({t2 - t1:.2f} s), predict extrapolated linearly; OpenBLAS threads={cores}"}
 
 
+def config_e_settings():
+    """BASELINE config E's 64 settings: l_df on 8 log-spaced values in [2, 12] km x noise on 8
+    log-spaced values in [1e-3, 5e-2] (the same grid as the committed config-E fixture)."""
+    return [dict(l_df=float(l), noise=float(nz)) for l in np.geomspace(2.0, 12.0, 8)
+            for nz in np.geomspace(1e-3, 5e-2, 8)]
+
+
+def run_sweep(args, ws, rank, dev):
+    """Config E: one step = the whole 64-setting sweep (fit + LML + exact gradient per
+    setting), settings dealt round robin over the ranks and the results all-reduced
+    (hyper.sweep); value = settings per second for the whole job (strong scaling)."""
+    from gp2d import data as D
+    from gp2d import engine as E
+    from gp2d import hyper as H
+    x1, x2, u, v = D.synthetic_tracks(args.ntrain, seed=2016)
+    xt = torch.tensor(np.stack([x1, x2], 1), device=dev)
+    yt = torch.tensor(np.concatenate([u, v]), device=dev)
+    settings = config_e_settings()
+    ks = E.KernelSpec(kind="df", l_df=5.0)
+
+    def sweep():
+        return H.sweep(ks, xt, yt, settings, noise=0.0025, eval_gradient=True, device=dev)
+
+    for _ in range(args.warmup):
+        sweep()
+    barrier(ws)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        vals, grads = sweep()
+    barrier(ws)
+    dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    if ws > 1:
+        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    elapsed = float(dt.item())
+    if rank == 0:
+        n = 2 * E.padded_points(args.ntrain)
+        # per setting: POTRF n³/3 + TRTRI n³/3 + K_y⁻¹ = WᵀW n³/3 (FP64 MFMA), the rest O(n²)
+        per_gpu = len(settings) / ws * n ** 3 * args.steps / elapsed / 1e12
+        out = {
+            "metric": f"hyperparameter settings/sec (fit + LML + gradient), 64-setting sweep, N_train={args.ntrain}, "
+                      "div-free 2D kernel",
+            "value": len(settings) * args.steps / elapsed, "unit": "settings/s", "n_gpus": ws,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (seeded drifter field, SURVEY.md §8d)",
+            "config": {"workload": f"BASELINE config E: 64 (l_df, noise) settings x N_train={args.ntrain}, "
+                                   f"div-free, LML + exact gradient per setting, settings dealt over {ws} GPU(s)",
+                       "n_train": args.ntrain, "settings": len(settings), "parallelism": f"settings round robin x{ws}"},
+            "roofline": {"bound": "mfma", "achieved": per_gpu, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": per_gpu / FP64_PEAK_TFLOPS, "traffic": None,
+                         "kernel": "whole sweep per GPU: POTRF + TRTRI + W^T W (n^3 FP64 flop per setting) / wall time"},
+            "finite_settings": int(np.isfinite(vals).sum()),
+        }
+        print(json.dumps(out), flush=True)
+    if ws > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     ws, rank, dev = setup_dist(args)
+    if args.config == "E":
+        return run_sweep(args, ws, rank, dev)
     from gp2d import data as D
     from gp2d import distributed as GD
     from gp2d import engine as E
