@@ -104,17 +104,6 @@ static int assemble_impl(const double* xa, int64_t na, int64_t na_pad, const dou
   return check_launch("assemble");
 }
 
-// Output tile width of the int8 variance GEMM: 256 (one 512-thread workgroup per CU, the
-// default) or 128 (two workgroups per CU, each one's epilogue under the other's MFMAs;
-// measured slower: 943k vs 909k cycles per launch at 1.57 vs 1.64 GHz, the extra LDS-DMA
-// pieces cost more clock than the overlap returns).  GP2D_IGEMM_TBN=128 selects it.
-static int igemm_tile_width() {
-  static const int w = [] {
-    const char* e = std::getenv("GP2D_IGEMM_TBN");
-    return (e && std::atoi(e) == 128) ? 128 : 256;
-  }();
-  return w;
-}
 
 // ------------------------------------------------------------- Ozaki constants
 static const int kModuli[OZ_MAXMOD] = {256, 255, 253, 251, 247, 241, 239, 233,
@@ -225,7 +214,6 @@ namespace {
 // trailing SYRK, `inv` (low priority) the triangular inverse of the fused factor
 // (gp2d_potrf_inv).  (Hardware CU masks splitting the CUs between the streams were measured
 // slower at every split)  One factorisation at a time per device.
-constexpr int kReserveCUs = 0;   // default CUs kept free of the bulk SYRK (GP2D_RESERVE_CUS)
 
 struct FactorStreams {
   std::mutex mu;
@@ -254,22 +242,11 @@ int factor_streams(FactorCtx& c, int nblk) {
   if (!g_fs.crit[dev]) {
     int lo = 0, hi = 0;
     if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) { lo = 0; hi = 0; }
-    // The diagonal kernel needs a whole CU (130 KB of LDS); with the bulk SYRK's workgroups
-    // (2 × 74 KB per CU) refilling every freed slot it can wait most of its run for one
-    // (777 µs per block in situ at n = 32768 vs 55 µs alone).  GP2D_RESERVE_CUS = R keeps the
-    // bulk stream off R CUs (the top R bits of its CU mask), so one is always free for crit.
-    const char* rv = std::getenv("GP2D_RESERVE_CUS");
-    const int reserve = rv ? std::atoi(rv) : kReserveCUs;
-    hipDeviceProp_t prop;
-    const int ncu = (hipGetDeviceProperties(&prop, dev) == hipSuccess) ? prop.multiProcessorCount : 0;
-    bool bulk_ok;
-    if (reserve > 0 && ncu > reserve) {
-      std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-      for (int c = 0; c < ncu - reserve; ++c) mask[c / 32] |= 1u << (c % 32);
-      bulk_ok = hipExtStreamCreateWithCUMask(&g_fs.bulk[dev], (uint32_t)mask.size(), mask.data()) == hipSuccess;
-    } else {
-      bulk_ok = hipStreamCreateWithPriority(&g_fs.bulk[dev], hipStreamNonBlocking, lo) == hipSuccess;
-    }
+    // crit (diagonal kernels, skinny panel GEMMs) and aux at the highest priority, bulk (the
+    // trailing SYRK) and inv (the fused inverse's GEMMs) at the lowest.  Keeping R CUs free of
+    // the bulk stream (CU-masked stream) was measured: no gain at N = 4096, slower at N = 16384
+    // (DESIGN.md §3.6).
+    const bool bulk_ok = hipStreamCreateWithPriority(&g_fs.bulk[dev], hipStreamNonBlocking, lo) == hipSuccess;
     if (hipStreamCreateWithPriority(&g_fs.crit[dev], hipStreamNonBlocking, hi) != hipSuccess || !bulk_ok ||
         hipStreamCreateWithPriority(&g_fs.aux[dev], hipStreamNonBlocking, hi) != hipSuccess ||
         hipStreamCreateWithPriority(&g_fs.inv[dev], hipStreamNonBlocking, lo) != hipSuccess) {
@@ -775,21 +752,14 @@ static int predict_ozaki_impl(const int8_t* wres, const double* rowscale, int nm
         std::lock_guard<std::mutex> lk(g_timing.mu);
         if (g_timing.on) { e0 = g_timing.get(); e1 = g_timing.get(); hipEventRecord(e0, s); }
       }
-      const bool narrow = igemm_tile_width() == 128;
-      const dim3 ggrid((unsigned)(ncols / (narrow ? 128 : IBN)), (unsigned)(n / IBM));
+      const dim3 ggrid((unsigned)(ncols / IBN), (unsigned)(n / IBM));
       for (int l = 0; l < nm; ++l) {
         const int8_t* Al = wres + (size_t)l * n * n;
         const int8_t* Bl = B + (size_t)l * bplane;
         uint8_t* Cl = cres + (size_t)l * n * ncols;
-        if (narrow)
-          igemm_nt_mod_kernel<128, 3><<<ggrid, 256, 0, s>>>(Al, Bl, Cl, n, (int)n, (int)ncols, (int)n, 1, oc.m[l],
-                                                            (int)(cp / IBN), (int)(ntr_pad / IBK),
-                                                            use_skip ? slist : nullptr, use_skip ? scnt : nullptr);
-        else
-          igemm_nt_mod_kernel<256, I_NSTAGE><<<ggrid, 512, 0, s>>>(Al, Bl, Cl, n, (int)n, (int)ncols, (int)n, 1,
-                                                                   oc.m[l], (int)(cp / IBN),
-                                                                   (int)(ntr_pad / IBK), use_skip ? slist : nullptr,
-                                                                   use_skip ? scnt : nullptr);
+        igemm_nt_mod_kernel<256, I_NSTAGE><<<ggrid, 512, 0, s>>>(Al, Bl, Cl, n, (int)n, (int)ncols, (int)n, 1, oc.m[l],
+                                                                 (int)(cp / IBN), (int)(ntr_pad / IBK),
+                                                                 use_skip ? slist : nullptr, use_skip ? scnt : nullptr);
         GP2D_CHECK(check_launch("igemm_nt_mod_kernel"));
       }
       if (e0) {
