@@ -715,8 +715,8 @@ static int predict_ozaki_impl(const int8_t* wres, const double* rowscale, int nm
   OzakiConsts oc;
   GP2D_CHECK(make_ozaki_consts(nmod, k, oc));
   const int nm = oc.nmod;
-  // the GEMM epilogue's biased sums (ozaki_mod_u31) stay below 2^31 for K = n < 2^16
-  GP2D_REQUIRE(n < 65536, "ozaki: the int8 GEMM epilogue needs n < 65536 (N_train < 32768)");
+  // the GEMM epilogue's biased sums (ozaki_mod_u32) stay below 2^32 for K = n < 2^17
+  GP2D_REQUIRE(n < 131072, "ozaki: the int8 GEMM epilogue needs n < 131072 (N_train < 65536)");
   const int64_t nmseg = (ntr_pad + OZ_KS_T - 1) / OZ_KS_T;
   const int64_t npseg = (n + OZ_CRT_ROWS - 1) / OZ_CRT_ROWS;
   const double kss = gp2d_kernel_diag(k);

@@ -288,6 +288,38 @@ __global__ __launch_bounds__(64) void ozaki_slab_list_kernel(const uint8_t* __re
   if (lane == 0) C[kslabs >> 2] = c;
 }
 
+// Modular reduction of the biased GEMM sums, all in full-rate 24-bit VALU operations.
+// The accumulators start at bias = m·⌈K·2^14 / m⌉ (≥ every |Σ a·b| with |a|, |b| ≤ 128), so
+// a sum v, read as unsigned, lies in [0, 2^32) for K < 2^17 (the int32 MFMA accumulation
+// wraps mod 2^32, the same bits).  With vh = v >> 20 (< 2^12) and c20 = 2^20 mod m,
+//   y = v − vh·(2^20 − c20) = (v mod 2^20) + vh·c20 ≡ v (mod m),   0 ≤ y < 2^20 + 2^20 = 2^21
+// (the 24-bit mad is exact mod 2^32 and its true result is below 2^21);
+// q = ⌊8y · ⌈2^29/m⌉ / 2^32⌋ (v_mul_hi_u32_u24: 8y < 2^24, and ⌈2^29/m⌉ < 2^24 for m > 32) is
+// exactly ⌊y/m⌋, since y·(⌈2^29/m⌉ − 2^29/m)/2^29 < 2^21/2^29 ≤ 1/m for m ≤ 256; r = y − q·m.
+struct OzModConsts {
+  int neg_c;       // −(2^20 − c20)
+  int neg_m;       // −m
+  uint32_t magic;  // ⌈2^29 / m⌉
+};
+__host__ __device__ inline uint32_t ozaki_acc_bias(int K, int m) {
+  return (uint32_t)((((int64_t)K << 14) + m - 1) / m * m);
+}
+__device__ __forceinline__ OzModConsts ozaki_mod_consts(int m) {
+  OzModConsts c;
+  c.neg_c = -((1 << 20) - (1 << 20) % m);
+  c.neg_m = -m;
+  c.magic = (uint32_t)(((1u << 29) + (uint32_t)m - 1) / (uint32_t)m);
+  return c;
+}
+__device__ __forceinline__ uint32_t ozaki_mod_u32(uint32_t v, const OzModConsts& c) {
+  int y, r;
+  uint32_t q;
+  asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(y) : "v"(v >> 20), "s"(c.neg_c), "v"(v));
+  asm("v_mul_hi_u32_u24 %0, %1, %2" : "=v"(q) : "s"(c.magic), "v"(y << 3));
+  asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(q), "s"(c.neg_m), "v"(y));
+  return (uint32_t)r;
+}
+
 // ------------------------------------------------------------------ INT8 NT GEMM mod m
 // C[i][j] = (Σ_k A[i][k]·B[j][k]) mod m, A lower-triangular (row block i0 needs k < i0+256).
 //
@@ -309,36 +341,6 @@ __global__ __launch_bounds__(64) void ozaki_slab_list_kernel(const uint8_t* __re
 // chunk ^ g((row>>2)&3) with g = [0,2,3,1], which spreads every group over 16 distinct
 // 4-bank slots.  The DMA writes LDS lane-linearly; the swizzle is applied on the global
 // source address (an involution, so the same formula maps both ways).
-// Modular reduction of the biased GEMM sums, all in full-rate 24-bit VALU operations.
-// The accumulators start at bias = m·⌈K·2^14 / m⌉ (≥ every |Σ a·b| with |a|, |b| ≤ 128), so
-// a sum v lies in [0, 2^31) for K < 2^16.  With vh = v >> 20 (< 2^11) and c20 = 2^20 mod m,
-//   y = v − vh·(2^20 − c20) = (v mod 2^20) + vh·c20 ≡ v (mod m),   0 ≤ y < 2^20 + 2^19;
-// q = ⌊8y · ⌈2^29/m⌉ / 2^32⌋ (v_mul_hi_u32_u24: 8y < 2^24, and ⌈2^29/m⌉ < 2^24 for m > 32) is
-// exactly ⌊y/m⌋, since y·(⌈2^29/m⌉ − 2^29/m)/2^29 < 2^21/2^29 ≤ 1/m for m ≤ 256; r = y − q·m.
-struct OzModConsts {
-  int neg_c;       // −(2^20 − c20)
-  int neg_m;       // −m
-  uint32_t magic;  // ⌈2^29 / m⌉
-};
-__host__ __device__ inline int ozaki_acc_bias(int K, int m) {
-  return (int)((((int64_t)K << 14) + m - 1) / m * m);
-}
-__device__ __forceinline__ OzModConsts ozaki_mod_consts(int m) {
-  OzModConsts c;
-  c.neg_c = -((1 << 20) - (1 << 20) % m);
-  c.neg_m = -m;
-  c.magic = (uint32_t)(((1u << 29) + (uint32_t)m - 1) / (uint32_t)m);
-  return c;
-}
-__device__ __forceinline__ uint32_t ozaki_mod_u31(uint32_t v, const OzModConsts& c) {
-  int y, r;
-  uint32_t q;
-  asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(y) : "v"(v >> 20), "s"(c.neg_c), "v"(v));
-  asm("v_mul_hi_u32_u24 %0, %1, %2" : "=v"(q) : "s"(c.magic), "v"(y << 3));
-  asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(q), "s"(c.neg_m), "v"(y));
-  return (uint32_t)r;
-}
-
 constexpr int IBM = 256, IBN = 256, IBK = 64;
 constexpr int I_OP = IBM * IBK;        // bytes per operand per stage (16 KB) = one layout tile
 constexpr int I_STAGE = 2 * I_OP;      // A then B
@@ -420,7 +422,7 @@ __global__ __launch_bounds__(TBN * 2, (TBN == 256) ? 1 : 2) void igemm_nt_mod_ke
 
   // the accumulators start at a multiple of m above every |Σ_k a·b| ≤ K·128² (centred
   // residues), so the sums leave the MFMAs non-negative and ≡ the true sums (mod m)
-  const int bias = ozaki_acc_bias(K, modulus);
+  const int bias = (int)ozaki_acc_bias(K, modulus);   // the bit pattern of an unsigned value
   i4v acc[8][4];
 #pragma unroll
   for (int mi = 0; mi < 8; ++mi)
@@ -560,7 +562,7 @@ __global__ __launch_bounds__(TBN * 2, (TBN == 256) ? 1 : 2) void igemm_nt_mod_ke
   }
   // Epilogue: residues mod m, packed 4 rows per dword into an LDS image of Cᵀ [col][row]
   // (pitch 272 B), then written out as coalesced 16-B row runs of the column-major residue
-  // plane.  Six full-rate VALU operations per residue (ozaki_mod_u31; no v_mul_lo_u32, no
+  // plane.  Six full-rate VALU operations per residue (ozaki_mod_u32; no v_mul_lo_u32, no
   // float conversions, no range fix-ups).
   uint8_t* T = reinterpret_cast<uint8_t*>(smem);
   constexpr int TP = IBM + 16;
@@ -572,7 +574,7 @@ __global__ __launch_bounds__(TBN * 2, (TBN == 256) ? 1 : 2) void igemm_nt_mod_ke
     for (int ni = 0; ni < 4; ++ni) {
       uint32_t pk = 0;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) pk |= ozaki_mod_u31((uint32_t)acc[mi][ni][u], mc) << (8 * u);
+      for (int u = 0; u < 4; ++u) pk |= ozaki_mod_u32((uint32_t)acc[mi][ni][u], mc) << (8 * u);
       const int rloc = wr * 128 + mi * 16 + 4 * lq;
       const int cloc = wc * 64 + ni * 16 + l16;
       *reinterpret_cast<uint32_t*>(T + cloc * TP + rloc) = pk;

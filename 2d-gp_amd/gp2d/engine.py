@@ -289,9 +289,9 @@ def fit(kernel: KernelSpec, x, y, noise: float, jitter: float = 0.0, device=None
     if ntr < 1:
         raise ValueError("need at least one training point")
     npad, n = fit_layout(kernel, ntr, variance)
-    if variance == "ozaki" and n >= 65536:
-        # the int8 GEMM epilogue's biased sums stay below 2^31 only for K = n < 2^16
-        raise ValueError(f"the ozaki variance engine supports n < 65536 (N_train < 32768); got n = {n}: "
+    if variance == "ozaki" and n >= 131072:
+        # the int8 GEMM epilogue's biased sums stay below 2^32 only for K = n < 2^17
+        raise ValueError(f"the ozaki variance engine supports n < 131072 (N_train < 65536); got n = {n}: "
                          "use variance='f64'")
     perm = None
     if variance == "ozaki" and ntr > 1:   # Morton order: exact-zero K* slabs cluster (skipped)

@@ -162,8 +162,8 @@ void   gp2d_ozaki_set_skip(int on);
  * coordinate (bbox: 6 doubles of device scratch).  The ozaki engine sorts training and grid
  * points by these codes so that all-zero K* tiles cluster into skippable slabs.          */
 int    gp2d_morton_codes(const double* pts, int64_t n, int dim, double* bbox, int64_t* codes, void* stream);
-/* gp2d_predict_ozaki / _planes need n < 65536 (N_train < 32768): the int8 GEMM's biased int32
- * sums must stay below 2^31 (the FP64 engine, gp2d_predict, has no such bound).          */
+/* gp2d_predict_ozaki / _planes need n < 131072 (N_train < 65536): the int8 GEMM's biased
+ * 32-bit sums must stay below 2^32 (the FP64 engine, gp2d_predict, has no such bound).    */
 int    gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int nmod, int64_t n,
                           const double* alpha, const double* xtr, int64_t ntr, int64_t ntr_pad,
                           const double* xg, int64_t m, const gp2d_kernel_t* k,

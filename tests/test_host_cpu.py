@@ -196,3 +196,33 @@ def test_bench_scaling_defaults(monkeypatch):
     monkeypatch.setattr(sys, "argv", ["bench.py", "--fit-mode", "bcast"])
     a = bench.parse()
     assert (a.grid_global, a.fit_mode) == (256, "bcast")
+
+
+def test_ozaki_epilogue_reduction_exact():
+    """The int8 GEMM epilogue's six-operation reduction (csrc/ozaki.hpp ozaki_mod_u32),
+    emulated bit for bit: for every modulus of the table and biased sums v anywhere in
+    [0, 2^32) (K < 2^17), y = v + (v >> 20)·(−(2^20 − 2^20 mod m)) mod 2^32 (v_mad_i32_i24),
+    q = hi32(8y · ⌈2^29/m⌉) (v_mul_hi_u32_u24, both operands < 2^24), r = y − q·m gives
+    0 ≤ r < m and r ≡ v (mod m)."""
+    moduli = [256, 255, 253, 251, 247, 241, 239, 233, 229, 227, 223, 217, 211, 199, 197, 193]
+    rng = np.random.default_rng(5)
+    edges = np.array([0, 1, 2 ** 20 - 1, 2 ** 20, 2 ** 31 - 1, 2 ** 31, 2 ** 32 - 2 ** 15, 2 ** 32 - 1],
+                     dtype=np.uint64)
+    v = np.concatenate([edges, rng.integers(0, 2 ** 32, 400_000, dtype=np.uint64)])
+    for m in moduli:
+        neg_c = -((1 << 20) - (1 << 20) % m)
+        magic = ((1 << 29) + m - 1) // m
+        assert magic < (1 << 24)
+        vh = v >> np.uint64(20)
+        y = (v.astype(np.int64) + vh.astype(np.int64) * neg_c) % (1 << 32)   # mod 2^32 like the mad
+        assert y.max() < (1 << 21)
+        y8 = y << 3
+        assert y8.max() < (1 << 24)
+        q = (y8 * magic) >> 32
+        r = y - q * m
+        assert r.min() >= 0 and r.max() < m, m
+        assert np.array_equal(r, (v % np.uint64(m)).astype(np.int64)), m
+    # the bias keeps every sum of K products of centred int8 residues in [0, 2^32)
+    for K, m in [(8192, 251), (32768, 193), (131071, 197)]:
+        bias = ((K << 14) + m - 1) // m * m
+        assert bias % m == 0 and bias - (K << 14) >= 0 and bias + (K << 14) < (1 << 32)
