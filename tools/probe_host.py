@@ -14,11 +14,14 @@ from gp2d import data as D  # noqa: E402
 from gp2d import distributed as GD  # noqa: E402
 from gp2d import engine as E  # noqa: E402
 
-x1, x2, u, v = D.synthetic_tracks(4096, seed=2016)
+NTR = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+G = int(sys.argv[2]) if len(sys.argv) > 2 else 256
+x1, x2, u, v = D.synthetic_tracks(NTR, seed=2016)
 xt = torch.tensor(np.stack([x1, x2], 1), device="cuda")
 yt = torch.tensor(np.concatenate([u, v]), device="cuda")
-_, _, xg = D.bbox_grid(x1, x2, 256, pad=5.0)
+_, _, xg = D.bbox_grid(x1, x2, G, pad=5.0)
 xg = torch.tensor(xg[:8192], device="cuda")
+xg_all = torch.tensor(D.bbox_grid(x1, x2, G, pad=5.0)[2], device="cuda")
 spec = E.KernelSpec(kind="df", l_df=5.0)
 gp = E.fit(spec, xt, yt, 0.0025, variance="ozaki")
 pred = E.Predictor(gp, 8192)
@@ -50,4 +53,21 @@ res = {"fit_enqueue_ms": host_ms(lambda: E.fit(spec, xt, yt, 0.0025, variance="o
        "predict_8192_enqueue_ms": host_ms(lambda: pred(xg)),
        "pack_enqueue_ms": host_ms(pack),
        "ozaki_prepare_enqueue_ms": host_ms(lambda: E.ozaki_prepare(gp, diag_add=0.0025))}
-print(res)
+res["full_predict_enqueue_ms"] = host_ms(lambda: pred(xg_all))
+
+
+def job_gpu():
+    E.fit(spec, xt, yt, 0.0025, variance="ozaki", check=False)
+    pred(xg_all)
+
+
+ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+torch.cuda.synchronize()
+ev0.record()
+for _ in range(10):
+    job_gpu()
+ev1.record()
+torch.cuda.synchronize()
+res["job_wall_ms"] = ev0.elapsed_time(ev1) / 10
+res["job_enqueue_ms"] = host_ms(job_gpu)
+print(NTR, G, res)
