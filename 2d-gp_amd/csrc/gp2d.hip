@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cmath>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -213,10 +214,12 @@ namespace {
 // (block-column updates, diagonal block, panel TRSM) at the highest priority, `bulk` the
 // trailing SYRK, `inv` (low priority) the triangular inverse of the fused factor
 // (gp2d_potrf_inv).  (Hardware CU masks splitting the CUs between the streams were measured
-// slower at every split)  One factorisation at a time per device.
+// slower at every split)  One factorisation enqueue at a time per device (a
+// per-device mutex held across potrf_impl serialises concurrent host threads).
 
 struct FactorStreams {
   std::mutex mu;
+  std::vector<std::unique_ptr<std::mutex>> enqueue;   // per device: one factorisation enqueue at a time
   std::vector<hipStream_t> crit, bulk, aux, inv;   // indexed by device
   std::vector<std::vector<hipEvent_t>> ev;         // 5 fixed events
   std::vector<std::vector<hipEvent_t>> blk;        // one per block column (fused inverse)
@@ -227,6 +230,7 @@ struct FactorCtx {
   hipStream_t crit, bulk, aux, inv;
   std::vector<hipEvent_t>* ev;
   std::vector<hipEvent_t>* blk;
+  std::mutex* enqueue;
 };
 
 int factor_streams(FactorCtx& c, int nblk) {
@@ -238,6 +242,7 @@ int factor_streams(FactorCtx& c, int nblk) {
     g_fs.inv.resize(dev + 1, nullptr);
     g_fs.ev.resize(dev + 1);
     g_fs.blk.resize(dev + 1);
+    while ((int)g_fs.enqueue.size() <= dev) g_fs.enqueue.push_back(std::make_unique<std::mutex>());
   }
   if (!g_fs.crit[dev]) {
     int lo = 0, hi = 0;
@@ -268,6 +273,7 @@ int factor_streams(FactorCtx& c, int nblk) {
   c.inv = g_fs.inv[dev];
   c.ev = &g_fs.ev[dev];
   c.blk = &g_fs.blk[dev];
+  c.enqueue = g_fs.enqueue[dev].get();
   return 0;
 }
 
@@ -373,6 +379,9 @@ static int potrf_impl(double* A, int64_t n, int64_t lda, double* dinv, int* info
   const bool fused = Tws != nullptr;
   FactorCtx fc;
   GP2D_CHECK(factor_streams(fc, fused ? 1 : 0));
+  // the device's internal streams and events are shared: two host threads factoring on one
+  // device would interleave their records and waits, so the whole enqueue sequence is serialised
+  std::lock_guard<std::mutex> enqueue_lock(*fc.enqueue);
   hipStream_t sc = fc.crit, sb = fc.bulk, sa = fc.aux, si = fc.inv;
   std::vector<hipEvent_t>& ev = *fc.ev;
   hipEvent_t e_pan = ev[0], e_syrk = ev[1], e_join = ev[2], e_start = ev[3], e_aux = ev[4];
@@ -1065,8 +1074,9 @@ int gp2d_transpose(const double* A, int64_t n, int64_t lda, double* At, void* st
 
 // ------------------------------------------------------------- RCCL broadcast
 // ncclBroadcast of the caller's communicator, resolved at first use from the RCCL the process
-// already has loaded (RTLD_NOLOAD: the library that created `comm`), else librccl.so.1 from
-// the ROCm install — no link-time dependency, so the engine loads where RCCL is absent.
+// already has loaded (dlsym(RTLD_DEFAULT), then an RTLD_NOLOAD librccl.so.1: the library that
+// created `comm`), else librccl.so.1 from the ROCm install — no link-time dependency, so the
+// engine loads where RCCL is absent.  `comm` must come from that same RCCL instance.
 }  // extern "C"
 namespace {
 typedef int (*rccl_bcast_fn)(const void*, void*, size_t, int, int, void*, hipStream_t);
@@ -1078,6 +1088,11 @@ struct RcclSyms {
 const RcclSyms& rccl_syms() {
   static const RcclSyms r = [] {
     RcclSyms x;
+    // 1. whatever RCCL the process already resolves globally (the one that made `comm`, under
+    //    any file name); 2. an already loaded librccl.so.1; 3. the ROCm install's copy
+    x.bcast = reinterpret_cast<rccl_bcast_fn>(dlsym(RTLD_DEFAULT, "ncclBroadcast"));
+    x.errstr = reinterpret_cast<rccl_errstr_fn>(dlsym(RTLD_DEFAULT, "ncclGetErrorString"));
+    if (x.bcast) return x;
     void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
     if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
     if (h) {

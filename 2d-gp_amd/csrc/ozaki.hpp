@@ -373,7 +373,8 @@ __device__ __forceinline__ void vmwait_barrier(std::integral_constant<int, W>) {
 //
 // Two shapes (TBN = output columns per workgroup; rows are always 256 = IBM):
 //   TBN = 256: 512 threads, 8 waves as 2×4, one workgroup per CU, 4-stage ring (128 KB).
-//   TBN = 128: (alternative, measured slower — see igemm_tile_width in gp2d.hip)
+//   TBN = 128: (alternative, measured slower; instantiated only in tools/microbench/igemm_bench.hip
+//              (IG_TBN), numbers in DESIGN.md §3.6)
 //              256 threads, 4 waves as 2×2, TWO workgroups per CU, 3-stage ring of 24 KB
 //              stages (72 KB each).  Every wave computes the same 128×64 register tile as in
 //              the 256 shape and a SIMD still holds two waves, but they belong to different

@@ -112,7 +112,8 @@ def fit_sharded(spec: E.KernelSpec, x, y, noise: float, device, mode: str = "bca
 
 
 def krige_jobs_sharded(jobs, variance: str = "ozaki", chunk: int = 8192, var_mode: str = "latent",
-                       compute_var: bool = True, jitter: float = 0.0, device=None, align: int = 64):
+                       compute_var: bool = True, jitter: float = 0.0, device=None, align: int = 64,
+                       stats: dict | None = None):
     """A stream of independent kriging jobs (kernel, x, y, noise, xg) — the reference's
     runKrig.py sweep / per-window krig.kriging calls — spread over all ranks: job j is FITTED
     by rank j mod world only (round robin, on a side stream, up to one job per rank ahead),
@@ -124,7 +125,9 @@ def krige_jobs_sharded(jobs, variance: str = "ozaki", chunk: int = 8192, var_mod
     Per job a rank does 1/world of a fit plus 1/world of the predict, so for a stream of jobs
     the fit — the serial part of a one-job multi-GPU predict — is divided like the grid
     (DESIGN.md §5).  Every rank must pass the same job sequence (x, y are read on the owner
-    only); a non-SPD K_y raises numpy.linalg.LinAlgError on every rank at that job."""
+    only); a non-SPD K_y raises numpy.linalg.LinAlgError on every rank at that job.  Nothing is
+    read ahead before the first next(); `stats` counts the fits this rank issues (with their
+    host time stamps, engine.note_fit_issued)."""
     ws, rank = world()
     dev = E._require_device(device)
     if ws == 1:   # one rank: the single-GPU pipelined form (the next fit under this predict)
@@ -135,7 +138,7 @@ def krige_jobs_sharded(jobs, variance: str = "ozaki", chunk: int = 8192, var_mod
                 seen.append(job)
                 yield job
         for mean, var in E.krige_jobs(feed(), variance=variance, chunk=chunk, var_mode=var_mode,
-                                      compute_var=compute_var, jitter=jitter, device=dev):
+                                      compute_var=compute_var, jitter=jitter, device=dev, stats=stats):
             xg = seen.popleft()[4]
             yield 0, int(xg.shape[0]), mean, var
         return
@@ -159,6 +162,7 @@ def krige_jobs_sharded(jobs, variance: str = "ozaki", chunk: int = 8192, var_mod
             if idx % ws == rank and idx not in own:
                 spec, x, y, noise, _ = job
                 fit_stream.wait_stream(main)
+                E.note_fit_issued(stats)
                 gp, err = None, None
                 with torch.cuda.stream(fit_stream):
                     try:
@@ -207,7 +211,7 @@ def krige_jobs_sharded(jobs, variance: str = "ozaki", chunk: int = 8192, var_mod
         gp, ready = cur
         main.wait_event(ready)
         gp.record_stream(main)
-        if pred is None or pred.gp.n != gp.n or pred.ozaki != ("ozaki" in gp.extra):
+        if pred is None or not pred.fits(gp):
             pred = E.Predictor(gp, chunk)
         pred.gp = gp
         out = predict_shard(pred, E._as_points(xg, spec.input_dim, dev), var_mode=var_mode,

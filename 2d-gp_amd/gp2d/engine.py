@@ -12,6 +12,7 @@ Reference call sites replaced:
 from __future__ import annotations
 
 import ctypes
+import time
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -477,6 +478,12 @@ class Predictor:
             self.wbytes = int(N.lib().gp2d_predict_workspace(gp.n, self.chunk, bd))
         self.work = torch.empty(self.wbytes // 8 + 1, dtype=torch.float64, device=gp.device)
 
+    def fits(self, gp: GPFit) -> bool:
+        """True if this workspace serves `gp` as is: same matrix order, engine and block size
+        (the FP64 workspace and the chunk rounding depend on the block size)."""
+        return (self.gp.n == gp.n and self.ozaki == ("ozaki" in gp.extra)
+                and self.gp.kernel.block_dim == gp.kernel.block_dim)
+
     def __call__(self, xg, var_mode: str = "latent", compute_var: bool = True, out=None,
                  planes: KstarPlanes | None = None):
         """planes: K* residue planes of this same grid from kstar_planes() (ozaki engine):
@@ -539,8 +546,16 @@ def predict(gp: GPFit, xg, var_mode: str = "latent", compute_var: bool = True, c
     return Predictor(gp, chunk)(xg, var_mode=var_mode, compute_var=compute_var)
 
 
+def note_fit_issued(stats: dict | None):
+    """Count a fit enqueued by a job stream (krige_jobs / krige_jobs_sharded) with its host
+    time stamp — bench.py checks that every timed job's fit is issued inside its clock."""
+    if stats is not None:
+        stats["fits_issued"] = stats.get("fits_issued", 0) + 1
+        stats.setdefault("fit_issue_times", []).append(time.perf_counter())
+
+
 def krige_jobs(jobs, variance: str = "ozaki", chunk: int = 8192, var_mode: str = "latent",
-               compute_var: bool = True, jitter: float = 0.0, device=None):
+               compute_var: bool = True, jitter: float = 0.0, device=None, stats: dict | None = None):
     """Independent kriging jobs (kernel, x, y, noise, xg), one after another — the reference's
     runKrig.py:1-40 sweep (one GP_laser / krig.kriging fit + grid predict per setting or
     time window) run in one process.  Yields (mean, var) per job, in order, on the current
@@ -551,7 +566,9 @@ def krige_jobs(jobs, variance: str = "ozaki", chunk: int = 8192, var_mode: str =
     (bench.py --pipeline).  The fit of job i+1 waits for the work queued on the
     current stream before it (so input tensors made there are ready); a non-SPD K_y of job i
     raises numpy.linalg.LinAlgError when job i is yielded, as fit() would.  The predict
-    workspace is reused while consecutive jobs have the same padded size."""
+    workspace is reused while consecutive jobs have the same padded size.  Nothing is read
+    ahead before the first next(): a fresh generator's first fit is issued by that call (the
+    bench times its jobs on a fresh generator for this reason).  `stats` counts the fits issued."""
     dev = _require_device(device)
     main = torch.cuda.current_stream(dev)
     side = torch.cuda.Stream(dev)
@@ -559,6 +576,7 @@ def krige_jobs(jobs, variance: str = "ozaki", chunk: int = 8192, var_mode: str =
     def queue_fit(job):
         kernel, x, y, noise, _ = job
         side.wait_stream(main)
+        note_fit_issued(stats)
         with torch.cuda.stream(side):
             return fit(kernel, x, y, noise, jitter=jitter, device=dev, variance=variance, check=False)
 
@@ -571,7 +589,7 @@ def krige_jobs(jobs, variance: str = "ozaki", chunk: int = 8192, var_mode: str =
         gp.record_stream(main)
         nxt = next(it, None)
         gp_next = queue_fit(nxt) if nxt is not None else None
-        if pred is None or pred.gp.n != gp.n or pred.ozaki != ("ozaki" in gp.extra):
+        if pred is None or not pred.fits(gp):
             pred = Predictor(gp, chunk)
         pred.gp = gp
         out = pred(job[4], var_mode=var_mode, compute_var=compute_var)

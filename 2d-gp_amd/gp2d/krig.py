@@ -200,7 +200,8 @@ class Krig:
         d = dict(X=_to_numpy(self._X), y=_to_numpy(self._y), family=s.family, kind=str(s.kind), l_df=s.l_df,
                  l_cf=s.l_cf, ratio=s.ratio, variances=np.asarray(s.variances, dtype=np.float64),
                  lengthscales=np.asarray(s.lengthscales, dtype=np.float64), var_t=s.var_t, l_t=s.l_t,
-                 noise=self.noise, jitter=self.jitter,
+                 noise=self.noise, jitter=self.jitter, jitchol=self.jitchol,
+                 jitchol_used=float(self.gp.extra.get("jitchol", 0.0)),
                  var_mode=self.var_mode, variance=self.variance, chunk=self.chunk)
         if with_factor:
             d["W"] = _to_numpy(self.gp.W)
@@ -228,16 +229,22 @@ class Krig:
         extra = {}
         if "variance" in z.files:
             extra = dict(variance=str(z["variance"]), chunk=int(z["chunk"]))
+        if "jitchol" in z.files:
+            extra["jitchol"] = int(z["jitchol"])
         k = cls(spec, noise=float(z["noise"]), jitter=float(z["jitter"]), var_mode=str(z["var_mode"]),
                 device=device, **extra)
         if "W" in z.files:
-            k._restore(z["X"], z["y"], z["W"], z["alpha"], z["perm"] if "perm" in z.files else None)
+            used = float(z["jitchol_used"]) if "jitchol_used" in z.files else 0.0
+            k._restore(z["X"], z["y"], z["W"], z["alpha"], z["perm"] if "perm" in z.files else None, used)
         elif refit:
             k.fit(z["X"], z["y"])
         return k
 
-    def _restore(self, X, y, W, alpha, perm):
-        """Rebuild the device fit from a saved factor (no assembly, no factorisation)."""
+    def _restore(self, X, y, W, alpha, perm, jitchol_used: float = 0.0):
+        """Rebuild the device fit from a saved factor (no assembly, no factorisation).
+        `jitchol_used` is the jitter a jitchol retry added to the saved factor's K_y diagonal:
+        the Ozaki residue planes take the a-priori moduli count from the diagonal the factor was
+        built with (noise + jitter + that jitter), exactly as fit() did."""
         dev = E._require_device(self.device)
         spec = self.spec
         bd, d = spec.block_dim, spec.input_dim
@@ -257,8 +264,9 @@ class Krig:
         gp = E.GPFit(kernel=spec, noise=self.noise, x=Xd, n_train=ntr, n_pad=npad,
                      W=torch.as_tensor(np.ascontiguousarray(W), device=dev),
                      alpha=torch.as_tensor(np.ascontiguousarray(alpha), device=dev), device=dev, y=Y, perm=pm)
+        gp.extra["jitchol"] = float(jitchol_used)
         if self.variance == "ozaki":
-            E.ozaki_prepare(gp, diag_add=self.noise + self.jitter)
+            E.ozaki_prepare(gp, diag_add=float(self.noise + (self.jitter + jitchol_used)))
         self.gp = gp
         self._pred = E.Predictor(gp, self.chunk)
         self._X, self._y = X, y

@@ -91,9 +91,9 @@ def parse():
         a.kind, a.ntrain, a.grid = "mixed", 4096, 256
     elif a.config == "D":
         a.kind, a.ntrain, a.grid_global = "mixed", 16384, 512
-    if a.steps is None:
-        a.steps = {"D": 4, "E": 2}.get(a.config, 100)
     ws = int(os.environ.get("WORLD_SIZE", "1"))
+    if a.steps is None:   # config D: every rank owns at least two of the timed jobs' fits
+        a.steps = {"D": max(4, 2 * ws), "E": 2}.get(a.config, 100)
     if a.grid_global == 0 and ws > 1 and a.scaling in ("auto", "strong"):
         a.grid_global = a.grid   # N>1 default: one job grid sharded over the ranks
     if a.fit_mode is None:
@@ -246,6 +246,7 @@ def main():
         a = args.kstar_ahead
         cfg["ahead"] = args.variance == "ozaki" and (a == 1 or (a == -1 and ws > 1 and mode == "bcast"))
 
+    stats = {}      # fits issued (engine.note_fit_issued): every timed job's fit must be issued after t0
     last = [None]   # the previous step's fit: its non-SPD check runs one step late (no host sync)
 
     def check_last():
@@ -257,10 +258,12 @@ def main():
     main_stream = torch.cuda.current_stream(dev)
 
     def do_fit():
+        if cfg["mode"] != "bcast" or rank == 0:   # bcast: rank 0 fits every job
+            E.note_fit_issued(stats)
         if not cfg["pipeline"]:
             return GD.fit_sharded(spec, xt, yt, noise, dev, mode=cfg["mode"], variance=args.variance, check=False)
-        # job i+1's fit is queued on its own stream behind job i's fit only, so it runs while
-        # job i's predict (main stream) does; the predict waits for its own fit's event
+        # the fit is queued on its own stream behind the previous fit only, so it runs while
+        # the previous job's predict (main stream) does; the predict waits for its own fit's event
         fit_stream.wait_stream(main_stream) if cfg["first"] else None
         cfg["first"] = False
         with torch.cuda.stream(fit_stream):
@@ -275,7 +278,7 @@ def main():
             pred_cache["k"] = planes
         gp = do_fit()
         pr = pred_cache.get("p")
-        if pr is None or pr.gp.n != gp.n or pr.ozaki != ("ozaki" in gp.extra):
+        if pr is None or not pr.fits(gp):
             pr = E.Predictor(gp, args.chunk)
             pred_cache["p"] = pr
         pr.gp = gp
@@ -323,47 +326,80 @@ def main():
                    "ms_per_step": 1e3 * (tu1 - tu0) / args.unpipelined_steps, "steps": args.unpipelined_steps,
                    "kernel_ms": ukms, "kernel_launches": uklaunch, "kernel_flops": ukflops}
         cfg["pipeline"] = True
-    run = step
-    api = "engine.fit + Predictor"
+    # A job stream (engine.krige_jobs / distributed.krige_jobs_sharded) reads no job ahead before
+    # its first next(), so warmup and timed jobs run on separate generators: the warmup one is
+    # drained before the clock starts, and the timed one is created after t0 — every timed job's
+    # fit (including the first, and at N > 1 the whole fill of the fit window) is inside the clock.
+    stream, api = None, "engine.fit + Predictor"
     if cfg["mode"] == "rr":
         # the global grid on every rank; each job's fit on one rank, its shard predicted on all
-        xg_full = torch.tensor(xg_all, device=dev)
-        jobs = GD.krige_jobs_sharded(itertools.repeat((spec, xt, yt, noise, xg_full), args.warmup + args.steps),
-                                     variance=args.variance, chunk=args.chunk)
-        run = functools.partial(next, jobs)
+        job = (spec, xt, yt, noise, torch.tensor(xg_all, device=dev))
+
+        def stream(k):
+            return GD.krige_jobs_sharded(itertools.repeat(job, k), variance=args.variance, chunk=args.chunk,
+                                         stats=stats)
         api = "distributed.krige_jobs_sharded"
     elif cfg["pipeline"] and cfg["mode"] in ("local", "replicate") and not cfg["ahead"]:
-        # the shipped API for a sweep of jobs: engine.krige_jobs (one generator over warmup +
-        # timed jobs, so no fit is queued past the last timed job and none is left unoverlapped)
-        jobs = E.krige_jobs(itertools.repeat((spec, xt, yt, noise, xg), args.warmup + args.steps),
-                            variance=args.variance, chunk=args.chunk)
-        run = functools.partial(next, jobs)
+        job = (spec, xt, yt, noise, xg)
+
+        def stream(k):   # the shipped API for a sweep of jobs
+            return E.krige_jobs(itertools.repeat(job, k), variance=args.variance, chunk=args.chunk, stats=stats)
         api = "engine.krige_jobs"
-    for _ in range(args.warmup):
-        run()
+    trace = os.environ.get("GP2D_BENCH_TRACE") == "1"   # per-step wall times on stderr (diagnostics)
+
+    def run_jobs(k, t_ref=None):
+        it = stream(k) if stream is not None else (step() for _ in range(k))
+        for i, _ in enumerate(it):
+            if trace and t_ref is not None:
+                torch.cuda.synchronize()
+                print(f"[rank {rank}] step {i}: {1e3 * (time.perf_counter() - t_ref):.1f} ms since start",
+                      file=sys.stderr, flush=True)
+        check_last()
+
+    # round robin: at least one warmup job per rank, so every rank has fitted before the clock
+    warm = max(args.warmup, ws) if cfg["mode"] == "rr" else args.warmup
+    run_jobs(warm)
     barrier(ws)
     E.timing_enable(True)
     E.timing_read()
+    stats.clear()
     barrier(ws)
     t0 = time.perf_counter()
-    trace = os.environ.get("GP2D_BENCH_TRACE") == "1"   # per-step wall times on stderr (diagnostics)
-    for i in range(args.steps):
-        run()
-        if trace:
-            torch.cuda.synchronize()
-            print(f"[rank {rank}] step {i}: {1e3 * (time.perf_counter() - t0):.1f} ms since start", file=sys.stderr,
-                  flush=True)
-    check_last()
+    run_jobs(args.steps, t0)
     barrier(ws)
     t1 = time.perf_counter()
     kms, klaunch, kflops = E.timing_read()
     E.timing_enable(False)
+    # fits issued inside [t0, t1] on this rank (all of this rank's fits of the timed jobs)
+    fit_times = stats.get("fit_issue_times", [])
+    fits = torch.tensor([sum(t0 <= t <= t1 for t in fit_times), len(fit_times)], dtype=torch.float64, device=dev)
     dt = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
     if ws > 1:
         dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+        dist.all_reduce(fits, op=dist.ReduceOp.SUM)
     elapsed = float(dt.item())
     ms_per_step = 1e3 * elapsed / args.steps
     value = m_all * args.steps / elapsed
+    fits_expected = args.steps * (1 if cfg["mode"] in ("rr", "bcast") or ws == 1 else ws)
+    timed_fits = {"issued_in_window": int(fits[0].item()), "issued_total": int(fits[1].item()),
+                  "expected": fits_expected, "warmup_jobs_run": warm}
+    if timed_fits["issued_in_window"] != fits_expected or timed_fits["issued_total"] != fits_expected:
+        raise RuntimeError(f"bench: timed region holds {timed_fits} fits, expected {fits_expected}")
+
+    # one job alone (unpipelined, its grid sharded over the ranks; at N > 1 fitted on rank 0 and
+    # broadcast): the single-job reading beside the job-stream value
+    reps = 1 if args.ntrain > 8192 else 3
+    barrier(ws)
+    ts = time.perf_counter()
+    for _ in range(reps):
+        run_jobs(1) if stream is not None else (step(), check_last())
+    barrier(ws)
+    dts = torch.tensor([time.perf_counter() - ts], dtype=torch.float64, device=dev)
+    if ws > 1:
+        dist.all_reduce(dts, op=dist.ReduceOp.MAX)
+    single_ms = 1e3 * float(dts.item()) / reps
+    single_job = {"ms": single_ms, "value": m_all / (single_ms * 1e-3), "reps": reps,
+                  "fit": "rank 0, factor broadcast" if ws > 1 else "local"}
 
     # mean-only throughput (secondary, same fit; at most 20 jobs)
     mo_steps = min(args.steps, 20)
@@ -451,6 +487,8 @@ def main():
         "pipelined": cfg["pipeline"],
         "api": api,
         "unpipelined": unpiped,
+        "single_job": single_job,
+        "timed_fits": timed_fits,
         "mean_only_value": mean_only,
     }
     if ws == 1 and (args.cpu_baseline > 0 or (args.cpu_baseline < 0 and args.ntrain <= 4096)):

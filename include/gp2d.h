@@ -89,7 +89,10 @@ int gp2d_assemble(const double* xa, int64_t na, int64_t na_pad,
  * 128).  Replaces np.linalg.inv(K) (GP_laser.py:118, GP_scripts.py:50) and the
  * Cholesky inside GPy / sklearn (_gpr.py:349).  On return the strict upper
  * triangle is zero.  If dinv != NULL it receives the (n/128) inverted 128×128
- * diagonal blocks (input to gp2d_trtri).  *info_dev as LAPACK potrf.            */
+ * diagonal blocks (input to gp2d_trtri).  *info_dev as LAPACK potrf.
+ * Thread safety: the factorisation runs on internal per-device streams and events
+ * joined to `stream`; concurrent calls for one device from several host threads are
+ * serialised (a per-device lock is held while the work is enqueued).            */
 size_t gp2d_potrf_workspace(int64_t n);
 int gp2d_potrf(double* A, int64_t n, int64_t lda, double* dinv, int* info_dev,
                void* work, size_t work_bytes, void* stream);

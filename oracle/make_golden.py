@@ -308,6 +308,41 @@ def gen_configs(gs, out):
     np.savez_compressed(os.path.join(out, "configs_N4096.npz"), **d)
 
 
+def gen_config_b(gs, out):
+    """BASELINE config B at its real workload: div-free (α = 1, ℓ = 5 km, noise 0.0025),
+    N_train = 1024 bench tracks (gp2d.data.synthetic_tracks(1024, seed=2016)), the whole
+    128 × 128 bbox grid (bbox_grid(…, 128, pad=5)) through the reference's GP_laser.py:113-134
+    recipe with its vectorised myKernel and np.linalg.inv — mean and variance at ALL 16,384
+    points — plus the refined posterior (_refined_posterior) at the 512-point subsample for the
+    elementwise gate."""
+    x, y, u, v = synthetic_tracks(1024)
+    xa = np.stack([x, y], 1)
+    gx = np.linspace(x.min() - 5, x.max() + 5, 128)      # = gp2d.data.bbox_grid(x, y, 128, pad=5)
+    gy = np.linspace(y.min() - 5, y.max() + 5, 128)
+    GX, GY = np.meshgrid(gx, gy)
+    xg = np.stack([GX.reshape(-1), GY.reshape(-1)], 1)
+    obs = np.concatenate([u, v])
+    t0 = time.time()
+    K = gs["myKernel"](xa, xa, 5.0, 5.0, 1.0)
+    K = K + np.identity(K.shape[0]) * 0.0025             # GP_laser.py:114-115
+    Ki = np.linalg.inv(K)                                # GP_laser.py:118
+    Ks = gs["myKernel"](xg, xa, 5.0, 5.0, 1.0)           # GP_laser.py:122 (vectorised form)
+    f = np.ravel(gs["getMean"](Ks, Ki, obs[:, None]))    # GP_laser.py:134
+    d0 = np.diag(gs["myKernel"](xg[:2], xg[:2], 5.0, 5.0, 1.0))   # the diagonal is constant (r = 0)
+    assert np.all(d0 == d0[0])
+    kss = np.full(2 * xg.shape[0], d0[0])
+    var = kss - np.einsum("ij,ij->i", Ks, Ks @ Ki)       # diag of GP_laser.py:129
+    idx = config_subsample(xa, xg)
+    M = xg.shape[0]
+    rows = np.concatenate([idx, M + idx])
+    mr, vr = _refined_posterior(K, Ks[rows], kss[rows], obs)
+    print(f"  config B: N=1024, {M} points, {time.time() - t0:.1f}s; inv recipe vs refined at {idx.size}: "
+          f"var elementwise {np.max(np.abs(var[rows] - vr) / vr):.1e}")
+    np.savez_compressed(os.path.join(out, "config_b_full.npz"), x_sum=np.array([x.sum(), y.sum()]),
+                        u_sum=np.array([u.sum(), v.sum()]), xg_sum=xg.sum(0), mean=f, var=var, idx=idx,
+                        mean_refined=mr, var_refined=vr)
+
+
 def gen_config_d(gs, out):
     """BASELINE config D on rank 0's shard: mixed (α = ½, ℓ = 5), N_train = 16384 (a 32768²
     K), the 512 × 512 bbox grid cut into 8 shards (gp2d.data.shard_range) — rank 0 holds the
@@ -698,7 +733,8 @@ def main():
                 indices=lambda: gen_indices(a.out), grids=lambda: gen_grids(a.out),
                 lml=lambda: gen_lml(gs, a.out), st=lambda: gen_st(gs, a.out),
                 prep=lambda: gen_prep(a.out), window=lambda: gen_prior_window(a.out),
-                configs=lambda: gen_configs(gs, a.out), config_d=lambda: gen_config_d(gs, a.out),
+                configs=lambda: gen_configs(gs, a.out), config_b=lambda: gen_config_b(gs, a.out),
+                config_d=lambda: gen_config_d(gs, a.out),
                 config_e=lambda: gen_config_e(gs, a.out))
     for name, fn in jobs.items():
         if a.only and name not in a.only.split(","):

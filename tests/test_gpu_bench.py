@@ -29,6 +29,9 @@ def test_bench_json_contract(variance):
     assert d["n_gpus"] == 1 and d["steps"] == 2 and d["warmup"] == 1 and d["higher_is_better"] is True
     assert d["value"] > 0 and abs(d["value"] - 32 * 32 / (d["ms_per_step"] * 1e-3)) / d["value"] < 1e-6
     assert d["vs_baseline"] is None and d["scaling"] == "weak" and "workload" in d["config"]
+    # every timed job's fit is issued inside the clock (a fresh job generator after t0)
+    assert d["timed_fits"]["issued_in_window"] == d["timed_fits"]["issued_total"] == 2
+    assert d["single_job"]["ms"] > 0
     r = d["roofline"]
     for key in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
         assert key in r, key
@@ -58,3 +61,6 @@ def test_bench_two_ranks_default_contract():
     assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["api"] == "distributed.krige_jobs_sharded"
     assert abs(d["value"] - 64 * 64 / (d["ms_per_step"] * 1e-3)) / d["value"] < 1e-6
     assert "cpu_baseline" not in d and d["roofline"]["frac"] > 0
+    # job j is fitted by rank j mod 2 only: the 4 timed jobs' 4 fits, all issued after t0
+    assert d["timed_fits"]["issued_in_window"] == d["timed_fits"]["issued_total"] == 4
+    assert d["timed_fits"]["warmup_jobs_run"] >= 2

@@ -9,6 +9,9 @@ container; /root/reference is not read here):
     same posterior with an extended-precision refinement step (make_golden._refined_posterior).
   * config_d_rank0.npz — config D's rank-0 shard (N_train = 16384, 32768 of the 512² points).
   * config_e_share.npz — rank 0's share of config E's 64-setting sweep at N_train = 4096.
+  * config_b_full.npz — config B at its real workload (div-free, N_train = 1024, the whole
+    128 × 128 grid): the reference recipe's mean / variance at all 16,384 points, the refined
+    posterior at the 512-point subsample.
 
 Gates (north_star: fp64 posterior mean / variance within 1e-10 relative):
   * normwise: max|a − b| / max|b| ≤ 1e-10 per output vector, against the reference recipe;
@@ -138,3 +141,47 @@ def test_config_e_sweep_share(golden):
         # ∂/∂ℓ: the fixture's central difference is good to ~1e-8 relative; ∂/∂noise is exact
         assert abs(grads[j, il] - ref[0]) < 1e-6 * abs(ref[0])
         assert abs(grads[j, inz] - ref[1]) < 1e-9 * abs(ref[1])
+
+
+@pytest.mark.parametrize("variance", ["ozaki", "f64"])
+def test_config_b_full_grid(golden, variance):
+    """Config B exactly as `bench.py --config B` runs it (df, N_train = 1024, 128² grid, 8192-point
+    chunks): normwise per component over ALL 16,384 grid points against the reference recipe,
+    elementwise at the 512 subsample points against the refined posterior."""
+    g = golden("config_b_full.npz")
+    x1, x2, u, v = D.synthetic_tracks(1024, seed=2016)
+    assert np.array_equal(g["x_sum"], [x1.sum(), x2.sum()]) and np.array_equal(g["u_sum"], [u.sum(), v.sum()])
+    _, _, xg = D.bbox_grid(x1, x2, 128, pad=5.0)
+    assert np.array_equal(g["xg_sum"], xg.sum(0))
+    ks = E.KernelSpec(kind="df", l_df=5.0)
+    gp = E.fit(ks, torch.tensor(np.stack([x1, x2], 1), device="cuda"),
+               torch.tensor(np.concatenate([u, v]), device="cuda"), noise=0.0025, variance=variance)
+    mu, var = (t.cpu().numpy() for t in E.Predictor(gp, 8192)(torch.tensor(xg, device="cuda")))
+    m = xg.shape[0]
+    for c in (slice(0, m), slice(m, 2 * m)):
+        assert rel(mu[c], g["mean"][c]) < GATE
+        assert rel(var[c], g["var"][c]) < GATE
+    rows = np.concatenate([g["idx"], m + g["idx"]])
+    ev, em = elem_var(var[rows], g["var_refined"]), elem_mean(mu[rows], g["mean_refined"])
+    print(f"B/{variance}: var normwise {rel(var, g['var']):.2e}, var elementwise {ev:.2e}, mean elementwise {em:.2e}")
+    assert ev < GATE and em < GATE
+
+
+def test_headline_ozaki_full_grid_elementwise(n4096):
+    """The headline's Ozaki variance at EVERY one of the 65,536 grid points (both components),
+    elementwise against the FP64-MFMA engine on the same fit inputs (itself 4e-12 from the
+    refined posterior at the fixture points): max_j |v_oz − v_f64| / v_f64 ≤ 1e-10; the mean
+    (fp64 K*α on both engines, different point orders) elementwise with the mean floor."""
+    g, x, y, xg = n4096
+    ks = E.KernelSpec(kind="df", l_df=5.0)
+    xt, yt, gt = (torch.tensor(a, device="cuda") for a in (x, y, xg))
+    out = {}
+    for variance in ("ozaki", "f64"):
+        gp = E.fit(ks, xt, yt, noise=0.0025, variance=variance)
+        out[variance] = [t.cpu().numpy() for t in E.Predictor(gp, 8192)(gt)]
+        del gp
+    (mo, vo), (mf, vf) = out["ozaki"], out["f64"]
+    assert vo.size == 2 * 65536 and np.all(vf > 0)
+    ev, em = elem_var(vo, vf), elem_mean(mo, mf)
+    print(f"headline full grid, Ozaki vs FP64 engine: var elementwise {ev:.2e}, mean elementwise {em:.2e}")
+    assert ev < GATE and em < GATE

@@ -202,3 +202,45 @@ def test_round_robin_jobs_non_spd_raises_on_every_rank(tmp_path):
     _spawn(_rr_worker, world, str(tmp_path), "ozaki", 3)
     for i in range(world):
         assert int(np.load(os.path.join(tmp_path, f"rr{i}.npz"))["raised"]) == 3, i
+
+
+def _window_worker(rank, world, port, out_dir):
+    """bench.py's timing pattern: a warmup generator drained, then t0, then a FRESH generator
+    over the timed jobs; the fits this rank issues are stamped (stats)."""
+    for p in (ROOT, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import time
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from gp2d import distributed as GD
+    job = _jobs()[0]
+    for _ in GD.krige_jobs_sharded([job] * 2, chunk=1024):
+        pass
+    torch.cuda.synchronize()
+    dist.barrier()
+    stats = {}
+    t0 = time.perf_counter()
+    n_out = sum(1 for _ in GD.krige_jobs_sharded([job] * 5, chunk=1024, stats=stats))
+    torch.cuda.synchronize()
+    dist.barrier()
+    t1 = time.perf_counter()
+    ts = np.asarray(stats.get("fit_issue_times", []))
+    np.savez(os.path.join(out_dir, f"win{rank}.npz"), inside=int(((ts >= t0) & (ts <= t1)).sum()), total=len(ts),
+             issued=int(stats.get("fits_issued", 0)), n_out=n_out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_round_robin_timed_window_holds_every_fit(tmp_path):
+    """With a fresh krige_jobs_sharded generator started after t0, the fits of all 5 timed jobs
+    are issued inside [t0, t1] — 3 on rank 0 (jobs 0, 2, 4), 2 on rank 1 — and none before."""
+    world = 2
+    _spawn(_window_worker, world, str(tmp_path))
+    r = [np.load(os.path.join(tmp_path, f"win{i}.npz")) for i in range(world)]
+    assert [int(x["total"]) for x in r] == [3, 2]
+    assert [int(x["inside"]) for x in r] == [3, 2]
+    assert [int(x["issued"]) for x in r] == [3, 2]
+    assert all(int(x["n_out"]) == 5 for x in r)

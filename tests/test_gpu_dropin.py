@@ -158,3 +158,36 @@ def test_krig_checkpoint_restores_without_refit(tmp_path, variance, monkeypatch)
     mu2, var2 = k2.predict(xg)
     assert np.array_equal(mu, mu2) and np.array_equal(var, var2)
     assert k2.log_likelihood() == pytest.approx(k.log_likelihood(), rel=1e-13)
+
+
+@pytest.mark.parametrize("variance", ["f64", "ozaki"])
+def test_krig_checkpoint_of_jitchol_rescued_fit(tmp_path, variance, monkeypatch):
+    """A fit that needed GPy's jitchol jitter (repeated points, no noise), saved with its factor
+    and loaded: bit-identical predictions (the Ozaki planes take the moduli count of the jittered
+    diagonal); saved without the factor, the refit keeps the jitchol setting and succeeds."""
+    rng = np.random.default_rng(4)
+    x = rng.uniform(0, 20, (60, 2))
+    x = np.concatenate([x, x[:5]])
+    y = rng.normal(size=2 * x.shape[0])
+    xg = rng.uniform(0, 20, (300, 2))
+    k = krig.Krig("df", l_df=3.0, noise=0.0, variance=variance, jitchol=5).fit(x, y)
+    used = k.gp.extra["jitchol"]
+    assert used > 0
+    mu, var = k.predict(xg)
+    p, q = str(tmp_path / "model.npz"), str(tmp_path / "model_nofactor.npz")
+    k.save(p, with_factor=True)
+    k.save(q)
+    k3 = krig.Krig.load(q)   # refit from the inputs: needs jitchol again
+    assert k3.jitchol == 5 and k3.gp.extra["jitchol"] == used
+    mu3, var3 = k3.predict(xg)
+    assert np.array_equal(mu, mu3) and np.array_equal(var, var3, equal_nan=True)
+
+    def no_fit(*a, **kw):
+        raise AssertionError("Krig.load refitted a checkpoint that carries the factor")
+    monkeypatch.setattr(E, "fit", no_fit)
+    k2 = krig.Krig.load(p)
+    assert k2.gp.extra["jitchol"] == used
+    if variance == "ozaki":
+        assert k2.gp.extra["ozaki"][2] == k.gp.extra["ozaki"][2]
+    mu2, var2 = k2.predict(xg)
+    assert np.array_equal(mu, mu2) and np.array_equal(var, var2, equal_nan=True)
