@@ -1,0 +1,38 @@
+// dfact.hpp — device helpers of the distributed factor (one job's POTRF + TRTRI over several
+// GPUs; host side gp2d.hip gp2d_dfact_*, gp2d/distributed.py fit_distributed).
+//
+// 1-D block-cyclic by 256-column super-blocks: rank s mod P owns super-column s.  Every rank
+// holds the whole n×n K_y but reads and writes only its own super-columns, which end up holding
+// W = L⁻¹ (right-looking TRTRI fused into the right-looking POTRF: at step s every rank applies
+// the broadcast panel [D_s = L_ss⁻¹; L21] to its trailing K_y columns AND to its W columns
+// J ≤ s: X[s] = D_s·R[s], R[t>s] −= L[t,s]·X[s]).  The GEMMs run on gemm_f64_kernel with
+// block-cyclic column tiles (GemmParams::jgrp / jstep / cyc_lower).
+#pragma once
+#include "common.hpp"
+
+namespace gp2d {
+
+constexpr int DF_SB = 256;   // super-block width (two 128-wide GEMM tiles)
+
+// Column block s of A becomes the s-th block column of the identity (rows of the super-block:
+// I, every other row: 0): the TRTRI's initial right-hand side R[:, s] = E_s, written once the
+// owner has read its K_y panel.  One thread per element pair, two rows per workgroup.
+__global__ __launch_bounds__(256) void dfact_reset_col_kernel(double* __restrict__ A, int64_t n, int64_t lda,
+                                                              int64_t c0) {
+  const int64_t i = 2 * (int64_t)blockIdx.x + (threadIdx.x >> 7);
+  const int c = 2 * (int)(threadIdx.x & 127);
+  if (i >= n) return;
+  const int64_t r = i - c0;             // row within the super-block, if any
+  d2 v;
+  v.x = (r == c) ? 1.0 : 0.0;
+  v.y = (r == c + 1) ? 1.0 : 0.0;
+  *reinterpret_cast<d2*>(A + i * lda + c0 + c) = v;
+}
+
+// A failed diagonal block reports its local leading-minor order in *tmp; the first failure
+// of the whole factorisation is kept in *info as a global order.
+__global__ void dfact_info_kernel(int* __restrict__ info, const int* __restrict__ tmp, int64_t off) {
+  if (threadIdx.x == 0 && *tmp != 0 && *info == 0) *info = (int)(off + *tmp);
+}
+
+}  // namespace gp2d

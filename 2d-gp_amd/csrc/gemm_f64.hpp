@@ -47,7 +47,19 @@ struct GemmParams {
   int xcd_cols;  // 1-D grid: groups of 8 column tiles × all row blocks, column tile = XCD label
   int cols_first;  // 1-D grid, column blocks slow and ascending: heavy-first order for b_lower
   double* P; int64_t ldp; int64_t sP;         // EPI_COLSQ partials [M/BM][N]
+  // Block-cyclic column tiles (the distributed factor, dfact.hpp): with jgrp > 0, column tile
+  // bj sits jt = (bj / jgrp)·jgrp·jstep + bj % jgrp tiles from C's (and op(B)'s) first column
+  // tile — groups of jgrp consecutive tiles, one group every jstep groups (a rank's super-
+  // columns).  cyc_lower: only tiles with bi + mask_off ≥ jt run (the lower triangle in global
+  // tile coordinates, mask_off = C's first global row tile − its first global column tile);
+  // on bi + mask_off == jt the tile stores its lower triangle only.
+  int jgrp, jstep;
+  int cyc_lower, mask_off;
 };
+
+__host__ __device__ inline int cyc_tile(const GemmParams& p, int bj) {
+  return p.jgrp > 0 ? (bj / p.jgrp) * p.jgrp * p.jstep + bj % p.jgrp : bj;
+}
 
 __device__ __forceinline__ void tri_tile(int t, int& bi, int& bj) {
   int r = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
@@ -84,7 +96,9 @@ __global__ __launch_bounds__(256, 2) void gemm_f64_kernel(GemmParams p) {
     bi = p.rev_rows ? (int)(gridDim.y - 1 - blockIdx.y) : (int)blockIdx.y;
   }
   const int z = blockIdx.z;
-  const int i0 = bi * GBM, j0 = bj * GBN;
+  const int jt = cyc_tile(p, bj);
+  if (p.cyc_lower && bi + p.mask_off < jt) return;   // strictly above the global diagonal
+  const int i0 = bi * GBM, j0 = jt * GBN;
   const double* __restrict__ A = p.A + z * p.sA;
   const double* __restrict__ B = p.B + z * p.sB;
 
@@ -168,7 +182,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f64_kernel(GemmParams p) {
 
   if (EPI == EPI_STORE) {
     double* __restrict__ C = p.C + z * p.sC;
-    const bool diag_tile = p.c_lower && (bi == bj);
+    const bool diag_tile = (p.c_lower && bi == bj) || (p.cyc_lower && bi + p.mask_off == jt);
     const bool has_beta = p.beta != 0.0;
     // per 16-row group: all 16 C loads in flight together, then the updates and stores
     // (element-wise load → use → store chains leave one HBM round trip per element)
@@ -193,7 +207,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f64_kernel(GemmParams p) {
           const int col = j0 + wc * 64 + ni * 16 + lr;
           double v = p.alpha * acc[mi][ni][r];
           if (has_beta) v = fma(p.beta, old[ni][r], v);
-          if (!(diag_tile && col > row)) C[(int64_t)row * p.ldc + col] = v;
+          if (!(diag_tile && col - j0 > row - i0)) C[(int64_t)row * p.ldc + col] = v;
         }
     }
   } else {

@@ -10,6 +10,7 @@
 #include "predict.hpp"
 #include "ozaki.hpp"
 #include "lml.hpp"
+#include "dfact.hpp"
 #include "../../include/gp2d.h"
 
 #include <dlfcn.h>
@@ -519,6 +520,164 @@ int gp2d_trtri(double* A, int64_t n, int64_t lda, const double* dinv, void* work
   put_diag_blocks_kernel<<<dim3(NB * NB / 256, nb), 256, 0, s>>>(A, lda, dinv);
   GP2D_CHECK(check_launch("put_diag_blocks_kernel"));
   return trtri_levels(A, lda, nb, T, s);
+}
+
+// ------------------------------------------------------------------------ distributed factor
+// One job's POTRF + TRTRI over P ranks (dfact.hpp): 256-column super-blocks dealt block-
+// cyclically, a panel broadcast per step by the caller.  Every GEMM below is gemm_f64_kernel;
+// the per-element arithmetic does not depend on P (each tile sums the same K range in the same
+// order), so any P gives the bits of P = 1.
+size_t gp2d_dfact_panel_doubles(int64_t n) { return (size_t)(n > 0 ? n : 0) * DF_SB; }
+
+size_t gp2d_dfact_workspace(int64_t) {
+  // the two 128×128 inverse diagonal blocks of a super-block and one int
+  return (size_t)2 * NB * NB * sizeof(double) + 64;
+}
+
+static int dfact_args(const double* A, int64_t n, int64_t lda, int s) {
+  GP2D_REQUIRE(A != nullptr, "dfact: NULL matrix");
+  GP2D_REQUIRE(n > 0 && n % DF_SB == 0, "dfact: n must be a positive multiple of 256");
+  GP2D_REQUIRE(n <= INT32_MAX && lda >= n && lda % 2 == 0, "dfact: lda must be >= n and even");
+  GP2D_REQUIRE(s >= 0 && (int64_t)s * DF_SB < n, "dfact: super-block index out of range");
+  return 0;
+}
+
+// Owner's step: super-column s (rows s·256..n) factored on ONE stream — diagonal block 0,
+// its panel TRSM down to row n, the column update of sub-column 1 by sub-column 0, diagonal
+// block 1, its panel TRSM — then copied into the panel buffer with the head's diagonal blocks
+// replaced by their inverses: head = [[D0, ·], [L10, D1]] (D_i = L_ii⁻¹; the upper right block
+// is never read).  Receivers apply D_s = L_ss⁻¹ as D0, then L10, then D1 (gp2d_dfact_invstep).
+int gp2d_dfact_panel(double* A, int64_t n, int64_t lda, int s, double* panel, int* info_dev, void* work,
+                     size_t work_bytes, void* stream) {
+  GP2D_CHECK(dfact_args(A, n, lda, s));
+  GP2D_REQUIRE(panel != nullptr && info_dev != nullptr, "dfact_panel: NULL panel or info");
+  GP2D_REQUIRE(work != nullptr && work_bytes >= gp2d_dfact_workspace(n), "dfact_panel: workspace too small");
+  hipStream_t st = S(stream);
+  const int64_t s0 = (int64_t)s * DF_SB;
+  double* As = A + s0 * lda + s0;                  // the super-column from its diagonal down
+  const int64_t rows = n - s0;                     // ≥ 256
+  double* dinv = static_cast<double*>(work);       // [2][128][128]
+  int* tmp = reinterpret_cast<int*>(dinv + 2 * NB * NB);
+  GP2D_EV(hipMemsetAsync(tmp, 0, sizeof(int), st));
+  potrf_diag_kernel<<<1, 256, 0, st>>>(As, lda, 0, dinv, tmp, 0);
+  GP2D_CHECK(check_launch("potrf_diag_kernel"));
+  double* P0 = As + (int64_t)NB * lda;             // rows below diagonal block 0, sub-column 0
+  gemm_f64_panel_kernel<<<(unsigned)((rows - NB) / PNL_R), 256, 0, st>>>(P0, lda, dinv, NB, P0, lda, 1.0, 0.0);
+  GP2D_CHECK(check_launch("gemm_f64_panel_kernel"));
+  double* C1 = P0 + NB;                            // sub-column 1 from row s0 + 128 down
+  gemm_f64_panel_kernel<<<(unsigned)((rows - NB) / PNL_R), 256, 0, st>>>(P0, lda, P0, lda, C1, lda, -1.0, 1.0);
+  GP2D_CHECK(check_launch("gemm_f64_panel_kernel"));
+  potrf_diag_kernel<<<1, 256, 0, st>>>(As, lda, NB, dinv, tmp, 0);
+  GP2D_CHECK(check_launch("potrf_diag_kernel"));
+  if (rows > DF_SB) {
+    double* P1 = C1 + (int64_t)NB * lda;           // rows below diagonal block 1, sub-column 1
+    gemm_f64_panel_kernel<<<(unsigned)((rows - DF_SB) / PNL_R), 256, 0, st>>>(P1, lda, dinv + NB * NB, NB, P1, lda,
+                                                                             1.0, 0.0);
+    GP2D_CHECK(check_launch("gemm_f64_panel_kernel"));
+  }
+  dfact_info_kernel<<<1, 64, 0, st>>>(info_dev, tmp, s0);
+  GP2D_CHECK(check_launch("dfact_info_kernel"));
+  GP2D_EV(hipMemcpy2DAsync(panel, DF_SB * sizeof(double), As, lda * sizeof(double), DF_SB * sizeof(double), rows,
+                           hipMemcpyDeviceToDevice, st));
+  for (int b = 0; b < 2; ++b)
+    GP2D_EV(hipMemcpy2DAsync(panel + (int64_t)b * NB * DF_SB + b * NB, DF_SB * sizeof(double), dinv + b * NB * NB,
+                             NB * sizeof(double), NB * sizeof(double), NB, hipMemcpyDeviceToDevice, st));
+  return 0;
+}
+
+// first owned super-column ≥ t (rank r of P), and how many owned ones lie in [t, t_hi)
+static void dfact_owned(int t, int t_hi, int P, int r, int& first, int& count) {
+  first = t + ((r - t) % P + P) % P;
+  count = first < t_hi ? (t_hi - 1 - first) / P + 1 : 0;
+}
+
+int gp2d_dfact_update(double* A, int64_t n, int64_t lda, int s, const double* panel, int nranks, int rank,
+                      int t_lo, int t_hi, void* stream) {
+  GP2D_CHECK(dfact_args(A, n, lda, s));
+  GP2D_REQUIRE(panel != nullptr, "dfact_update: NULL panel");
+  GP2D_REQUIRE(nranks >= 1 && rank >= 0 && rank < nranks, "dfact_update: bad rank / world size");
+  const int nsb = (int)(n / DF_SB);
+  int first, count;
+  dfact_owned(std::max(t_lo, s + 1), std::min(t_hi, nsb), nranks, rank, first, count);
+  if (count == 0) return 0;
+  // A[rows ≥ t·256, t] −= L21[t rows..] · L21[t block]ᵀ for the owned t, lower tiles only
+  const int64_t r0 = (int64_t)(s + 1) * DF_SB;
+  const double* L21 = panel + (int64_t)DF_SB * DF_SB;   // global row r0 + i at panel row i
+  GemmParams q = gemm_params();
+  q.A = L21; q.lda = DF_SB;
+  q.B = L21 + ((int64_t)first * DF_SB - r0) * DF_SB; q.ldb = DF_SB;
+  q.C = A + r0 * lda + (int64_t)first * DF_SB; q.ldc = lda;
+  q.M = (int)(n - r0); q.N = count * DF_SB; q.K = DF_SB;
+  q.alpha = -1.0; q.beta = 1.0;
+  q.jgrp = DF_SB / GBN; q.jstep = nranks;
+  q.cyc_lower = 1; q.mask_off = 2 * (s + 1) - 2 * first;
+  return launch_gemm<true, EPI_STORE>(q, 1, S(stream));
+}
+
+int gp2d_dfact_invstep(double* A, int64_t n, int64_t lda, int s, const double* panel, int nranks, int rank,
+                       void* stream) {
+  GP2D_CHECK(dfact_args(A, n, lda, s));
+  GP2D_REQUIRE(panel != nullptr, "dfact_invstep: NULL panel");
+  GP2D_REQUIRE(nranks >= 1 && rank >= 0 && rank < nranks, "dfact_invstep: bad rank / world size");
+  hipStream_t st = S(stream);
+  const int64_t s0 = (int64_t)s * DF_SB;
+  if (s % nranks == rank) {   // this rank's W column block s starts as the identity block column
+    dfact_reset_col_kernel<<<(unsigned)((n + 1) / 2), 256, 0, st>>>(A, n, lda, s0);
+    GP2D_CHECK(check_launch("dfact_reset_col_kernel"));
+  }
+  int first, count;
+  dfact_owned(0, s + 1, nranks, rank, first, count);
+  if (count == 0) return 0;
+  double* Xs = A + s0 * lda + (int64_t)first * DF_SB;   // rows of super-block s, owned columns ≤ s
+  auto cyc = [&](GemmParams& q) { q.jgrp = DF_SB / GBN; q.jstep = nranks; };
+  // X[s] = D_s · R[s] with D_s = [[D0, 0], [−D1·L10·D0, D1]], as a block forward substitution:
+  // X_lo = D0·R_lo, R_hi −= L10·X_lo, X_hi = D1·R_hi.  The in-place products are one 128-row tile
+  // per column tile, which reads its whole K range before it stores.
+  auto prod = [&](const double* Aop, double* Bc, double alpha, double beta, double* Cc) -> int {
+    GemmParams q = gemm_params();
+    q.A = Aop; q.lda = DF_SB;
+    q.B = Bc; q.ldb = lda;
+    q.C = Cc; q.ldc = lda;
+    q.M = NB; q.N = count * DF_SB; q.K = NB;
+    q.alpha = alpha; q.beta = beta;
+    cyc(q);
+    return launch_gemm<false, EPI_STORE>(q, 1, st);
+  };
+  double* Xlo = Xs;
+  double* Xhi = Xs + (int64_t)NB * lda;
+  GP2D_CHECK(prod(panel, Xlo, 1.0, 0.0, Xlo));                                   // D0
+  GP2D_CHECK(prod(panel + (int64_t)NB * DF_SB, Xlo, -1.0, 1.0, Xhi));            // L10
+  GP2D_CHECK(prod(panel + (int64_t)NB * DF_SB + NB, Xhi, 1.0, 0.0, Xhi));       // D1
+  const int64_t rows = n - s0 - DF_SB;
+  if (rows > 0) {   // R[t > s] −= L21 · X[s]
+    GemmParams q = gemm_params();
+    q.A = panel + (int64_t)DF_SB * DF_SB; q.lda = DF_SB;
+    q.B = Xs; q.ldb = lda;
+    q.C = Xs + (int64_t)DF_SB * lda; q.ldc = lda;
+    q.M = (int)rows; q.N = count * DF_SB; q.K = DF_SB;
+    q.alpha = -1.0; q.beta = 1.0;
+    cyc(q);
+    GP2D_CHECK((launch_gemm<false, EPI_STORE>(q, 1, st)));
+  }
+  return 0;
+}
+
+int gp2d_copy2d(double* dst, int64_t ldd, const double* src, int64_t lds, int64_t rows, int64_t cols,
+                void* stream) {
+  GP2D_REQUIRE(rows >= 0 && cols >= 0, "copy2d: negative size");
+  if (rows == 0 || cols == 0) return 0;
+  GP2D_REQUIRE(dst && src && ldd >= cols && lds >= cols, "copy2d: NULL buffer or leading dimension < cols");
+  GP2D_EV(hipMemcpy2DAsync(dst, ldd * sizeof(double), src, lds * sizeof(double), cols * sizeof(double), rows,
+                           hipMemcpyDeviceToDevice, S(stream)));
+  return 0;
+}
+
+int gp2d_zero_upper(double* A, int64_t n, int64_t lda, void* stream) {
+  GP2D_REQUIRE(A != nullptr && n > 0 && n % NB == 0 && lda >= n && lda % 2 == 0,
+               "zero_upper: n must be a positive multiple of 128, lda >= n and even");
+  dim3 zg((unsigned)((n / 2 + 255) / 256), (unsigned)n);
+  zero_upper_kernel<<<zg, 256, 0, S(stream)>>>(A, n, lda);
+  return check_launch("zero_upper_kernel");
 }
 
 // ------------------------------------------------------------------------ POTRS

@@ -10,6 +10,8 @@ single-GPU result.
 from __future__ import annotations
 
 import collections
+import ctypes
+import time
 
 import numpy as np
 import torch
@@ -109,6 +111,174 @@ def fit_sharded(spec: E.KernelSpec, x, y, noise: float, device, mode: str = "bca
     if variance == "ozaki" and "ozaki" not in gp.extra:
         E.ozaki_prepare(gp, diag_add=float(noise + jitter))   # a-priori moduli count: no host sync
     return gp
+
+
+SB = 256   # super-block width of the distributed factor (csrc/dfact.hpp DF_SB)
+
+
+def _owned_blocks(nsb: int, ws: int, r: int):
+    return list(range(r, nsb, ws))
+
+
+def fit_distributed(spec: E.KernelSpec, x, y, noise: float, device=None, variance: str = "ozaki",
+                    jitter: float = 0.0, lookahead: bool = True, stats: dict | None = None,
+                    emulate: tuple | None = None) -> E.GPFit:
+    """ONE job's fit spread over all ranks (the config-D single job: /root/reference/krig.py:541-557
+    predicts one model's large grid): every rank assembles K_y, then a 1-D block-cyclic POTRF
+    fused with the right-looking TRTRI (include/gp2d.h gp2d_dfact_*) — rank s mod P factors
+    super-column s (256 wide), broadcasts the panel [L_ss⁻¹; L21] (torch.distributed: RCCL under
+    'nccl'), and every rank applies it to its own K_y columns (POTRF trailing update) and to its
+    own W = L⁻¹ columns (TRTRI step).  The owned W columns are then all-gathered (lower parts only,
+    ≈ n²/2 doubles in all), so every rank ends with the full W, α and the ozaki residue planes,
+    ready to predict its grid shard (predict_shard).
+
+    Per rank: 1/P of the POTRF's and the TRTRI's GEMM flops, one panel receive per step
+    (n²/2 doubles in all) and the all-gather.  The next owner updates its next super-column with
+    the panel first and factors it while the rest of the step's GEMMs run (look-ahead), so the
+    chain of diagonal factorisations is not serialised behind the trailing updates.
+
+    Every element's arithmetic is the same for any world size, so P ranks return the bits of one
+    (tests/test_gpu_distributed.py); a non-SPD K_y raises numpy.linalg.LinAlgError on every rank.
+    `stats` (optional dict) receives host-side timestamps of the phases.
+
+    emulate=(P, r) (measurement only, tools/probe_dfit.py; one process, no process group): run
+    rank r's share of a P-rank factorisation — its panels, updates and inverse steps, no
+    broadcast (the panels it did not factor hold stale data) and no all-gather; the returned
+    factor is NOT W."""
+    ws, rank = world()
+    if emulate is not None:
+        if ws != 1:
+            raise ValueError("emulate is for one process without a process group")
+        ws, rank = int(emulate[0]), int(emulate[1])
+    dev = E._require_device(device)
+    if variance not in E.VARIANCE_ENGINES:
+        raise ValueError(f"variance must be one of {E.VARIANCE_ENGINES}")
+    if variance == "ozaki" and not spec.is_vector:
+        raise ValueError("the ozaki variance engine supports the vector families only")
+    L = E.N.lib()
+    d, bd = spec.input_dim, spec.block_dim
+    X = E._as_points(x, d, dev)
+    ntr = X.shape[0]
+    if ntr < 1:
+        raise ValueError("need at least one training point")
+    npad, n = E.fit_layout(spec, ntr, "ozaki")   # n a multiple of 256 (the super-block)
+    if variance == "ozaki" and n >= 131072:
+        raise ValueError(f"the ozaki variance engine supports n < 131072; got n = {n}")
+    perm = None
+    if variance == "ozaki" and ntr > 1:
+        perm = E.morton_order(X)
+        X = X[perm].contiguous()
+    main = torch.cuda.current_stream(dev)
+    sh = E._stream_handle(dev)
+    P = E._ptr
+    desc = spec.desc()
+    A = torch.empty((n, n), dtype=torch.float64, device=dev)
+    E.N.check(L.gp2d_assemble(P(X), ntr, npad, P(X), ntr, npad, ctypes.byref(desc), float(noise + jitter), 1,
+                              P(A), n, sh), "gp2d_assemble")
+    nsb = n // SB
+    pdoubles = int(L.gp2d_dfact_panel_doubles(n))
+    panels = [torch.empty(pdoubles, dtype=torch.float64, device=dev) for _ in range(2)]
+    wbytes = int(L.gp2d_dfact_workspace(n))
+    work = torch.empty(wbytes // 8 + 1, dtype=torch.float64, device=dev)
+    info = torch.zeros(1, dtype=torch.int32, device=dev)
+    comm = torch.cuda.Stream(dev)
+    t0 = time.perf_counter()
+
+    factored = {}   # s → main-stream event after the owner's gp2d_dfact_panel(s)
+    done = {}       # s → main-stream event after step s's last read of its panel buffer
+
+    def factor(s):   # owner of s: panel s into its buffer, on the main stream
+        E.N.check(L.gp2d_dfact_panel(P(A), n, n, s, P(panels[s % 2]), P(info), P(work), wbytes, sh),
+                  "gp2d_dfact_panel")
+        ev = torch.cuda.Event()
+        ev.record(main)
+        factored[s] = ev
+
+    if rank == 0:
+        factor(0)
+    for s in range(nsb):
+        owner = s % ws
+        buf = panels[s % 2]
+        rows = n - s * SB
+        if ws > 1 and emulate is None:
+            # the buffer's previous user (step s − 2) is done; the owner's panel s is written —
+            # the broadcast does not wait for the rest of step s − 1 (it overlaps it)
+            if s >= 2:
+                comm.wait_event(done.pop(s - 2))
+            if owner == rank:
+                comm.wait_event(factored.pop(s))
+            with torch.cuda.stream(comm):
+                dist.broadcast(buf[:rows * SB], owner)
+            main.wait_stream(comm)
+        nxt = s + 1
+        rest_lo = nxt
+        if lookahead and nxt < nsb and nxt % ws == rank:
+            # look-ahead: bring super-column s+1 up to date and factor it before the rest of step s
+            E.N.check(L.gp2d_dfact_update(P(A), n, n, s, P(buf), ws, rank, nxt, nxt + 1, sh), "gp2d_dfact_update")
+            factor(nxt)
+            rest_lo = nxt + 1
+        E.N.check(L.gp2d_dfact_update(P(A), n, n, s, P(buf), ws, rank, rest_lo, nsb, sh), "gp2d_dfact_update")
+        if not lookahead and nxt < nsb and nxt % ws == rank:
+            factor(nxt)
+        E.N.check(L.gp2d_dfact_invstep(P(A), n, n, s, P(buf), ws, rank, sh), "gp2d_dfact_invstep")
+        ev = torch.cuda.Event()
+        ev.record(main)
+        done[s] = ev
+    del panels, work
+    t1 = time.perf_counter()
+    if ws > 1 and emulate is None:
+        _allgather_w_columns(A, n, ws, rank, dev)
+        dist.all_reduce(info, op=dist.ReduceOp.MAX)
+    E.N.check(L.gp2d_zero_upper(P(A), n, n, sh), "gp2d_zero_upper")
+    t2 = time.perf_counter()
+    Y = E._pad_obs(y, ntr, npad, bd, dev)
+    if perm is not None:
+        for c in range(bd):
+            Y[c * npad:c * npad + ntr] = Y[c * npad:c * npad + ntr][perm]
+    alpha = torch.empty(n, dtype=torch.float64, device=dev)
+    pbytes = int(L.gp2d_potrs_workspace(n))
+    pwork = torch.empty(pbytes // 8 + 1, dtype=torch.float64, device=dev)
+    E.N.check(L.gp2d_potrs_inv(P(A), n, n, P(Y), P(alpha), P(pwork), pbytes, sh), "gp2d_potrs_inv")
+    del pwork
+    gp = E.GPFit(kernel=spec, noise=float(noise), x=X, n_train=ntr, n_pad=npad, W=A, alpha=alpha, device=dev,
+                 y=Y, perm=perm)
+    if emulate is not None:
+        return gp
+    E._raise_fit_errors(int(info.item()), None)
+    if variance == "ozaki":
+        E.ozaki_prepare(gp, diag_add=float(noise + jitter))
+    if stats is not None:
+        stats.update(host_factor_s=t1 - t0, host_gather_s=t2 - t1)
+    return gp
+
+
+def _allgather_w_columns(A: torch.Tensor, n: int, ws: int, rank: int, dev):
+    """Every rank's W super-columns to every rank: super-column t travels as its rows
+    [256·t, n) (the part below the diagonal block's top; W is zero above it)."""
+    L = E.N.lib()
+    P, sh = E._ptr, E._stream_handle(dev)
+    nsb = n // SB
+    sizes = [sum((n - t * SB) * SB for t in _owned_blocks(nsb, ws, r)) for r in range(ws)]
+    cap = max(sizes)
+    send = torch.empty(cap, dtype=torch.float64, device=dev)
+    off = 0
+    for t in _owned_blocks(nsb, ws, rank):
+        rows = n - t * SB
+        E.N.check(L.gp2d_copy2d(P(send[off:]), SB, P(A[t * SB:, t * SB:]), n, rows, SB, sh), "gp2d_copy2d")
+        off += rows * SB
+    recv = torch.empty(ws * cap, dtype=torch.float64, device=dev)
+    if dist.get_backend() == "nccl":
+        dist.all_gather_into_tensor(recv, send)
+    else:   # gloo (the CPU / shared-card rehearsals)
+        dist.all_gather(list(recv.view(ws, cap).unbind(0)), send)
+    for r in range(ws):
+        if r == rank:
+            continue
+        off = r * cap
+        for t in _owned_blocks(nsb, ws, r):
+            rows = n - t * SB
+            E.N.check(L.gp2d_copy2d(P(A[t * SB:, t * SB:]), n, P(recv[off:]), SB, rows, SB, sh), "gp2d_copy2d")
+            off += rows * SB
 
 
 def krige_jobs_sharded(jobs, variance: str = "ozaki", chunk: int = 8192, var_mode: str = "latent",

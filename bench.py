@@ -84,6 +84,8 @@ def parse():
                     help="time the numpy oracle on the host cores (N=1 only); -1 = only when N_train <= 4096")
     ap.add_argument("--cpu-sample-points", type=int, default=2048)
     ap.add_argument("--pmc-json", default=None)
+    ap.add_argument("--single-job-dist", type=int, default=0,
+                    help="also time one job with distributed.fit_distributed at N = 1 (always at N > 1)")
     a = ap.parse_args()
     if a.config == "B":
         a.kind, a.ntrain, a.grid = "df", 1024, 128
@@ -201,6 +203,43 @@ def run_sweep(args, ws, rank, dev):
     if ws > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def single_job_distributed(args, ws, spec, xt, yt, noise, xg, m_all, dev, pred_cache, mean, var, reps):
+    """One job with its FIT spread over the ranks too (distributed.fit_distributed: block-cyclic
+    POTRF + TRTRI, panel broadcasts, W all-gathered), then each rank's grid shard predicted —
+    the one-job multi-GPU reading of DESIGN.md §5 (config D).  One untimed warm job first."""
+    from gp2d import distributed as GD
+    from gp2d import engine as E
+
+    def job():
+        gp = GD.fit_distributed(spec, xt, yt, noise, dev, variance=args.variance)
+        pr = pred_cache.get("pd")
+        if pr is None or not pr.fits(gp):
+            pr = E.Predictor(gp, args.chunk)
+            pred_cache["pd"] = pr
+        pr.gp = gp
+        pr(xg, out=(mean, var))
+        return gp
+
+    job()
+    barrier(ws)
+    tf = time.perf_counter()
+    gp = GD.fit_distributed(spec, xt, yt, noise, dev, variance=args.variance)
+    barrier(ws)
+    fit_s = time.perf_counter() - tf
+    del gp
+    ts = time.perf_counter()
+    for _ in range(reps):
+        job()
+    barrier(ws)
+    dts = torch.tensor([time.perf_counter() - ts, fit_s], dtype=torch.float64, device=dev)
+    if ws > 1:
+        dist.all_reduce(dts, op=dist.ReduceOp.MAX)
+    ms = 1e3 * float(dts[0].item()) / reps
+    return {"ms": ms, "value": m_all / (ms * 1e-3), "reps": reps, "fit_ms": 1e3 * float(dts[1].item()),
+            "fit": f"distributed.fit_distributed over {ws} rank(s): 256-column block-cyclic POTRF + TRTRI, "
+                   "panel broadcasts, W columns all-gathered"}
 
 
 def main():
@@ -400,6 +439,9 @@ def main():
     single_ms = 1e3 * float(dts.item()) / reps
     single_job = {"ms": single_ms, "value": m_all / (single_ms * 1e-3), "reps": reps,
                   "fit": "rank 0, factor broadcast" if ws > 1 else "local"}
+    if ws > 1 or args.single_job_dist:
+        single_job["distributed_fit"] = single_job_distributed(args, ws, spec, xt, yt, noise, xg, m_all, dev,
+                                                               pred_cache, mean, var, reps)
 
     # mean-only throughput (secondary, same fit; at most 20 jobs)
     mo_steps = min(args.steps, 20)

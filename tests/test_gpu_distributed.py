@@ -244,3 +244,97 @@ def test_round_robin_timed_window_holds_every_fit(tmp_path):
     assert [int(x["inside"]) for x in r] == [3, 2]
     assert [int(x["issued"]) for x in r] == [3, 2]
     assert all(int(x["n_out"]) == 5 for x in r)
+
+
+# ------------------------------------------------------------------ one job's factor over ranks
+def _dfit_problem(n):
+    rng = np.random.default_rng(4242 + n)
+    x = np.stack([rng.uniform(0, 60, n), rng.uniform(0, 45, n)], 1)
+    y = np.concatenate([np.sin(x[:, 1] / 7), np.cos(x[:, 0] / 9)]) + rng.normal(0, 0.05, 2 * n)
+    GX, GY = np.meshgrid(np.linspace(-5, 65, 40), np.linspace(-5, 50, 43))
+    return x, y, np.stack([GX.reshape(-1), GY.reshape(-1)], 1)
+
+
+def _dfit_worker(rank, world, port, out_dir, n, kind, noise):
+    for p in (ROOT, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from gp2d import distributed as GD
+    from gp2d import engine as E
+    x, y, xg = _dfit_problem(n)
+    dev = torch.device("cuda", 0)
+    spec = E.KernelSpec(kind=kind, l_df=5.0, l_cf=4.0, ratio=0.5 if kind == "mixed" else 1.0)
+    out = {}
+    try:
+        gp = GD.fit_distributed(spec, torch.tensor(x, device=dev), torch.tensor(y, device=dev), noise, dev)
+        lo, hi, mean, var = GD.predict_shard(E.Predictor(gp, 1024), torch.tensor(xg, device=dev))
+        fm, fv = GD.gather_shards(xg.shape[0], 2, lo, hi, mean, var, dev)
+        out = dict(W=gp.W.cpu().numpy(), alpha=gp.alpha.cpu().numpy(), mean=fm.cpu().numpy(),
+                   var=fv.cpu().numpy(), nmod=int(gp.extra["ozaki"][2]), raised=0)
+    except np.linalg.LinAlgError:
+        out = dict(raised=1)
+    torch.cuda.synchronize()
+    np.savez(os.path.join(out_dir, f"dfit{rank}.npz"), **out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n,kind", [(1024, "df"), (700, "mixed")])
+def test_distributed_fit_two_ranks_bit_identical(tmp_path, n, kind):
+    """fit_distributed over two ranks (block-cyclic POTRF + TRTRI, a panel broadcast per
+    256-column super-block, W columns all-gathered): both ranks hold the bits of the one-rank
+    run of the same algorithm (W, α, and the sharded posterior), and agree with engine.fit's
+    factor and posterior to 1e-12 / 1e-10 (relative, normwise)."""
+    from gp2d import distributed as GD
+    from gp2d import engine as E
+    world = 2
+    _spawn(_dfit_worker, world, str(tmp_path), n, kind, 0.0025)
+    r = [np.load(os.path.join(tmp_path, f"dfit{i}.npz")) for i in range(world)]
+    x, y, xg = _dfit_problem(n)
+    spec = E.KernelSpec(kind=kind, l_df=5.0, l_cf=4.0, ratio=0.5 if kind == "mixed" else 1.0)
+    gp1 = GD.fit_distributed(spec, x, y, 0.0025)                  # world 1: no process group here
+    mu1, var1 = (t.cpu().numpy() for t in E.Predictor(gp1, 1024)(xg))
+    W1 = gp1.W.cpu().numpy()
+    assert W1.shape[0] // 256 >= 6                                 # both ranks own super-columns
+    for i in range(world):
+        assert int(r[i]["raised"]) == 0
+        assert np.array_equal(r[i]["W"], W1), i
+        assert np.array_equal(r[i]["alpha"], gp1.alpha.cpu().numpy()), i
+        assert np.array_equal(r[i]["mean"], mu1) and np.array_equal(r[i]["var"], var1), i
+    assert np.array_equal(np.triu(W1, 1), np.zeros_like(W1))       # W = L⁻¹ is lower-triangular
+    gp = E.fit(spec, x, y, 0.0025, variance="ozaki")
+    Wr = gp.W.cpu().numpy()
+    k = Wr.shape[0]   # engine.fit pads to the same 256 multiple for the ozaki engine
+    assert k == W1.shape[0]
+    assert np.linalg.norm(W1 - Wr) / np.linalg.norm(Wr) < 1e-12
+    mu, var = (t.cpu().numpy() for t in E.Predictor(gp, 1024)(xg))
+    assert np.linalg.norm(mu1 - mu) / np.linalg.norm(mu) < 1e-10
+    assert np.linalg.norm(var1 - var) / np.linalg.norm(var) < 1e-10
+
+
+def test_distributed_fit_non_spd_raises_on_every_rank(tmp_path):
+    world = 2
+    _spawn(_dfit_worker, world, str(tmp_path), 700, "df", -100.0)
+    for i in range(world):
+        assert int(np.load(os.path.join(tmp_path, f"dfit{i}.npz"))["raised"]) == 1, i
+
+
+def test_distributed_fit_one_rank_lookahead_and_f64():
+    """One process: the look-ahead order changes no bits; the FP64 engine's posterior from the
+    distributed factor matches engine.fit's (1e-10)."""
+    from gp2d import distributed as GD
+    from gp2d import engine as E
+    x, y, xg = _dfit_problem(900)
+    spec = E.KernelSpec(kind="df", l_df=5.0)
+    a = GD.fit_distributed(spec, x, y, 0.0025, variance="f64")
+    b = GD.fit_distributed(spec, x, y, 0.0025, variance="f64", lookahead=False)
+    assert torch.equal(a.W, b.W) and torch.equal(a.alpha, b.alpha)
+    mu1, var1 = (t.cpu().numpy() for t in E.Predictor(a, 1024)(xg))
+    gp = E.fit(spec, x, y, 0.0025, variance="f64")
+    mu, var = (t.cpu().numpy() for t in E.Predictor(gp, 1024)(xg))
+    assert np.linalg.norm(mu1 - mu) / np.linalg.norm(mu) < 1e-10
+    assert np.linalg.norm(var1 - var) / np.linalg.norm(var) < 1e-10
