@@ -23,6 +23,9 @@ using namespace gp2d;
 #ifndef IGEMM_EXTRA
 #define IGEMM_EXTRA
 #endif
+#ifndef IGEMM_THREADS
+#define IGEMM_THREADS (2 * IG_TBN)
+#endif
 #ifndef IGEMM_INV   // the dev copies still take 1/m (the product kernel reduces without it)
 #define IGEMM_INV
 #endif
@@ -52,7 +55,7 @@ int main() {
 #else
   const dim3 gl = g;
 #endif
-  auto launch = [&]() { IGEMM_KERNEL<<<gl, 2 * IG_TBN>>>(dA, dB, dC, n, n, nc, kx, low, mod IGEMM_INV, 1 << 30, 0 IGEMM_EXTRA); };
+  auto launch = [&]() { IGEMM_KERNEL<<<gl, IGEMM_THREADS>>>(dA, dB, dC, n, n, nc, kx, low, mod IGEMM_INV, 1 << 30, 0 IGEMM_EXTRA); };
   for (int w = 0; w < 3; ++w) launch();
   (void)hipDeviceSynchronize();
   (void)hipEventRecord(e0);
