@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import collections
 import ctypes
+import os
 import time
 
 import numpy as np
@@ -19,6 +20,15 @@ import torch.distributed as dist
 
 from . import data as D
 from . import engine as E
+
+
+# GP2D_FORCE_COLLECTIVES=1 (tests only): run the multi-rank code paths (broadcasts, all-gathers,
+# round-robin fits) even at world size 1 — the real RCCL calls on a one-GPU box
+FORCE_COLLECTIVES = os.environ.get("GP2D_FORCE_COLLECTIVES") == "1"
+
+
+def _solo(ws: int) -> bool:
+    return ws == 1 and not (FORCE_COLLECTIVES and dist.is_available() and dist.is_initialized())
 
 
 def world():
@@ -35,7 +45,7 @@ def broadcast_fit(gp: E.GPFit | None, spec: E.KernelSpec, noise: float, x, devic
     the metadata broadcast carries it and EVERY rank raises (numpy.linalg.LinAlgError for a
     failed factor) instead of waiting for a factor that never comes."""
     ws, rank = world()
-    if ws == 1:
+    if _solo(ws):
         if error is not None:
             raise error
         return gp
@@ -99,7 +109,7 @@ def fit_sharded(spec: E.KernelSpec, x, y, noise: float, device, mode: str = "bca
     INT8 residue planes from the broadcast factor locally (no extra traffic).  check=False as
     in engine.fit (replicate mode; in bcast mode rank 0 checks before broadcasting)."""
     ws, rank = world()
-    if ws == 1 or mode == "replicate":
+    if _solo(ws) or mode == "replicate":
         return E.fit(spec, x, y, noise, jitter=jitter, device=device, variance=variance, check=check)
     gp, err = None, None
     if rank == 0:
@@ -200,7 +210,7 @@ def fit_distributed(spec: E.KernelSpec, x, y, noise: float, device=None, varianc
         owner = s % ws
         buf = panels[s % 2]
         rows = n - s * SB
-        if ws > 1 and emulate is None:
+        if not _solo(ws) and emulate is None:
             # the buffer's previous user (step s − 2) is done; the owner's panel s is written —
             # the broadcast does not wait for the rest of step s − 1 (it overlaps it)
             if s >= 2:
@@ -226,7 +236,7 @@ def fit_distributed(spec: E.KernelSpec, x, y, noise: float, device=None, varianc
         done[s] = ev
     del panels, work
     t1 = time.perf_counter()
-    if ws > 1 and emulate is None:
+    if not _solo(ws) and emulate is None:
         _allgather_w_columns(A, n, ws, rank, dev)
         dist.all_reduce(info, op=dist.ReduceOp.MAX)
     E.N.check(L.gp2d_zero_upper(P(A), n, n, sh), "gp2d_zero_upper")
@@ -300,7 +310,7 @@ def krige_jobs_sharded(jobs, variance: str = "ozaki", chunk: int = 8192, var_mod
     host time stamps, engine.note_fit_issued)."""
     ws, rank = world()
     dev = E._require_device(device)
-    if ws == 1:   # one rank: the single-GPU pipelined form (the next fit under this predict)
+    if _solo(ws):   # one rank: the single-GPU pipelined form (the next fit under this predict)
         seen = collections.deque()
 
         def feed():
@@ -406,7 +416,7 @@ def gather_shards(m: int, bd: int, lo: int, hi: int, mean, var, device, align: i
     """All-gather the shards and reassemble the full [u(M)..., v(M)...] vectors in rank order.
     `align` must be the one predict_shard used (checked against this rank's (lo, hi))."""
     ws, rank = world()
-    if ws == 1:
+    if _solo(ws):
         return mean, var
     ranges = [D.shard_range(m, ws, r, align) for r in range(ws)]
     if ranges[rank] != (lo, hi):

@@ -32,6 +32,16 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
+# GP2D_FORCE_COLLECTIVES=1 (tests only): take the multi-rank code paths — collectives,
+# round-robin fits, the distributed single job — even at world size 1, so a one-GPU box can run
+# them under the real RCCL backend (torchrun --nproc-per-node 1)
+FORCE_COLLECTIVES = os.environ.get("GP2D_FORCE_COLLECTIVES") == "1"
+
+
+def is_multi(ws: int) -> bool:
+    return ws > 1 or FORCE_COLLECTIVES
+
+
 METRIC = "posterior grid points/sec (fit+predict), N_train=4096, div-free 2D kernel"
 FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 matrix (= vector) dense peak; measured 76.5 (tools/microbench)
 HBM_PEAK_GBS = 8000.0
@@ -96,16 +106,16 @@ def parse():
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     if a.steps is None:   # config D: every rank owns at least two of the timed jobs' fits
         a.steps = {"D": max(4, 2 * ws), "E": 2}.get(a.config, 100)
-    if a.grid_global == 0 and ws > 1 and a.scaling in ("auto", "strong"):
+    if a.grid_global == 0 and is_multi(ws) and a.scaling in ("auto", "strong"):
         a.grid_global = a.grid   # N>1 default: one job grid sharded over the ranks
     if a.fit_mode is None:
-        a.fit_mode = "rr" if (ws > 1 and a.grid_global > 0) else "replicate"
+        a.fit_mode = "rr" if (is_multi(ws) and a.grid_global > 0) else "replicate"
     return a
 
 
 def setup_dist(args):
     ws = int(os.environ.get("WORLD_SIZE", "1"))
-    if ws > 1:
+    if is_multi(ws):
         # one process per GPU; GP2D_DIST_BACKEND=gloo (and ranks sharing a device) only for
         # rehearsing the multi-rank path on a one-GPU box
         local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
@@ -118,7 +128,7 @@ def setup_dist(args):
 
 
 def barrier(ws):
-    if ws > 1:
+    if is_multi(ws):
         dist.barrier()
     torch.cuda.synchronize()
 
@@ -177,7 +187,7 @@ def run_sweep(args, ws, rank, dev):
         vals, grads = sweep()
     barrier(ws)
     dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-    if ws > 1:
+    if is_multi(ws):
         dist.all_reduce(dt, op=dist.ReduceOp.MAX)
     elapsed = float(dt.item())
     if rank == 0:
@@ -200,7 +210,7 @@ def run_sweep(args, ws, rank, dev):
             "finite_settings": int(np.isfinite(vals).sum()),
         }
         print(json.dumps(out), flush=True)
-    if ws > 1:
+    if is_multi(ws):
         dist.barrier()
         dist.destroy_process_group()
 
@@ -234,7 +244,7 @@ def single_job_distributed(args, ws, spec, xt, yt, noise, xg, m_all, dev, pred_c
         job()
     barrier(ws)
     dts = torch.tensor([time.perf_counter() - ts, fit_s], dtype=torch.float64, device=dev)
-    if ws > 1:
+    if is_multi(ws):
         dist.all_reduce(dts, op=dist.ReduceOp.MAX)
     ms = 1e3 * float(dts[0].item()) / reps
     return {"ms": ms, "value": m_all / (ms * 1e-3), "reps": reps, "fit_ms": 1e3 * float(dts[1].item()),
@@ -275,15 +285,15 @@ def main():
     var = torch.empty(2 * m, dtype=torch.float64, device=dev)
     pred_cache = {}
     side = torch.cuda.Stream(dev) if args.variance == "ozaki" else None
-    cfg = {"mode": args.fit_mode if ws > 1 else "local", "ahead": False,
-           "pipeline": bool(args.pipeline) and ws == 1 or (bool(args.pipeline) and args.fit_mode == "replicate")
-           or (ws > 1 and args.fit_mode == "rr"),
+    cfg = {"mode": args.fit_mode if is_multi(ws) else "local", "ahead": False,
+           "pipeline": bool(args.pipeline) and not is_multi(ws) or (bool(args.pipeline) and args.fit_mode == "replicate")
+           or (is_multi(ws) and args.fit_mode == "rr"),
            "first": True}
 
     def set_mode(mode):
         cfg["mode"] = mode
         a = args.kstar_ahead
-        cfg["ahead"] = args.variance == "ozaki" and (a == 1 or (a == -1 and ws > 1 and mode == "bcast"))
+        cfg["ahead"] = args.variance == "ozaki" and (a == 1 or (a == -1 and is_multi(ws) and mode == "bcast"))
 
     stats = {}      # fits issued (engine.note_fit_issued): every timed job's fit must be issued after t0
     last = [None]   # the previous step's fit: its non-SPD check runs one step late (no host sync)
@@ -327,7 +337,7 @@ def main():
         return gp
 
     probe = {}
-    if ws > 1 and args.fit_mode == "auto":
+    if is_multi(ws) and args.fit_mode == "auto":
         # measure one step in each mode (after a warm step of each), max over ranks, keep the faster
         for mode in ("bcast", "replicate"):
             set_mode(mode)
@@ -343,7 +353,7 @@ def main():
     else:
         set_mode(cfg["mode"])
     unpiped = None
-    if cfg["pipeline"] and ws == 1 and args.unpipelined_steps > 0:
+    if cfg["pipeline"] and not is_multi(ws) and args.unpipelined_steps > 0:
         # reference: the same jobs strictly one after another, measured BEFORE the timed region
         # (the dominant kernel's launch time without a concurrent fit = its roofline alone)
         cfg["pipeline"] = False
@@ -413,13 +423,13 @@ def main():
     fit_times = stats.get("fit_issue_times", [])
     fits = torch.tensor([sum(t0 <= t <= t1 for t in fit_times), len(fit_times)], dtype=torch.float64, device=dev)
     dt = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-    if ws > 1:
+    if is_multi(ws):
         dist.all_reduce(dt, op=dist.ReduceOp.MAX)
         dist.all_reduce(fits, op=dist.ReduceOp.SUM)
     elapsed = float(dt.item())
     ms_per_step = 1e3 * elapsed / args.steps
     value = m_all * args.steps / elapsed
-    fits_expected = args.steps * (1 if cfg["mode"] in ("rr", "bcast") or ws == 1 else ws)
+    fits_expected = args.steps * (1 if cfg["mode"] in ("rr", "bcast") or not is_multi(ws) else ws)
     timed_fits = {"issued_in_window": int(fits[0].item()), "issued_total": int(fits[1].item()),
                   "expected": fits_expected, "warmup_jobs_run": warm}
     if timed_fits["issued_in_window"] != fits_expected or timed_fits["issued_total"] != fits_expected:
@@ -434,12 +444,12 @@ def main():
         run_jobs(1) if stream is not None else (step(), check_last())
     barrier(ws)
     dts = torch.tensor([time.perf_counter() - ts], dtype=torch.float64, device=dev)
-    if ws > 1:
+    if is_multi(ws):
         dist.all_reduce(dts, op=dist.ReduceOp.MAX)
     single_ms = 1e3 * float(dts.item()) / reps
     single_job = {"ms": single_ms, "value": m_all / (single_ms * 1e-3), "reps": reps,
-                  "fit": "rank 0, factor broadcast" if ws > 1 else "local"}
-    if ws > 1 or args.single_job_dist:
+                  "fit": "rank 0, factor broadcast" if is_multi(ws) else "local"}
+    if is_multi(ws) or args.single_job_dist:
         single_job["distributed_fit"] = single_job_distributed(args, ws, spec, xt, yt, noise, xg, m_all, dev,
                                                                pred_cache, mean, var, reps)
 
@@ -459,7 +469,7 @@ def main():
     mean_only = m_all * mo_steps / (t3 - t2)
 
     if rank != 0:
-        if ws > 1:
+        if is_multi(ws):
             dist.barrier()
             dist.destroy_process_group()
         return
@@ -523,7 +533,7 @@ def main():
                    "parallelism": (f"grid-sharded x{ws}, job j fitted on rank j mod {ws}, factor broadcast "
                                    "(RCCL, packed W)" if cfg["mode"] == "rr" else
                                    f"grid-sharded x{ws}, factor {cfg['mode']}" +
-                                   (" (RCCL broadcast of packed W)" if ws > 1 and cfg["mode"] == "bcast" else "")),
+                                   (" (RCCL broadcast of packed W)" if is_multi(ws) and cfg["mode"] == "bcast" else "")),
                    "fit_mode_probe_ms_per_step": probe or None, "kstar_ahead": cfg["ahead"]},
         "roofline": roof,
         "pipelined": cfg["pipeline"],
@@ -533,10 +543,10 @@ def main():
         "timed_fits": timed_fits,
         "mean_only_value": mean_only,
     }
-    if ws == 1 and (args.cpu_baseline > 0 or (args.cpu_baseline < 0 and args.ntrain <= 4096)):
+    if not is_multi(ws) and (args.cpu_baseline > 0 or (args.cpu_baseline < 0 and args.ntrain <= 4096)):
         out["cpu_baseline"] = cpu_baseline(x, y, xg_all, args.kind, 5.0, noise, args.cpu_sample_points)
     print(json.dumps(out), flush=True)
-    if ws > 1:
+    if is_multi(ws):
         dist.barrier()
         dist.destroy_process_group()
 

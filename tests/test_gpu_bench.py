@@ -64,3 +64,30 @@ def test_bench_two_ranks_default_contract():
     # job j is fitted by rank j mod 2 only: the 4 timed jobs' 4 fits, all issued after t0
     assert d["timed_fits"]["issued_in_window"] == d["timed_fits"]["issued_total"] == 4
     assert d["timed_fits"]["warmup_jobs_run"] >= 2
+    sj = d["single_job"]
+    assert sj["ms"] > 0 and sj["distributed_fit"]["ms"] > 0 and sj["distributed_fit"]["fit_ms"] > 0
+
+
+def test_bench_multi_rank_paths_under_rccl():
+    """The N > 1 code paths (round-robin fits with packed-W broadcasts, the distributed single
+    job with its panel broadcasts, all_gather_into_tensor and all_reduce) under the REAL RCCL
+    backend: one rank (GP2D_FORCE_COLLECTIVES=1 takes the multi-rank paths at world size 1;
+    RCCL refuses two ranks on one device, so N = 2..8 are the driver's runs)."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, GP2D_FORCE_COLLECTIVES="1")
+    env.pop("GP2D_DIST_BACKEND", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "1",
+           "--ntrain", "700", "--grid", "64", "--steps", "3", "--warmup", "1", "--chunk", "1024"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=200, cwd=ROOT, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["api"] == "distributed.krige_jobs_sharded" and d["scaling"] == "strong"
+    assert d["timed_fits"]["issued_in_window"] == d["timed_fits"]["issued_total"] == 3
+    assert d["single_job"]["distributed_fit"]["ms"] > 0
