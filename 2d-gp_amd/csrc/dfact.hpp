@@ -35,4 +35,22 @@ __global__ void dfact_info_kernel(int* __restrict__ info, const int* __restrict_
   if (threadIdx.x == 0 && *tmp != 0 && *info == 0) *info = (int)(off + *tmp);
 }
 
+// Row-block packing of a lower-triangular n×n matrix (n a multiple of 128): row block rb keeps
+// columns [0, 128·(rb+1)), stored row-major one block after the other — ≈ n²/2 doubles, the
+// factor broadcast's payload (gp2d_pack_lower).  One workgroup per (512-column chunk, row block).
+template <bool UNPACK>
+__global__ __launch_bounds__(256) void pack_lower_kernel(double* __restrict__ W, int64_t n, int64_t ldw,
+                                                         double* __restrict__ P) {
+  const int64_t rb = blockIdx.y, r0 = rb * 128, c1 = r0 + 128;
+  const int64_t c = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 2;
+  if (c >= c1) return;
+  const int64_t off = 128 * 128 * (rb * (rb + 1) / 2);
+#pragma unroll 4
+  for (int r = 0; r < 128; ++r) {
+    d2* w = reinterpret_cast<d2*>(W + (r0 + r) * ldw + c);
+    d2* p = reinterpret_cast<d2*>(P + off + r * c1 + c);
+    if (UNPACK) *w = *p; else *p = *w;
+  }
+}
+
 }  // namespace gp2d

@@ -672,6 +672,21 @@ int gp2d_copy2d(double* dst, int64_t ldd, const double* src, int64_t lds, int64_
   return 0;
 }
 
+size_t gp2d_pack_lower_doubles(int64_t n) {
+  const int64_t nb = n > 0 ? n / NB : 0;
+  return (size_t)(NB * NB) * (size_t)(nb * (nb + 1) / 2);
+}
+
+int gp2d_pack_lower(double* W, int64_t n, int64_t ldw, double* packed, int unpack, void* stream) {
+  GP2D_REQUIRE(W && packed, "pack_lower: NULL buffer");
+  GP2D_REQUIRE(n > 0 && n % NB == 0 && ldw >= n && ldw % 2 == 0,
+               "pack_lower: n must be a positive multiple of 128, ldw >= n and even");
+  const dim3 g((unsigned)((n + 511) / 512), (unsigned)(n / NB));
+  if (unpack) pack_lower_kernel<true><<<g, 256, 0, S(stream)>>>(W, n, ldw, packed);
+  else pack_lower_kernel<false><<<g, 256, 0, S(stream)>>>(W, n, ldw, packed);
+  return check_launch("pack_lower_kernel");
+}
+
 int gp2d_zero_upper(double* A, int64_t n, int64_t lda, void* stream) {
   GP2D_REQUIRE(A != nullptr && n > 0 && n % NB == 0 && lda >= n && lda % 2 == 0,
                "zero_upper: n must be a positive multiple of 128, lda >= n and even");

@@ -32,7 +32,7 @@ EXPORTS = (
     "gp2d_kernel_grad_count", "gp2d_kernel_grad_workspace", "gp2d_kernel_grad",
     "gp2d_gemm", "gp2d_transpose", "gp2d_bcast",
     "gp2d_dfact_panel_doubles", "gp2d_dfact_workspace", "gp2d_dfact_panel", "gp2d_dfact_update",
-    "gp2d_dfact_invstep", "gp2d_copy2d", "gp2d_zero_upper",
+    "gp2d_dfact_invstep", "gp2d_copy2d", "gp2d_zero_upper", "gp2d_pack_lower_doubles", "gp2d_pack_lower",
     "gp2d_timing_enable", "gp2d_timing_read", "gp2d_last_error",
 )
 
@@ -117,6 +117,8 @@ _SIGS = {
     "gp2d_dfact_invstep": (_I, [_P, _I64, _I64, _I, _P, _I, _I, _P]),
     "gp2d_copy2d": (_I, [_P, _I64, _P, _I64, _I64, _I64, _P]),
     "gp2d_zero_upper": (_I, [_P, _I64, _I64, _P]),
+    "gp2d_pack_lower_doubles": (_SZ, [_I64]),
+    "gp2d_pack_lower": (_I, [_P, _I64, _I64, _P, _I, _P]),
     "gp2d_timing_enable": (None, [_I]),
     "gp2d_timing_read": (_I, [ctypes.POINTER(_D), ctypes.POINTER(_I64), ctypes.POINTER(_D)]),
     "gp2d_last_error": (ctypes.c_char_p, []),

@@ -38,52 +38,94 @@ def world():
 
 
 def broadcast_fit(gp: E.GPFit | None, spec: E.KernelSpec, noise: float, x, device, src: int = 0,
-                  error: Exception | None = None) -> E.GPFit:
+                  error: Exception | None = None, layout: tuple | None = None) -> E.GPFit:
     """Broadcast W, α and the training points from `src` to every rank (RCCL
     ncclBroadcast under the 'nccl' backend).  Ranks other than `src` pass gp=None.
-    If the fit failed on `src` (`error`, e.g. a non-positive-definite K_y) the status word of
-    the metadata broadcast carries it and EVERY rank raises (numpy.linalg.LinAlgError for a
-    failed factor) instead of waiting for a factor that never comes."""
+
+    layout=None: a metadata broadcast first carries the sizes and a status word, read on the
+    host (one round trip); if the fit failed on `src` (`error`, e.g. a non-positive-definite K_y)
+    EVERY rank raises here (numpy.linalg.LinAlgError for a failed factor) instead of waiting for a
+    factor that never comes.
+
+    layout=(n, n_train, n_pad) (the job stream, where every rank knows the job's sizes): no host
+    round trip at all — the status travels on the device beside the factor (the owner's POTRF
+    `info`, or −1 for an error raised on the host) and the returned fit carries it as pending:
+    GPFit.check() raises, on every rank, once the job's predict has been queued."""
     ws, rank = world()
     if _solo(ws):
         if error is not None:
             raise error
         return gp
-    meta = torch.zeros(4, dtype=torch.int64, device=device)
-    if rank == src:
-        if error is None:
-            meta[0], meta[1], meta[2] = gp.n, gp.n_train, gp.n_pad
-        else:
-            meta[3] = 1 if isinstance(error, np.linalg.LinAlgError) else 2
-    dist.broadcast(meta, src)
-    n, ntr, npad, status = (int(v) for v in meta.tolist())
-    if status != 0:
+    dev = torch.device(device)
+    status = None
+    if layout is None:
+        meta = torch.zeros(4, dtype=torch.int64, device=dev)
         if rank == src:
-            raise error
-        if status == 1:
-            raise np.linalg.LinAlgError(f"the fit on rank {src} failed: K_y is not positive definite")
-        raise RuntimeError(f"the fit on rank {src} failed")
-    blocks = packed_blocks(n)
-    packed = torch.empty(blocks[-1][2], dtype=torch.float64, device=device)
-    if rank != src:
-        W = torch.zeros((n, n), dtype=torch.float64, device=device)
-        alpha = torch.empty(n, dtype=torch.float64, device=device)
-        X = torch.empty((ntr, spec.input_dim), dtype=torch.float64, device=device)
+            if error is None:
+                meta[0], meta[1], meta[2] = gp.n, gp.n_train, gp.n_pad
+            else:
+                meta[3] = 1 if isinstance(error, np.linalg.LinAlgError) else 2
+        dist.broadcast(meta, src)
+        n, ntr, npad, st = (int(v) for v in meta.tolist())
+        if st != 0:
+            if rank == src:
+                raise error
+            if st == 1:
+                raise np.linalg.LinAlgError(f"the fit on rank {src} failed: K_y is not positive definite")
+            raise RuntimeError(f"the fit on rank {src} failed")
     else:
+        n, ntr, npad = (int(v) for v in layout)
+        status = torch.full((1,), -1, dtype=torch.int32, device=dev)
+        if rank == src and error is None and gp is not None:
+            info = gp.extra.get("info_dev")
+            if info is not None:
+                status.copy_(info)
+            else:
+                status.zero_()
+        dist.broadcast(status, src)
+    packed = torch.empty(_packed_len(n), dtype=torch.float64, device=dev)
+    if rank == src and gp is not None and error is None:
         W, X, alpha = gp.W, gp.x, gp.alpha
-        for r0, c1, off in blocks[:-1]:
-            packed[off:off + PACK_ROWS * c1].view(PACK_ROWS, c1).copy_(W[r0:r0 + PACK_ROWS, :c1])
+        _pack_lower(W, n, packed, unpack=False)
+    else:
+        W = torch.zeros((n, n), dtype=torch.float64, device=dev)
+        alpha = torch.zeros(n, dtype=torch.float64, device=dev)
+        X = torch.zeros((ntr, spec.input_dim), dtype=torch.float64, device=dev)
+        if rank == src:
+            packed.zero_()
     # W = L⁻¹ is lower-triangular: only the row blocks' [0, end of their diagonal block)
     # columns travel (≈ half of n² doubles)
     dist.broadcast(packed, src)
     dist.broadcast(alpha, src)
     dist.broadcast(X, src)
-    if rank == src:
-        return gp
-    for r0, c1, off in blocks[:-1]:
-        W[r0:r0 + PACK_ROWS, :c1].copy_(packed[off:off + PACK_ROWS * c1].view(PACK_ROWS, c1))
-    return E.GPFit(kernel=spec, noise=float(noise), x=X, n_train=ntr, n_pad=npad, W=W, alpha=alpha,
-                   device=torch.device(device))
+    if rank == src and gp is not None and error is None:
+        out = gp
+    else:
+        _pack_lower(W, n, packed, unpack=True)
+        out = E.GPFit(kernel=spec, noise=float(noise), x=X, n_train=ntr, n_pad=npad, W=W, alpha=alpha, device=dev)
+    if status is not None and out is not gp:   # the owner's own fit keeps its pending info read
+        out.pending = E.pending_status(status, error if rank == src else None)
+    return out
+
+
+def _packed_len(n: int) -> int:
+    return packed_blocks(n)[-1][2]
+
+
+def _pack_lower(W: torch.Tensor, n: int, packed: torch.Tensor, unpack: bool):
+    """W's lower block triangle ↔ the packed payload: one gp2d_pack_lower launch on a device
+    tensor; CPU tensors (the gloo CPU tests of the communication logic) are copied block by
+    block."""
+    if W.is_cuda:
+        E.N.check(E.N.lib().gp2d_pack_lower(E._ptr(W), n, W.stride(0), E._ptr(packed), int(unpack),
+                                            E._stream_handle(W.device)), "gp2d_pack_lower")
+        return
+    for r0, c1, off in packed_blocks(n)[:-1]:
+        blk = packed[off:off + PACK_ROWS * c1].view(PACK_ROWS, c1)
+        if unpack:
+            W[r0:r0 + PACK_ROWS, :c1].copy_(blk)
+        else:
+            blk.copy_(W[r0:r0 + PACK_ROWS, :c1])
 
 
 PACK_ROWS = 128   # the matrix order is a multiple of 128 (engine.fit_layout)
@@ -354,8 +396,9 @@ def krige_jobs_sharded(jobs, variance: str = "ozaki", chunk: int = 8192, var_mod
                 own[idx] = (gp, err, ev)
 
     def receive(idx, job):
-        """Job idx's factor from its owner, on the comm stream: (gp, ready event) or the
-        exception every rank raises for it (kept until the job's turn)."""
+        """Job idx's factor from its owner, on the comm stream: (gp, ready event); the fit's
+        status travels on the device (gp.check() raises on every rank when the job is yielded),
+        so no rank waits on the host for another rank's fit."""
         spec, x, _, noise, _ = job
         owner = idx % ws
         gp, err = None, None
@@ -363,20 +406,18 @@ def krige_jobs_sharded(jobs, variance: str = "ozaki", chunk: int = 8192, var_mod
             gp, err, ev = own.pop(idx)
             if gp is not None:
                 comm.wait_event(ev)
-                gp.record_stream(comm)
-                try:
-                    gp.check()
-                except Exception as e:   # noqa: BLE001
-                    gp, err = None, e
-        try:
-            with torch.cuda.stream(comm):
-                gp = broadcast_fit(gp, spec, noise, x, dev, src=owner, error=err)
-                if variance == "ozaki" and "ozaki" not in gp.extra:
-                    E.ozaki_prepare(gp, diag_add=float(noise + jitter))   # a-priori moduli count
-                ready = torch.cuda.Event()
-                ready.record(comm)
-        except Exception as e:   # noqa: BLE001
-            return e
+                gp.record_stream(comm)   # its status word is the factor's info (the owner's own
+                #                          check() also raises a preparation error)
+            else:
+                comm.wait_stream(main)
+        ntr = int(np.prod(tuple(x.shape))) // spec.input_dim
+        npad, n = E.fit_layout(spec, ntr, variance)
+        with torch.cuda.stream(comm):
+            gp = broadcast_fit(gp, spec, noise, x, dev, src=owner, error=err, layout=(n, ntr, npad))
+            if variance == "ozaki" and "ozaki" not in gp.extra:
+                E.ozaki_prepare(gp, diag_add=float(noise + jitter))   # a-priori moduli count
+            ready = torch.cuda.Event()
+            ready.record(comm)
         return gp, ready
 
     refill()
@@ -386,8 +427,6 @@ def krige_jobs_sharded(jobs, variance: str = "ozaki", chunk: int = 8192, var_mod
     pred = None
     while window:
         idx, (spec, x, y, noise, xg) = window.popleft()
-        if isinstance(cur, Exception):
-            raise cur
         gp, ready = cur
         main.wait_event(ready)
         gp.record_stream(main)
@@ -397,8 +436,9 @@ def krige_jobs_sharded(jobs, variance: str = "ozaki", chunk: int = 8192, var_mod
         out = predict_shard(pred, E._as_points(xg, spec.input_dim, dev), var_mode=var_mode,
                             compute_var=compute_var, align=align)
         refill()
-        # the next job's factor travels (host may wait for its owner) while this predict runs
+        # the next job's factor travels while this predict runs
         cur = receive(*window[0]) if window else None
+        gp.check()   # this job's status (broadcast with its factor): raises on every rank
         yield out
 
 

@@ -233,12 +233,27 @@ _PINNED_INFO: list = []
 
 
 def _raise_fit_errors(inf: int, err):
+    if inf < 0:   # a status word from the job stream: the fit raised on its owner's host
+        if err is not None:
+            raise err
+        raise RuntimeError("the fit failed on the rank that owned it (see that rank's error)")
     if inf != 0:
         raise np.linalg.LinAlgError(
             f"K_y is not positive definite (leading minor of order {inf}); "
             "increase the noise / jitter (cf. sklearn _gpr.py:350-358)")
     if err is not None:
         raise err
+
+
+def pending_status(status: torch.Tensor, err=None) -> tuple:
+    """A GPFit.pending triple for a device status word (int32, LAPACK-style info; < 0: failed on
+    another rank): copied to pinned host memory after the work queued so far on the current
+    stream, checked by GPFit.check()."""
+    host = _PINNED_INFO.pop() if _PINNED_INFO else torch.empty(1, dtype=torch.int32, pin_memory=True)
+    host.copy_(status, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(status.device))
+    return host, ev, err
 
 
 def fit(kernel: KernelSpec, x, y, noise: float, jitter: float = 0.0, device=None, variance: str = "f64",
@@ -333,6 +348,7 @@ def fit(kernel: KernelSpec, x, y, noise: float, jitter: float = 0.0, device=None
     N.check(L.gp2d_potrs_inv(_ptr(A), n, n, _ptr(Y), _ptr(alpha), _ptr(pwork), pbytes, s), "gp2d_potrs_inv")
     gp = GPFit(kernel=kernel, noise=float(noise), x=X, n_train=ntr, n_pad=npad, W=A, alpha=alpha, device=dev,
                y=Y, perm=perm)
+    gp.extra["info_dev"] = info   # the factor's status word on the device (the job stream broadcasts it)
     del pwork
     err = None
     if variance == "ozaki":

@@ -264,7 +264,11 @@ int gp2d_transpose(const double* A, int64_t n, int64_t lda, double* At, void* st
  * diagonal block.  Per-element arithmetic is independent of P (P = 2 gives the bits of P = 1).
  * gp2d_copy2d: dst[rows×cols] = src (leading dims in doubles; hipMemcpy2DAsync) — the panel and
  *   W-column packing of the caller.  gp2d_zero_upper: zero the strict upper triangle of A outside
- *   its 128×128 diagonal blocks.                                                          */
+ *   its 128×128 diagonal blocks.
+ * gp2d_pack_lower: the factor broadcast's payload (any fit mode that sends W = L⁻¹): row block
+ *   rb of the lower-triangular n×n W keeps columns [0, 128·(rb+1)), blocks stored one after the
+ *   other (gp2d_pack_lower_doubles(n) = 128²·nb(nb+1)/2 doubles, ≈ n²/2); unpack = 1 writes them
+ *   back (the rest of W is left as it is).                                                  */
 size_t gp2d_dfact_panel_doubles(int64_t n);
 size_t gp2d_dfact_workspace(int64_t n);
 int gp2d_dfact_panel(double* A, int64_t n, int64_t lda, int s, double* panel, int* info_dev, void* work,
@@ -276,6 +280,8 @@ int gp2d_dfact_invstep(double* A, int64_t n, int64_t lda, int s, const double* p
 int gp2d_copy2d(double* dst, int64_t ldd, const double* src, int64_t lds, int64_t rows, int64_t cols,
                 void* stream);
 int gp2d_zero_upper(double* A, int64_t n, int64_t lda, void* stream);
+size_t gp2d_pack_lower_doubles(int64_t n);
+int gp2d_pack_lower(double* W, int64_t n, int64_t ldw, double* packed, int unpack, void* stream);
 
 /* ---- multi-GPU: factor broadcast --------------------------------
  * gp2d_bcast: in-place ncclBroadcast of `bytes` bytes of device memory from rank `root` over
