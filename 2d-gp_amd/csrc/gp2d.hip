@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cmath>
+#include <atomic>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -211,21 +212,33 @@ int gp2d_assemble(const double* xa, int64_t na, int64_t na_pad, const double* xb
 
 // ------------------------------------------------------------------------ POTRF
 namespace {
-// POTRF streams (one set per device, created lazily): `crit` carries the critical path
+// POTRF streams (a pool of sets per device, created lazily): `crit` carries the critical path
 // (block-column updates, diagonal block, panel TRSM) at the highest priority, `bulk` the
 // trailing SYRK, `inv` (low priority) the triangular inverse of the fused factor
 // (gp2d_potrf_inv).  (Hardware CU masks splitting the CUs between the streams were measured
-// slower at every split)  One factorisation enqueue at a time per device (a
-// per-device mutex held across potrf_impl serialises concurrent host threads).
+// slower at every split)  One factorisation enqueue at a time per set (its
+// mutex is held across potrf_impl's enqueue sequence).
 
 struct FactorStreams {
   std::mutex mu;
-  std::vector<std::unique_ptr<std::mutex>> enqueue;   // per device: one factorisation enqueue at a time
-  std::vector<hipStream_t> crit, bulk, aux, inv;   // indexed by device
-  std::vector<std::vector<hipEvent_t>> ev;         // 5 fixed events
-  std::vector<std::vector<hipEvent_t>> blk;        // one per block column (fused inverse)
+  // per device, up to GP2D_FACTOR_CTX stream sets, of which gp2d_factor_sets(k) puts k in use
+  // (default 1: every factorisation shares one set, as before the pool).  A caller stream keeps
+  // the set it was first given (sets dealt in order of first use), so with k > 1
+  // factorisations enqueued from different caller streams run concurrently on different sets
+  // — their chains interleave instead of queueing behind each other on one set of in-order
+  // streams
+  std::vector<std::vector<std::unique_ptr<struct FactorSet>>> sets;
+  std::vector<std::vector<std::pair<hipStream_t, int>>> owner;   // caller stream → its set
 };
+struct FactorSet {
+  std::mutex enqueue;                     // one factorisation enqueue at a time per set
+  hipStream_t crit = nullptr, bulk = nullptr, aux = nullptr, inv = nullptr;
+  std::vector<hipEvent_t> ev;             // 5 fixed events
+  std::vector<hipEvent_t> blk;            // one per block column (fused inverse)
+};
+constexpr int GP2D_FACTOR_CTX = 4;
 FactorStreams g_fs;
+std::atomic<int> g_factor_sets{1};   // sets in use (gp2d_factor_sets); 1: every caller shares one
 
 struct FactorCtx {
   hipStream_t crit, bulk, aux, inv;
@@ -234,47 +247,61 @@ struct FactorCtx {
   std::mutex* enqueue;
 };
 
-int factor_streams(FactorCtx& c, int nblk) {
+int factor_streams(FactorCtx& c, int nblk, hipStream_t caller) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) { set_error("hipGetDevice failed"); return -1; }
   std::lock_guard<std::mutex> lk(g_fs.mu);
-  if ((int)g_fs.crit.size() <= dev) {
-    g_fs.crit.resize(dev + 1, nullptr); g_fs.bulk.resize(dev + 1, nullptr); g_fs.aux.resize(dev + 1, nullptr);
-    g_fs.inv.resize(dev + 1, nullptr);
-    g_fs.ev.resize(dev + 1);
-    g_fs.blk.resize(dev + 1);
-    while ((int)g_fs.enqueue.size() <= dev) g_fs.enqueue.push_back(std::make_unique<std::mutex>());
+  if ((int)g_fs.sets.size() <= dev) {
+    g_fs.sets.resize(dev + 1);
+    g_fs.owner.resize(dev + 1);
   }
-  if (!g_fs.crit[dev]) {
+  auto& sets = g_fs.sets[dev];
+  auto& own = g_fs.owner[dev];
+  const int want = std::max(1, std::min(GP2D_FACTOR_CTX, g_factor_sets.load()));
+  int idx = -1;
+  for (const auto& pr : own)
+    if (pr.first == caller && pr.second < want) idx = pr.second;
+  if (idx < 0) {   // a new caller stream (or one whose set is no longer in use): next set in turn
+    int used = 0;
+    for (const auto& pr : own) used += pr.second < want;
+    idx = used % want;
+    for (auto& pr : own)
+      if (pr.first == caller) pr.second = idx;
+    bool known = false;
+    for (const auto& pr : own) known = known || pr.first == caller;
+    if (!known && own.size() < 256) own.emplace_back(caller, idx);
+  }
+  while ((int)sets.size() <= idx) {   // sets are created on first use: fewer streams, fewer HW queues shared
     int lo = 0, hi = 0;
     if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) { lo = 0; hi = 0; }
+    auto f = std::make_unique<FactorSet>();
     // crit (diagonal kernels, skinny panel GEMMs) and aux at the highest priority, bulk (the
-    // trailing SYRK) and inv (the fused inverse's GEMMs) at the lowest.  Keeping R CUs free of
-    // the bulk stream (CU-masked stream) was measured: no gain at N = 4096, slower at N = 16384
-    // (DESIGN.md §3.6).
-    const bool bulk_ok = hipStreamCreateWithPriority(&g_fs.bulk[dev], hipStreamNonBlocking, lo) == hipSuccess;
-    if (hipStreamCreateWithPriority(&g_fs.crit[dev], hipStreamNonBlocking, hi) != hipSuccess || !bulk_ok ||
-        hipStreamCreateWithPriority(&g_fs.aux[dev], hipStreamNonBlocking, hi) != hipSuccess ||
-        hipStreamCreateWithPriority(&g_fs.inv[dev], hipStreamNonBlocking, lo) != hipSuccess) {
+    // trailing SYRK) and inv (the fused inverse's GEMMs) at the lowest.  Keeping CUs free of
+    // the bulk stream (CU-masked streams) was measured slower.
+    if (hipStreamCreateWithPriority(&f->crit, hipStreamNonBlocking, hi) != hipSuccess ||
+        hipStreamCreateWithPriority(&f->bulk, hipStreamNonBlocking, lo) != hipSuccess ||
+        hipStreamCreateWithPriority(&f->aux, hipStreamNonBlocking, hi) != hipSuccess ||
+        hipStreamCreateWithPriority(&f->inv, hipStreamNonBlocking, lo) != hipSuccess) {
       set_error("hipStreamCreate failed"); return -1;
     }
-    g_fs.ev[dev].resize(5);
-    for (auto& e : g_fs.ev[dev])
+    f->ev.resize(5);
+    for (auto& e : f->ev)
       if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) { set_error("hipEventCreate failed"); return -1; }
+    sets.push_back(std::move(f));
   }
-  auto& b = g_fs.blk[dev];
-  while ((int)b.size() < nblk) {
+  FactorSet& f = *sets[idx];
+  while ((int)f.blk.size() < nblk) {
     hipEvent_t e;
     if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) { set_error("hipEventCreate failed"); return -1; }
-    b.push_back(e);
+    f.blk.push_back(e);
   }
-  c.crit = g_fs.crit[dev];
-  c.bulk = g_fs.bulk[dev];
-  c.aux = g_fs.aux[dev];
-  c.inv = g_fs.inv[dev];
-  c.ev = &g_fs.ev[dev];
-  c.blk = &g_fs.blk[dev];
-  c.enqueue = g_fs.enqueue[dev].get();
+  c.crit = f.crit;
+  c.bulk = f.bulk;
+  c.aux = f.aux;
+  c.inv = f.inv;
+  c.ev = &f.ev;
+  c.blk = &f.blk;
+  c.enqueue = &f.enqueue;
   return 0;
 }
 
@@ -379,9 +406,9 @@ static int potrf_impl(double* A, int64_t n, int64_t lda, double* dinv, int* info
   const int nb = (int)(n / NB);
   const bool fused = Tws != nullptr;
   FactorCtx fc;
-  GP2D_CHECK(factor_streams(fc, fused ? 1 : 0));
-  // the device's internal streams and events are shared: two host threads factoring on one
-  // device would interleave their records and waits, so the whole enqueue sequence is serialised
+  GP2D_CHECK(factor_streams(fc, fused ? 1 : 0, s));
+  // a set's streams and events are shared by every factorisation that draws it: two host
+  // threads on one set would interleave their records and waits, so its enqueue is serialised
   std::lock_guard<std::mutex> enqueue_lock(*fc.enqueue);
   hipStream_t sc = fc.crit, sb = fc.bulk, sa = fc.aux, si = fc.inv;
   std::vector<hipEvent_t>& ev = *fc.ev;
@@ -477,6 +504,12 @@ static int potrf_impl(double* A, int64_t n, int64_t lda, double* dinv, int* info
 
 extern "C" {
 size_t gp2d_potrf_workspace(int64_t) { return 0; }
+
+int gp2d_factor_sets(int k) {
+  const int prev = g_factor_sets.load();
+  if (k >= 1) g_factor_sets.store(std::min(k, GP2D_FACTOR_CTX));
+  return prev;
+}
 
 int gp2d_potrf(double* A, int64_t n, int64_t lda, double* dinv, int* info_dev, void*, size_t, void* stream) {
   return potrf_impl(A, n, lda, dinv, info_dev, S(stream), nullptr);

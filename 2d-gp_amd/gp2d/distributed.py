@@ -233,7 +233,7 @@ def fit_distributed(spec: E.KernelSpec, x, y, noise: float, device=None, varianc
     wbytes = int(L.gp2d_dfact_workspace(n))
     work = torch.empty(wbytes // 8 + 1, dtype=torch.float64, device=dev)
     info = torch.zeros(1, dtype=torch.int32, device=dev)
-    comm = torch.cuda.Stream(dev)
+    comm = E.side_stream(dev)
     t0 = time.perf_counter()
 
     factored = {}   # s → main-stream event after the owner's gp2d_dfact_panel(s)
@@ -365,8 +365,8 @@ def krige_jobs_sharded(jobs, variance: str = "ozaki", chunk: int = 8192, var_mod
             yield 0, int(xg.shape[0]), mean, var
         return
     main = torch.cuda.current_stream(dev)
-    fit_stream = torch.cuda.Stream(dev)
-    comm = torch.cuda.Stream(dev)   # broadcasts + the receivers' int8 preparation
+    fit_stream = E.side_stream(dev)
+    comm = E.side_stream(dev)   # broadcasts + the receivers' int8 preparation
     it = iter(jobs)
     window = collections.deque()   # (index, job) read ahead
     own = {}                       # index → (gp, error, event) of this rank's fits in flight

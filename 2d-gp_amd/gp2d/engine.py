@@ -11,6 +11,7 @@ Reference call sites replaced:
 """
 from __future__ import annotations
 
+import collections
 import ctypes
 import time
 from dataclasses import dataclass, field
@@ -55,6 +56,17 @@ def morton_order(P: torch.Tensor) -> torch.Tensor:
     N.check(N.lib().gp2d_morton_codes(_ptr(P), n, d, _ptr(scratch), _ptr(code), _stream_handle(P.device)),
             "gp2d_morton_codes")
     return torch.argsort(code, stable=True)
+
+
+def side_stream(device=None) -> torch.cuda.Stream:
+    """A stream for work that has to overlap the current (predict) stream — a job's fit, a
+    broadcast, concurrent settings.  Taken from torch's HIGH-priority pool: HIP maps streams
+    onto at most GPU_MAX_HW_QUEUES hardware queues per priority level (4 on the box), and two
+    streams that share a queue run in order, so a side stream on the current stream's queue
+    overlaps nothing.  torch's normal-priority pool streams can land there (tools/probe_queues.py:
+    pool streams 6 and 10 of 12 did, profiles/r03_queue_aliasing.json); the high-priority pool is
+    a different set of queues."""
+    return torch.cuda.Stream(device, priority=-1)
 
 
 def _as_points(x, dim: int, device) -> torch.Tensor:
@@ -571,7 +583,8 @@ def note_fit_issued(stats: dict | None):
 
 
 def krige_jobs(jobs, variance: str = "ozaki", chunk: int = 8192, var_mode: str = "latent",
-               compute_var: bool = True, jitter: float = 0.0, device=None, stats: dict | None = None):
+               compute_var: bool = True, jitter: float = 0.0, device=None, stats: dict | None = None,
+               fits_ahead: int = 1):
     """Independent kriging jobs (kernel, x, y, noise, xg), one after another — the reference's
     runKrig.py:1-40 sweep (one GP_laser / krig.kriging fit + grid predict per setting or
     time window) run in one process.  Yields (mean, var) per job, in order, on the current
@@ -584,34 +597,58 @@ def krige_jobs(jobs, variance: str = "ozaki", chunk: int = 8192, var_mode: str =
     raises numpy.linalg.LinAlgError when job i is yielded, as fit() would.  The predict
     workspace is reused while consecutive jobs have the same padded size.  Nothing is read
     ahead before the first next(): a fresh generator's first fit is issued by that call (the
-    bench times its jobs on a fresh generator for this reason).  `stats` counts the fits issued."""
+    bench times its jobs on a fresh generator for this reason).  `stats` counts the fits issued.
+
+    fits_ahead = k > 1: up to k fits in flight on k side streams, each queued before the
+    predict stream waits for the job ahead of it, so consecutive fits also overlap each other
+    (gp2d_potrf draws a separate internal stream set per call) — for small jobs whose
+    latency-bound fit is longer than their predict (config B)."""
     dev = _require_device(device)
     main = torch.cuda.current_stream(dev)
-    side = torch.cuda.Stream(dev)
+    k = max(1, int(fits_ahead))
+    sides = [side_stream(dev) for _ in range(k)]
+    prev_sets = N.lib().gp2d_factor_sets(k) if k > 1 else None   # one internal factor set per side stream
+    issued = [0]
 
     def queue_fit(job):
         kernel, x, y, noise, _ = job
+        side = sides[issued[0] % k]
+        issued[0] += 1
         side.wait_stream(main)
         note_fit_issued(stats)
         with torch.cuda.stream(side):
-            return fit(kernel, x, y, noise, jitter=jitter, device=dev, variance=variance, check=False)
+            return side, fit(kernel, x, y, noise, jitter=jitter, device=dev, variance=variance, check=False)
 
     it = iter(jobs)
-    job = next(it, None)
-    gp = queue_fit(job) if job is not None else None
-    pred = None
-    while job is not None:
-        main.wait_stream(side)
-        gp.record_stream(main)
-        nxt = next(it, None)
-        gp_next = queue_fit(nxt) if nxt is not None else None
-        if pred is None or not pred.fits(gp):
-            pred = Predictor(gp, chunk)
-        pred.gp = gp
-        out = pred(job[4], var_mode=var_mode, compute_var=compute_var)
-        gp.check()
-        yield out
-        job, gp = nxt, gp_next
+    queue = collections.deque()   # (job, side stream, gp) with the fit queued
+
+    def fill(limit):
+        while len(queue) < limit:
+            job = next(it, None)
+            if job is None:
+                return
+            queue.append((job, *queue_fit(job)))
+
+    try:
+        fill(1)
+        pred = None
+        while queue:
+            if k > 1:
+                fill(k)   # before the predict stream waits for the head job's fit
+            job, side, gp = queue.popleft()
+            main.wait_stream(side)
+            gp.record_stream(main)
+            if k == 1:
+                fill(1)   # the next job's fit, under this job's predict
+            if pred is None or not pred.fits(gp):
+                pred = Predictor(gp, chunk)
+            pred.gp = gp
+            out = pred(job[4], var_mode=var_mode, compute_var=compute_var)
+            gp.check()
+            yield out
+    finally:
+        if prev_sets is not None:
+            N.lib().gp2d_factor_sets(prev_sets)
 
 
 # ------------------------------------------------------------------ hyperparameters
@@ -636,6 +673,15 @@ def log_marginal_likelihood(gp: GPFit, eval_gradient: bool = False):
     sklearn log_marginal_likelihood(theta, eval_gradient=True) (_gpr.py:584-650); the
     gradient is the exact one (the reference's myKernel.update_gradients_full is not,
     SURVEY.md §0.2).  Both run in HIP kernels (gp2d_lml, gp2d_lml_grad)."""
+    out, g = lml_device(gp, eval_gradient)
+    if not eval_gradient:
+        return float(out.item())
+    return float(out.item()), g.cpu().numpy()
+
+
+def lml_device(gp: GPFit, eval_gradient: bool = False):
+    """log_marginal_likelihood without a host round trip: (lml, grad or None) as device tensors,
+    queued on the current stream (hyper.sweep overlaps settings this way)."""
     if gp.y is None:
         raise ValueError("this fit carries no observations (it was not made by engine.fit)")
     L = N.lib()
@@ -645,7 +691,7 @@ def log_marginal_likelihood(gp: GPFit, eval_gradient: bool = False):
     N.check(L.gp2d_lml(_ptr(gp.W), gp.n, gp.n, _ptr(gp.alpha), _ptr(gp.y), bd * gp.n_train, _ptr(out), s),
             "gp2d_lml")
     if not eval_gradient:
-        return float(out.item())
+        return out, None
     desc = gp.kernel.desc()
     ng = int(L.gp2d_lml_grad_count(ctypes.byref(desc)))
     wbytes = int(L.gp2d_lml_grad_workspace(gp.n))
@@ -653,7 +699,7 @@ def log_marginal_likelihood(gp: GPFit, eval_gradient: bool = False):
     g = torch.empty(ng, dtype=torch.float64, device=gp.device)
     N.check(L.gp2d_lml_grad(_ptr(gp.W), gp.n, gp.n, _ptr(gp.alpha), _ptr(gp.x), gp.n_train, gp.n_pad,
                             ctypes.byref(desc), _ptr(g), _ptr(work), wbytes, s), "gp2d_lml_grad")
-    return float(out.item()), g.cpu().numpy()
+    return out, g
 
 
 def kernel_grad(kernel: KernelSpec, xa, dL_dK, xb=None, device=None) -> np.ndarray:

@@ -21,6 +21,8 @@ bit-identical for any world size.
 """
 from __future__ import annotations
 
+import collections
+
 import dataclasses
 import math
 from dataclasses import dataclass, field
@@ -194,31 +196,74 @@ def optimize_restarts(kernel: E.KernelSpec, x, y, noise: float, num_restarts: in
 
 
 def sweep(kernel: E.KernelSpec, x, y, settings, noise: float = None, jitter: float = 0.0, device=None,
-          eval_gradient: bool = False):
+          eval_gradient: bool = False, concurrent: int = 1):
     """LML (and gradient) for each hyperparameter setting (a list of get_params-style dicts,
     missing keys taken from kernel/noise) — BASELINE config E.  Under torch.distributed the
     settings are dealt round-robin over ranks and the results all-reduced (bit-identical to
-    one rank).  Returns (lml[S], grad[S, P] or None); a non-PD setting gives -inf."""
+    one rank).  Returns (lml[S], grad[S, P] or None); a non-PD setting gives -inf.
+
+    concurrent = c > 1: the settings' fit + LML (+ gradient) chains are queued on c streams
+    with no host round trip (engine.fit(check=False), engine.lml_device), so the latency-bound
+    factorisations of c settings interleave on the GPU (each draws its own internal stream
+    set); results are read back 2c settings behind.  Same kernels, same bits as c = 1."""
     ws, rank = (dist.get_world_size(), dist.get_rank()) if dist.is_available() and dist.is_initialized() else (1, 0)
     base = get_params(kernel, noise if noise is not None else 0.0)
     S = len(settings)
     P = len(base)
     vals = np.zeros(S)
     grads = np.zeros((S, P))
-    for i in range(rank, S, ws):
-        p = dict(base)
-        p.update(settings[i])
-        k, nz = set_params(kernel, p)
-        try:
-            gp = E.fit(k, x, y, nz, jitter=jitter, device=device)
-        except np.linalg.LinAlgError:
-            vals[i] = -np.inf
-            continue
-        if eval_gradient:
-            vals[i], grads[i] = E.log_marginal_likelihood(gp, eval_gradient=True)
-        else:
-            vals[i] = E.log_marginal_likelihood(gp)
-        del gp
+    mine = list(range(rank, S, ws))
+    c = max(1, int(concurrent))
+    if c == 1:
+        for i in mine:
+            p = dict(base)
+            p.update(settings[i])
+            k, nz = set_params(kernel, p)
+            try:
+                gp = E.fit(k, x, y, nz, jitter=jitter, device=device)
+            except np.linalg.LinAlgError:
+                vals[i] = -np.inf
+                continue
+            if eval_gradient:
+                vals[i], grads[i] = E.log_marginal_likelihood(gp, eval_gradient=True)
+            else:
+                vals[i] = E.log_marginal_likelihood(gp)
+            del gp
+    else:
+        dev = E._require_device(device)
+        main = torch.cuda.current_stream(dev)
+        streams = [E.side_stream(dev) for _ in range(c)]
+        prev_sets = E.N.lib().gp2d_factor_sets(c)   # one internal factor stream set per stream
+        inflight = collections.deque()
+
+        def drain(limit):
+            while len(inflight) > limit:
+                i, gp, out, g, ev = inflight.popleft()
+                ev.synchronize()
+                try:
+                    gp.check()
+                except np.linalg.LinAlgError:
+                    vals[i] = -np.inf
+                    continue
+                vals[i] = float(out.item())
+                if g is not None:
+                    grads[i] = g.cpu().numpy()
+
+        for j, i in enumerate(mine):
+            p = dict(base)
+            p.update(settings[i])
+            k, nz = set_params(kernel, p)
+            st = streams[j % c]
+            st.wait_stream(main)
+            with torch.cuda.stream(st):
+                gp = E.fit(k, x, y, nz, jitter=jitter, device=dev, check=False)
+                out, g = E.lml_device(gp, eval_gradient)
+                ev = torch.cuda.Event()
+                ev.record(st)
+            inflight.append((i, gp, out, g, ev))
+            drain(2 * c)
+        drain(0)
+        E.N.lib().gp2d_factor_sets(prev_sets)
     if ws > 1:
         vals, grads = allreduce_disjoint(vals, grads, device)
     return vals, (grads if eval_gradient else None)

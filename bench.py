@@ -94,6 +94,10 @@ def parse():
                     help="time the numpy oracle on the host cores (N=1 only); -1 = only when N_train <= 4096")
     ap.add_argument("--cpu-sample-points", type=int, default=2048)
     ap.add_argument("--pmc-json", default=None)
+    ap.add_argument("--fits-ahead", type=int, default=None,
+                    help="N=1 job stream: fits in flight (engine.krige_jobs fits_ahead; default 1, config B 2)")
+    ap.add_argument("--sweep-concurrent", type=int, default=None,
+                    help="config E: settings whose fit + LML chains run concurrently (hyper.sweep concurrent)")
     ap.add_argument("--single-job-dist", type=int, default=0,
                     help="also time one job with distributed.fit_distributed at N = 1 (always at N > 1)")
     a = ap.parse_args()
@@ -176,8 +180,10 @@ def run_sweep(args, ws, rank, dev):
     settings = config_e_settings()
     ks = E.KernelSpec(kind="df", l_df=5.0)
 
+    conc = args.sweep_concurrent or 1
+
     def sweep():
-        return H.sweep(ks, xt, yt, settings, noise=0.0025, eval_gradient=True, device=dev)
+        return H.sweep(ks, xt, yt, settings, noise=0.0025, eval_gradient=True, device=dev, concurrent=conc)
 
     for _ in range(args.warmup):
         sweep()
@@ -284,7 +290,7 @@ def main():
     mean = torch.empty(2 * m, dtype=torch.float64, device=dev)
     var = torch.empty(2 * m, dtype=torch.float64, device=dev)
     pred_cache = {}
-    side = torch.cuda.Stream(dev) if args.variance == "ozaki" else None
+    side = E.side_stream(dev) if args.variance == "ozaki" else None
     cfg = {"mode": args.fit_mode if is_multi(ws) else "local", "ahead": False,
            "pipeline": bool(args.pipeline) and not is_multi(ws) or (bool(args.pipeline) and args.fit_mode == "replicate")
            or (is_multi(ws) and args.fit_mode == "rr"),
@@ -303,7 +309,7 @@ def main():
             last[0].check()
             last[0] = None
 
-    fit_stream = torch.cuda.Stream(dev)
+    fit_stream = E.side_stream(dev)
     main_stream = torch.cuda.current_stream(dev)
 
     def do_fit():
@@ -392,7 +398,8 @@ def main():
         job = (spec, xt, yt, noise, xg)
 
         def stream(k):   # the shipped API for a sweep of jobs
-            return E.krige_jobs(itertools.repeat(job, k), variance=args.variance, chunk=args.chunk, stats=stats)
+            return E.krige_jobs(itertools.repeat(job, k), variance=args.variance, chunk=args.chunk, stats=stats,
+                                fits_ahead=args.fits_ahead or 1)
         api = "engine.krige_jobs"
     trace = os.environ.get("GP2D_BENCH_TRACE") == "1"   # per-step wall times on stderr (diagnostics)
 

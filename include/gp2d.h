@@ -90,9 +90,13 @@ int gp2d_assemble(const double* xa, int64_t na, int64_t na_pad,
  * Cholesky inside GPy / sklearn (_gpr.py:349).  On return the strict upper
  * triangle is zero.  If dinv != NULL it receives the (n/128) inverted 128×128
  * diagonal blocks (input to gp2d_trtri).  *info_dev as LAPACK potrf.
- * Thread safety: the factorisation runs on internal per-device streams and events
- * joined to `stream`; concurrent calls for one device from several host threads are
- * serialised (a per-device lock is held while the work is enqueued).            */
+ * Concurrency: the factorisation runs on internal streams joined to `stream` at both
+ * ends.  By default every call shares one set of internal streams per device;
+ * gp2d_factor_sets(k) (k ≤ 4, returns the previous k) puts k sets in use — a caller
+ * stream keeps the set it first drew — so factorisations issued on different caller
+ * streams run concurrently, their latency-bound chains interleaved (engine.krige_jobs
+ * fits_ahead).  Each set's enqueue is serialised by its own lock (thread-safe).     */
+int gp2d_factor_sets(int k);
 size_t gp2d_potrf_workspace(int64_t n);
 int gp2d_potrf(double* A, int64_t n, int64_t lda, double* dinv, int* info_dev,
                void* work, size_t work_bytes, void* stream);

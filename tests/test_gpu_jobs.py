@@ -29,10 +29,12 @@ JOBS = [(1, 700, 60, "df"), (2, 700, 64, "mixed"), (3, 1500, 50, "df"), (4, 300,
         (5, 1500, 72, "mixed"), (6, 1500, 72, "df")]
 
 
-@pytest.mark.parametrize("variance", ["ozaki", "f64"])
-def test_krige_jobs_bit_identical_to_sequential(variance):
+@pytest.mark.parametrize("variance,ahead", [("ozaki", 1), ("f64", 1), ("ozaki", 2), ("ozaki", 3)])
+def test_krige_jobs_bit_identical_to_sequential(variance, ahead):
+    """fits_ahead > 1: consecutive fits in flight together, each drawing its own internal
+    factor stream set — still the bits of one job at a time."""
     jobs = [_job(*j) for j in JOBS]
-    got = [(m.clone(), v.clone()) for m, v in E.krige_jobs(jobs, variance=variance, chunk=2048)]
+    got = [(m.clone(), v.clone()) for m, v in E.krige_jobs(jobs, variance=variance, chunk=2048, fits_ahead=ahead)]
     assert len(got) == len(jobs)
     for (spec, x, y, noise, xg), (m, v) in zip(jobs, got):
         gp = E.fit(spec, x, y, noise, variance=variance)
@@ -40,9 +42,10 @@ def test_krige_jobs_bit_identical_to_sequential(variance):
         assert torch.equal(m, rm) and torch.equal(v, rv)
 
 
-def test_krige_jobs_non_spd_raises_at_its_job():
+@pytest.mark.parametrize("ahead", [1, 2])
+def test_krige_jobs_non_spd_raises_at_its_job(ahead):
     jobs = [_job(1, 500, 40, "df"), _job(2, 500, 40, "df", noise=-100.0), _job(3, 500, 40, "df")]
-    gen = E.krige_jobs(jobs, variance="ozaki", chunk=1024)
+    gen = E.krige_jobs(jobs, variance="ozaki", chunk=1024, fits_ahead=ahead)
     m, v = next(gen)
     assert torch.isfinite(v).all()
     with pytest.raises(np.linalg.LinAlgError):

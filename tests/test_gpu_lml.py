@@ -210,11 +210,16 @@ def test_optimize_restarts_mixed_and_fix():
     assert fixed.kernel.ratio == 0.5 and fixed.noise == 0.02
 
 
-def test_sweep_matches_individual_fits():
+@pytest.mark.parametrize("concurrent", [1, 3])
+def test_sweep_matches_individual_fits(concurrent):
+    """concurrent > 1 queues several settings' fit + LML chains on separate streams with no host
+    round trip; a non-PD setting still gives -inf (the last setting's negative noise)."""
     x, y = tracks(500, seed=8)
     ks = E.KernelSpec(kind="df", l_df=5.0)
-    settings = [dict(l_df=l, noise=nz) for l in (3.0, 5.0, 8.0) for nz in (0.0025, 0.01)]
-    vals, grads = H.sweep(ks, x, y, settings, noise=0.0025, eval_gradient=True)
+    settings = [dict(l_df=l, noise=nz) for l in (3.0, 5.0, 8.0) for nz in (0.0025, 0.01)] + [dict(noise=-50.0)]
+    vals, grads = H.sweep(ks, x, y, settings, noise=0.0025, eval_gradient=True, concurrent=concurrent)
+    assert vals[-1] == -np.inf
+    vals, grads, settings = vals[:-1], grads[:-1], settings[:-1]
     for s, v, g in zip(settings, vals, grads):
         gp = E.fit(E.KernelSpec(kind="df", l_df=s["l_df"]), x, y, s["noise"])
         rv, rg = E.log_marginal_likelihood(gp, eval_gradient=True)
