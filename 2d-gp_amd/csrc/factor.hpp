@@ -86,10 +86,14 @@ __device__ __forceinline__ void reg_trtri_lower(const double* __restrict__ Ls, d
 }
 
 // ---------------------------------------------------------------------------------------
-// Blocked diagonal-block kernel.  The 128×128 block lives in LDS (130 KB, fp64, row pitch
-// 130 doubles, so column-strided ds_read_b128 across 16 rows hit 16 distinct bank groups and
-// every access is a per-row base plus an immediate offset).  The n sequential pivots of the whole
-// factorisation are the critical path of POTRF, so each pivot must be cheap:
+// Blocked diagonal-block kernel.  The lower 128×128 block lives in LDS in a block-lower
+// layout: 32-row block row rb keeps columns [0, 32(rb+1)) — the whole of its diagonal 32×32
+// block, nothing right of it — at a row pitch of 32(rb+1) + 2 doubles (≡ 16 B mod 256 B, so
+// column-strided ds_read_b128 across 16 rows hit 16 distinct bank groups).  82 KB instead of
+// the 130 KB of a full-pitch square: the kernel then fits on a CU beside one workgroup of the
+// trailing SYRK (72 KB), where the square needed an empty CU and waited up to 240 µs for one
+// while the SYRK held every CU.  The n sequential pivots of the whole factorisation are the
+// critical path of POTRF, so each pivot must be cheap:
 //   Cholesky, 4 panels of 32 columns: ONE wave factors the 128−32p × 32 panel with the
 //     panel in registers (lane l: rows 32p+l and 32p+64+l) — per pivot a readlane of the
 //     diagonal, a sqrt, one LDS write/broadcast-read of the pivot column and ≤ 62 FMAs,
@@ -98,8 +102,18 @@ __device__ __forceinline__ void reg_trtri_lower(const double* __restrict__ Ls, d
 //   Inverse, W = L⁻¹ in place: each wave inverts one 32×32 diagonal block by forward
 //     substitution (lane j owns column j, no cross-lane traffic), then block rows
 //     i = 1..3:  T_ij = Σ_{p=j}^{i-1} L_ip W_pj,  W_ij = −W_ii T_ij.
-constexpr int DP = NB + 2;  // row pitch (doubles): 1040 B ≡ 4 banks mod 64, so 16 rows → 16 bank groups
-__device__ __forceinline__ int dsw(int r, int c) { return r * DP + c; }
+__host__ __device__ constexpr int dpitch(int rb) { return 32 * rb + 34; }   // doubles per row of block row rb
+// first double of block row rb: 32 · Σ_{i<rb} dpitch(i)
+__host__ __device__ constexpr int dbase(int rb) { return 512 * rb * (rb - 1) + 1088 * rb; }
+constexpr int DS_DOUBLES = dbase(NB / 32);   // 10,496 doubles = 82 KB
+static_assert(dbase(1) == 32 * dpitch(0) && dbase(2) == dbase(1) + 32 * dpitch(1) &&
+                  dbase(3) == dbase(2) + 32 * dpitch(2) && DS_DOUBLES == dbase(3) + 32 * dpitch(3),
+              "block-lower LDS layout");
+__device__ __forceinline__ int dsw(int r, int c) {
+  const int rb = r >> 5;
+  return dbase(rb) + (r & 31) * dpitch(rb) + c;
+}
+__device__ __forceinline__ int drowlen(int r) { return 32 * ((r >> 5) + 1); }   // stored columns of row r
 
 __device__ __forceinline__ double readlane_f64(double v, int lane) {
   const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
@@ -125,22 +139,37 @@ __device__ __forceinline__ Pivot make_pivot(double d) {
 // One pivot of the single-wave panel factorisation (K is a compile-time column index so
 // that x0/x1 stay in registers).  Column K+1 is updated first and pivot K+1 is formed
 // right after it, so its rsq/Newton chain overlaps the remaining FMAs of step K.
+// The multipliers L[c][K] come through one LDS broadcast of the column.  (Dev builds can take
+// the next GP2D_PANEL_RL columns' multipliers straight from lane c's register by v_readlane
+// instead, so the pivot chain K → K+1 carries no LDS round trip: 1, 2 and 4 such columns measured
+// 54.4–54.9 µs per diagonal block against 54.0 µs — the panel wave is issue-bound on its
+// 2·(31 − K) FMAs per pivot, not bound by the broadcast's latency; tools/microbench diag_bench_rl*.)
+#ifndef GP2D_PANEL_RL
+#define GP2D_PANEL_RL 0
+#endif
 template <int K, bool X1>
 __device__ __forceinline__ void panel_step(double (&x0)[32], double (&x1)[32], double* colbuf, int lane, int& bad,
                                            Pivot& pv) {
+  constexpr int RL = GP2D_PANEL_RL;
   bad = (bad == 0 && !(pv.d > 0.0)) ? K + 1 : bad;  // no branch: keeps the pivot chain schedulable
   x0[K] = (lane > K) ? x0[K] * pv.ird : ((lane == K) ? pv.rd : x0[K]);
   if constexpr (X1) x1[K] *= pv.ird;
   if constexpr (K < 31) {
-    if (lane < 32) colbuf[lane] = x0[K];
-    __builtin_amdgcn_wave_barrier();
-    constexpr int C0 = (K + 1) & ~1;
     double lc[32];
+    if constexpr (RL > 0) {
 #pragma unroll
-    for (int c = C0; c < 32; c += 2) {
-      const d2 t = *reinterpret_cast<const d2*>(colbuf + c);
-      lc[c] = t.x;
-      lc[c + 1] = t.y;
+      for (int c = K + 1; c < 32 && c <= K + RL; ++c) lc[c] = readlane_f64(x0[K], c);
+    }
+    constexpr int C0 = (K + 1 + RL) & ~1;
+    if constexpr (C0 < 32) {
+      if (lane < 32) colbuf[lane] = x0[K];
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int c = C0; c < 32; c += 2) {
+        const d2 t = *reinterpret_cast<const d2*>(colbuf + c);
+        if (c > K + RL) lc[c] = t.x;
+        lc[c + 1] = t.y;
+      }
     }
     x0[K + 1] = fma(-x0[K], lc[K + 1], x0[K + 1]);
     asm volatile("" : "+v"(x0[K + 1]));
@@ -174,13 +203,14 @@ __device__ __forceinline__ int panel_steps(std::integer_sequence<int, Ks...>, do
 }
 
 // Column step K of the forward substitution L X = I, 32×32 block at b0 (lane ↔ column j
-// of X): finalise x[K], then eliminate it from the rows below (pinned like panel_step).
+// of X): finalise x[K] (rl: lane i holds 1 / L_ii), then eliminate it from the rows below
+// (pinned like panel_step).
 template <int K>
-__device__ __forceinline__ void inv_step(double (&x)[32], const double* S, int b0) {
+__device__ __forceinline__ void inv_step(double (&x)[32], const double* S, int b0, double rl) {
   double lk[32];  // column K below the diagonal: all reads issued before the first use
 #pragma unroll
-  for (int i = K; i < 32; ++i) lk[i] = S[dsw(b0 + i, b0 + K)];
-  x[K] = x[K] * lk[K];  // the diagonal holds 1/L_KK here (see below)
+  for (int i = K + 1; i < 32; ++i) lk[i] = S[dsw(b0 + i, b0 + K)];
+  x[K] = x[K] * readlane_f64(rl, K);
 #pragma unroll
   for (int i = K + 1; i < 32; ++i) {
     x[i] = fma(-lk[i], x[K], x[i]);
@@ -188,8 +218,9 @@ __device__ __forceinline__ void inv_step(double (&x)[32], const double* S, int b
   }
 }
 template <int... Ks>
-__device__ __forceinline__ void inv_steps(std::integer_sequence<int, Ks...>, double (&x)[32], const double* S, int b0) {
-  (inv_step<Ks>(x, S, b0), ...);
+__device__ __forceinline__ void inv_steps(std::integer_sequence<int, Ks...>, double (&x)[32], const double* S, int b0,
+                                          double rl) {
+  (inv_step<Ks>(x, S, b0, rl), ...);
 }
 
 // 4×4 register tile of a 32×32 block product, one wave per block (lane → rows
@@ -261,149 +292,197 @@ __device__ __forceinline__ void tile4x4_store(double* __restrict__ S, int r, int
 // uses dinv), which is TRTRI's level 0.
 __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A, int64_t lda, int k0,
                                                          double* __restrict__ dinv, int* info, int inv_in_place) {
-  __shared__ __attribute__((aligned(16))) double S[NB * DP];
+  __shared__ __attribute__((aligned(16))) double S[DS_DOUBLES];
   __shared__ __attribute__((aligned(16))) double colbuf[32];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   double* Ab = A + (int64_t)k0 * lda + k0;
   GP2D_STAMP(0);
-  // load: 16-B vectors, rows coalesced, 8 loads in flight per thread
-#pragma unroll 1
-  for (int e0 = 0; e0 < (NB * NB / 2) / 256; e0 += 8) {
-    d2 v[8];
+  // load the stored (block-lower) part: block row rb is 32 rows × 16(rb+1) 16-B vectors, rows
+  // coalesced; all 20 loads of a thread in flight before the first LDS store
+  {
+    d2 v[20];
+    auto each = [&](auto&& fn) {
+      int u = 0;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int idx = tid + 256 * (e0 + u), r = idx >> 6, ch = idx & 63;
-      v[u] = *reinterpret_cast<const d2*>(Ab + (int64_t)r * lda + 2 * ch);
-    }
+      for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int idx = tid + 256 * (e0 + u), r = idx >> 6, ch = idx & 63;
-      *reinterpret_cast<d2*>(S + dsw(r, 2 * ch)) = v[u];
-    }
+        for (int w = 0; w < 2 * (rb + 1); ++w, ++u) {
+          const int idx = tid + 256 * w, rr = idx / (16 * (rb + 1)), ch = idx % (16 * (rb + 1));
+          fn(u, 32 * rb + rr, dbase(rb) + rr * dpitch(rb) + 2 * ch, 2 * ch);
+        }
+    };
+    each([&](int u, int r, int, int c) { v[u] = *reinterpret_cast<const d2*>(Ab + (int64_t)r * lda + c); });
+    each([&](int u, int, int s, int) { *reinterpret_cast<d2*>(S + s) = v[u]; });
   }
   __syncthreads();
   GP2D_STAMP(1);
-  // ---- Cholesky
-  // row mapping inside the per-wave 32×32 tiles of the trailing update: 8 rows per wave,
-  // 4 consecutive columns per lane
-  const int tr4 = 4 * (lane >> 3), tc4 = 4 * (lane & 7);  // 4×4 tile of a 32×32 block
-  for (int p = 0; p < 4; ++p) {
+  // ---- Cholesky and inverse, overlapped.  Wave 0 factors the four 32-column panels (the
+  // pivot chain); the trailing updates run with look-ahead (only the next panel's column
+  // before it, the rest beside it), waves 1–3 store finished column blocks of L while wave 0
+  // factors the next panel and invert the first three diagonal 32×32 blocks under the last
+  // panel.  The inverse is W = L⁻¹ by recursive doubling over the 32-blocks, with the same
+  // products summed in the same order as a level-by-level schedule:
+  //   W_pp = L_pp⁻¹;  W10 = −W11 (L10 W00),  W32 = −W33 (L32 W22);
+  //   T = L21·W11 (64-blocks: T20 = L20 W00 + L21 W10, T21 = L21 W11, T30, T31 alike), stored
+  //   over L21;  W20 = −W22 T20, W21 = −W22 T21, W30 = −(W32 T20 + W33 T30), W31 likewise.
+  // Each 32×32 product is one wave's 4×4-per-lane register tile (tile4x4).
+  // row mapping inside the per-wave 32×32 tiles: 8 rows per wave, 4 consecutive columns per lane
+  const int tr4 = 4 * (lane >> 3), tc4 = 4 * (lane & 7);
+  const bool storeL = !inv_in_place;
+  const bool inv = dinv != nullptr;
+  auto panel = [&](int p) {   // wave 0
     const int c0 = 32 * p;
-    if (wid == 0) {
-      const int r0 = c0 + lane, r1 = c0 + 64 + lane;
-      const bool v0 = r0 < NB, v1 = r1 < NB;
-      // rows past the block read a clamped (valid) row and are never written back
-      double* p0 = S + dsw(v0 ? r0 : NB - 1, c0);
-      double* p1 = S + dsw(v1 ? r1 : NB - 1, c0);
-      double x0[32], x1[32];
+    const int r0 = c0 + lane, r1 = c0 + 64 + lane;
+    const bool v0 = r0 < NB, v1 = r1 < NB;
+    // rows past the block read a clamped (valid) row and are never written back
+    double* p0 = S + dsw(v0 ? r0 : NB - 1, c0);
+    double* p1 = S + dsw(v1 ? r1 : NB - 1, c0);
+    double x0[32], x1[32];
 #pragma unroll
-      for (int c = 0; c < 32; c += 2) {
-        const d2 t0 = *reinterpret_cast<const d2*>(p0 + c);
-        const d2 t1 = *reinterpret_cast<const d2*>(p1 + c);
-        x0[c] = t0.x; x0[c + 1] = t0.y;
-        x1[c] = t1.x; x1[c + 1] = t1.y;
-      }
-      // rows c0+64+lane exist only for the first two panels
-      const int bad = (p < 2) ? panel_steps<true>(std::make_integer_sequence<int, 32>{}, x0, x1, colbuf, lane)
-                              : panel_steps<false>(std::make_integer_sequence<int, 32>{}, x0, x1, colbuf, lane);
-      if (bad && lane == 0 && info) atomicCAS(info, 0, k0 + c0 + bad);
-      if (v0) {
-#pragma unroll
-        for (int c = 0; c < 32; c += 2) *reinterpret_cast<d2*>(p0 + c) = d2{x0[c], x0[c + 1]};
-      }
-      if (v1) {
-#pragma unroll
-        for (int c = 0; c < 32; c += 2) *reinterpret_cast<d2*>(p1 + c) = d2{x1[c], x1[c + 1]};
-      }
+    for (int c = 0; c < 32; c += 2) {
+      const d2 t0 = *reinterpret_cast<const d2*>(p0 + c);
+      const d2 t1 = *reinterpret_cast<const d2*>(p1 + c);
+      x0[c] = t0.x; x0[c + 1] = t0.y;
+      x1[c] = t1.x; x1[c + 1] = t1.y;
     }
-    __syncthreads();
-    GP2D_STAMP(8 + 2 * p);
-    // trailing update of the lower 32×32 blocks (bi, bj), p < bj <= bi < 4: one wave per
-    // block, blocks dealt round-robin to the waves
-    {
-      const int t = 3 - p;  // trailing blocks per side
-      const int nblk = t * (t + 1) / 2;
-      for (int q = wid; q < nblk; q += 4) {
-        // q → (bi, bj) in row-major lower order over the trailing t×t block triangle
-        int bi = 0;
-        while ((bi + 1) * (bi + 2) / 2 <= q) ++bi;
-        const int bj = q - bi * (bi + 1) / 2;
-        const int r = 32 * (p + 1 + bi) + tr4, cc = 32 * (p + 1 + bj) + tc4;
-        double acc[4][4];
-        tile4x4_zero(acc);
-        tile4x4<true>(S, r, c0, c0, cc, acc);
-        tile4x4_store(S, r, cc, acc, -1.0, true);
-      }
+    // rows c0+64+lane exist only for the first two panels
+    const int bad = (p < 2) ? panel_steps<true>(std::make_integer_sequence<int, 32>{}, x0, x1, colbuf, lane)
+                            : panel_steps<false>(std::make_integer_sequence<int, 32>{}, x0, x1, colbuf, lane);
+    if (bad && lane == 0 && info) atomicCAS(info, 0, k0 + c0 + bad);
+    if (v0) {
+#pragma unroll
+      for (int c = 0; c < 32; c += 2) *reinterpret_cast<d2*>(p0 + c) = d2{x0[c], x0[c + 1]};
     }
-    __syncthreads();
-    GP2D_STAMP(9 + 2 * p);
-  }
-  GP2D_STAMP(2);
-  // ---- store L (zero strict upper)
-#pragma unroll 1
-  for (int e = 0; e < (inv_in_place ? 0 : (NB * NB / 2) / 256); ++e) {
-    const int idx = tid + 256 * e, r = idx >> 6, c = 2 * (idx & 63);
-    const d2 v = *reinterpret_cast<const d2*>(S + dsw(r, c));
-    *reinterpret_cast<d2*>(Ab + (int64_t)r * lda + c) = d2{(c <= r) ? v.x : 0.0, (c + 1 <= r) ? v.y : 0.0};
-  }
-  GP2D_STAMP(3);
-  if (!dinv) return;
-  // ---- inverse: 32×32 diagonal blocks, wave w ↔ block w, lane j ↔ column j.  The LDS
-  // diagonal is replaced by its reciprocals first (L is already stored), so each
-  // substitution step is a multiply, not a division.
-  __syncthreads();  // the L store above has read the diagonal
-  if (tid < NB) S[dsw(tid, tid)] = 1.0 / S[dsw(tid, tid)];
-  __syncthreads();
-  GP2D_STAMP(5);
-  {
-    const int b0 = 32 * wid, j = lane & 31;
-    double x[32];
+    if (v1) {
+#pragma unroll
+      for (int c = 0; c < 32; c += 2) *reinterpret_cast<d2*>(p1 + c) = d2{x1[c], x1[c + 1]};
+    }
+  };
+  // A(bi, bj) −= L(bi, p) · L(bj, p)ᵀ  (32-block indices), one wave
+  auto update = [&](int p, int bi, int bj) {
+    double acc[4][4];
+    tile4x4_zero(acc);
+    tile4x4<true>(S, 32 * bi + tr4, 32 * p, 32 * p, 32 * bj + tc4, acc);
+    tile4x4_store(S, 32 * bi + tr4, 32 * bj + tc4, acc, -1.0, true);
+  };
+  // column block cb of L (all 128 rows, zeros above the diagonal) to A, by threads [t0, t0+nt)
+  auto store_colblock = [&](int cb, int t0, int nt) {
+    for (int e = tid - t0; e < NB * 16; e += nt) {
+      const int r = e >> 4, c = 32 * cb + 2 * (e & 15);
+      d2 v = d2{0.0, 0.0};
+      if (r >= 32 * cb) v = *reinterpret_cast<const d2*>(S + dsw(r, c));
+      *reinterpret_cast<d2*>(Ab + (int64_t)r * lda + c) = d2{(c <= r) ? v.x : 0.0, (c + 1 <= r) ? v.y : 0.0};
+    }
+  };
+  // W(q,q) = L(q,q)⁻¹ by forward substitution (lane j ↔ column j), into x; one wave
+  auto diag_inverse = [&](int q, double (&x)[32]) {
+    const int b0 = 32 * q, j = lane & 31;
+    const double rl = 1.0 / S[dsw(b0 + j, b0 + j)];   // lane i: 1 / L_ii
 #pragma unroll
     for (int i = 0; i < 32; ++i) x[i] = (i == j) ? 1.0 : 0.0;
-    inv_steps(std::make_integer_sequence<int, 32>{}, x, S, b0);
-    __builtin_amdgcn_wave_barrier();
+    inv_steps(std::make_integer_sequence<int, 32>{}, x, S, b0, rl);
+  };
+  auto put_diag = [&](int q, const double (&x)[32]) {   // x (lanes 0–31) → S's diagonal block q
+    const int b0 = 32 * q, j = lane & 31;
     if (lane < 32) {
 #pragma unroll
-      for (int i = 0; i < 32; ++i) S[dsw(b0 + i, b0 + j)] = x[i];  // lower part: x[i] = 0 for i < j
+      for (int i = 0; i < 32; ++i) S[dsw(b0 + i, b0 + j)] = x[i];   // x[i] = 0 above the diagonal
     }
-  }
+  };
+  // acc = Σ_{p in [p0, p1]} X(bi, p) · Y(p, bj)  (NN, 32-block indices)
+  auto prod = [&](double (&acc)[4][4], int bi, int bj, int p0, int p1) {
+    tile4x4_zero(acc);
+    for (int p = p0; p <= p1; ++p) tile4x4<false>(S, 32 * bi + tr4, 32 * p, 32 * p, 32 * bj + tc4, acc);
+  };
+  auto put = [&](int bi, int bj, const double (&acc)[4][4], double sgn) {
+    tile4x4_store(S, 32 * bi + tr4, 32 * bj + tc4, acc, sgn, false);
+  };
+
+  // P0
+  if (wid == 0) panel(0);
+  __syncthreads();
+  GP2D_STAMP(2);
+  // U0 on the next panel's column (and (2,2))
+  update(0, wid == 0 ? 2 : wid, wid == 0 ? 2 : 1);
+  __syncthreads();
+  GP2D_STAMP(3);
+  // P1 | U0 on (3,2), (3,3) | L column block 0
+  if (wid == 0) panel(1);
+  else if (wid < 3) update(0, 3, wid + 1);
+  else if (storeL) store_colblock(0, 192, 64);
+  __syncthreads();
+  GP2D_STAMP(4);
+  // U1 on (2,2), (3,2), (3,3)
+  if (wid < 3) update(1, wid == 0 ? 2 : 3, wid == 2 ? 3 : 2);
+  __syncthreads();
+  GP2D_STAMP(5);
+  // P2 | L column block 1
+  if (wid == 0) panel(2);
+  else if (storeL) store_colblock(1, 64, 192);
   __syncthreads();
   GP2D_STAMP(6);
-  // ---- off-diagonal blocks by recursive doubling, W = [[W11, 0], [−W22·L21·W11, W22]]:
-  //   level 1 (32 → 64): wave 0 forms W_10 = −W_11 (L_10 W_00), wave 1 W_32 = −W_33 (L_32 W_22);
-  //   level 2 (64 → 128): T = L21·W11 (wave w ↔ block (2 + w/2, w%2)), stored over L21, then
-  //   W21 = −W22·T.  Each 32×32 product is one wave's 4×4-per-lane register tile.
-  {
-    double acc[4][4];
-    // level 1
-    const int lb = 2 * wid;  // wave 0: blocks (1,0), 1: (3,2)
-    const int r1 = 32 * (lb + 1) + tr4, c1 = 32 * lb + tc4;
-    tile4x4_zero(acc);
-    if (wid < 2) tile4x4<false>(S, r1, 32 * lb, 32 * lb, c1, acc);         // L_{lb+1,lb} W_{lb,lb}
-    __syncthreads();
-    if (wid < 2) tile4x4_store(S, r1, c1, acc, 1.0, false);
-    __syncthreads();
-    tile4x4_zero(acc);
-    if (wid < 2) tile4x4<false>(S, r1, 32 * (lb + 1), 32 * (lb + 1), c1, acc);  // W_{lb+1,lb+1} T
-    __syncthreads();
-    if (wid < 2) tile4x4_store(S, r1, c1, acc, -1.0, false);
-    __syncthreads();
-    // level 2: T_ij = Σ_p L_ip W_pj over p ∈ {0,1} with W_pj = 0 for p < j
-    const int bi = 2 + (wid >> 1), bj = wid & 1;
-    const int r2 = 32 * bi + tr4, c2 = 32 * bj + tc4;
-    tile4x4_zero(acc);
-    for (int p = bj; p < 2; ++p) tile4x4<false>(S, r2, 32 * p, 32 * p, c2, acc);
-    __syncthreads();
-    tile4x4_store(S, r2, c2, acc, 1.0, false);
-    __syncthreads();
-    // W_ij = −Σ_{q=2}^{i} W_iq T_qj
-    tile4x4_zero(acc);
-    for (int q = 2; q <= bi; ++q) tile4x4<false>(S, r2, 32 * q, 32 * q, c2, acc);
-    __syncthreads();
-    tile4x4_store(S, r2, c2, acc, -1.0, false);
-    __syncthreads();
+  if (wid == 0) update(2, 3, 3);
+  __syncthreads();
+  GP2D_STAMP(7);
+  // P3 | W00, W11 | L column block 2, then W22
+  double xd[32];
+  if (wid == 0) {
+    panel(3);
+  } else if (inv) {
+    if (wid == 3 && storeL) store_colblock(2, 192, 64);
+    diag_inverse(wid - 1, xd);
+    put_diag(wid - 1, xd);
+  } else if (storeL) {
+    store_colblock(2, 64, 192);
   }
-  GP2D_STAMP(4);
+  __syncthreads();
+  GP2D_STAMP(8);
+  if (!inv) {
+    if (storeL) store_colblock(3, 0, 256);
+    return;
+  }
+  // B: L column block 3, then W33 (registers) | T10 = L10 W00 → W10 = −W11 T10 | T32 = L32 W22
+  double acc[4][4], acc2[4][4];
+  if (wid == 0) {
+    if (storeL) store_colblock(3, 0, 64);
+    diag_inverse(3, xd);
+  } else if (wid == 1) {
+    prod(acc, 1, 0, 0, 0);
+    put(1, 0, acc, 1.0);
+    prod(acc, 1, 0, 1, 1);
+    put(1, 0, acc, -1.0);
+  } else if (wid == 2) {
+    prod(acc, 3, 2, 2, 2);
+    put(3, 2, acc, 1.0);
+  }
+  __syncthreads();
+  GP2D_STAMP(9);
+  // C: W33 → S, W32 = −W33 T32 | T20 | T21 and T31 | T30   (T kept in registers)
+  if (wid == 0) {
+    put_diag(3, xd);
+    prod(acc, 3, 2, 3, 3);
+    put(3, 2, acc, -1.0);
+  } else if (wid == 1) {
+    prod(acc, 2, 0, 0, 1);
+  } else if (wid == 2) {
+    prod(acc, 2, 1, 1, 1);
+    prod(acc2, 3, 1, 1, 1);
+  } else {
+    prod(acc, 3, 0, 0, 1);
+  }
+  __syncthreads();
+  if (wid == 1) put(2, 0, acc, 1.0);
+  if (wid == 2) { put(2, 1, acc, 1.0); put(3, 1, acc2, 1.0); }
+  if (wid == 3) put(3, 0, acc, 1.0);
+  __syncthreads();
+  GP2D_STAMP(10);
+  // E: W20 = −W22 T20, W21 = −W22 T21, W30 = −(W32 T20 + W33 T30), W31 = −(W32 T21 + W33 T31)
+  const int ebi = 2 + (wid >> 1), ebj = wid & 1;
+  prod(acc, ebi, ebj, 2, ebi);
+  __syncthreads();
+  put(ebi, ebj, acc, -1.0);
+  __syncthreads();
+  GP2D_STAMP(11);
   double* D = dinv + (int64_t)(k0 / NB) * NB * NB;
 #pragma unroll 1
   for (int e = 0; e < (NB * NB / 2) / 256; ++e) {
@@ -413,6 +492,7 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
     *reinterpret_cast<d2*>(D + (int64_t)r * NB + c) = w;
     if (inv_in_place) *reinterpret_cast<d2*>(Ab + (int64_t)r * lda + c) = w;
   }
+  GP2D_STAMP(12);
 }
 
 // Zero the strict upper triangle outside the diagonal blocks.

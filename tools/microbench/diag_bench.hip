@@ -1,5 +1,5 @@
 // Times the 128×128 diagonal-block kernels in isolation (dev tool).
-__device__ unsigned long long g_stamps[16];
+__device__ unsigned long long g_stamps[16];  // slots: see potrf_diag_kernel's GP2D_STAMP calls
 #define GP2D_STAMP(slot) do { if (threadIdx.x == 0) g_stamps[slot] = __builtin_amdgcn_s_memtime(); } while (0)
 #include "../../2d-gp_amd/csrc/factor.hpp"
 #include <cstdio>
@@ -152,8 +152,10 @@ int main() {
   timeit("trti2_diag (inv only)", [&] { trti2_diag_kernel<<<1, 256>>>(A, n, D); });
   potrf_diag_kernel<<<1, 256>>>(A, n, 0, D, info, 0); (void)hipDeviceSynchronize();
   unsigned long long st[16]; (void)hipMemcpyFromSymbol(st, HIP_SYMBOL(g_stamps), sizeof(st));
-  printf("phases (cycles): load %llu, chol %llu, store L %llu, rdiag %llu, diag-inv %llu, offdiag-inv %llu\n", st[1]-st[0], st[2]-st[1], st[3]-st[2], st[5]-st[3], st[6]-st[5], st[4]-st[6]);
-  printf("panels/trailing (cycles):"); for (int p = 0; p < 4; ++p) printf(" p%d %llu/%llu", p, st[8 + 2 * p] - (p ? st[7 + 2 * p] : st[1]), st[9 + 2 * p] - st[8 + 2 * p]); printf("\n");
+  const char* ph[12] = {"load", "P0", "U0", "P1", "U1", "P2", "U2", "P3", "B", "C", "E", "dinv"};
+  printf("phases (cycles):");
+  for (int q = 0; q < 12; ++q) printf(" %s %llu", ph[q], st[q + 1] - st[q]);
+  printf("  total %llu\n", st[12] - st[0]);
   int h; hipMemcpy(&h, info, 4, hipMemcpyDeviceToHost);
   printf("info=%d\n", h);
   return 0;
