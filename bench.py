@@ -103,6 +103,8 @@ def parse():
     a = ap.parse_args()
     if a.config == "B":
         a.kind, a.ntrain, a.grid = "df", 1024, 128
+        if a.fits_ahead is None:   # the 16-block fit outlasts the 128² predict: keep two fits in flight
+            a.fits_ahead = 2
     elif a.config == "C":
         a.kind, a.ntrain, a.grid = "mixed", 4096, 256
     elif a.config == "D":
@@ -545,6 +547,7 @@ def main():
         "roofline": roof,
         "pipelined": cfg["pipeline"],
         "api": api,
+        "fits_ahead": (args.fits_ahead or 1) if api == "engine.krige_jobs" else None,
         "unpipelined": unpiped,
         "single_job": single_job,
         "timed_fits": timed_fits,
