@@ -55,6 +55,13 @@ struct GemmParams {
   // on bi + mask_off == jt the tile stores its lower triangle only.
   int jgrp, jstep;
   int cyc_lower, mask_off;
+  // K split (EPI_STORE, beta = 0): with ksplit > 0 the launch carries 2·zcnt batch entries; a
+  // tile whose K range is longer than ksplit is cut at its middle: entry z < zcnt sums the low
+  // half into C, entry zcnt + z the high half into C2 (leading dimension ldc2, batch stride sC2;
+  // zeros for an uncut tile) — one round of triangular long-K tiles becomes two rounds of
+  // half-length ones; the caller adds C2 into C (add_into_kernel)
+  int ksplit, zcnt;
+  double* C2; int64_t ldc2; int64_t sC2;
 };
 
 __host__ __device__ inline int cyc_tile(const GemmParams& p, int bj) {
@@ -95,15 +102,22 @@ __global__ __launch_bounds__(256, 2) void gemm_f64_kernel(GemmParams p) {
     bj = blockIdx.x;
     bi = p.rev_rows ? (int)(gridDim.y - 1 - blockIdx.y) : (int)blockIdx.y;
   }
-  const int z = blockIdx.z;
+  int z = blockIdx.z;
+  const bool khigh = p.ksplit > 0 && z >= p.zcnt;   // the k ≥ ksplit half of a split product
+  if (khigh) z -= p.zcnt;
   const int jt = cyc_tile(p, bj);
   if (p.cyc_lower && bi + p.mask_off < jt) return;   // strictly above the global diagonal
   const int i0 = bi * GBM, j0 = jt * GBN;
   const double* __restrict__ A = p.A + z * p.sA;
   const double* __restrict__ B = p.B + z * p.sB;
 
-  const int kb = max(p.b_lower ? j0 : 0, p.a_upper ? i0 : 0);
-  const int ke = p.a_lower ? min(p.K, i0 + GBM) : p.K;
+  int kb = max(p.b_lower ? j0 : 0, p.a_upper ? i0 : 0);
+  int ke = p.a_lower ? min(p.K, i0 + GBM) : p.K;
+  if (p.ksplit > 0) {   // tiles longer than ksplit: low half [kb, mid), high half [mid, ke)
+    const int mid = (ke - kb > p.ksplit) ? kb + (((ke - kb) / 2) & ~(GBK - 1)) : ke;
+    if (khigh) kb = mid;
+    else ke = mid;
+  }
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
@@ -181,7 +195,8 @@ __global__ __launch_bounds__(256, 2) void gemm_f64_kernel(GemmParams p) {
   }
 
   if (EPI == EPI_STORE) {
-    double* __restrict__ C = p.C + z * p.sC;
+    double* __restrict__ C = khigh ? p.C2 + z * p.sC2 : p.C + z * p.sC;
+    const int64_t ldc = khigh ? p.ldc2 : p.ldc;
     const bool diag_tile = (p.c_lower && bi == bj) || (p.cyc_lower && bi + p.mask_off == jt);
     const bool has_beta = p.beta != 0.0;
     // per 16-row group: all 16 C loads in flight together, then the updates and stores
@@ -196,7 +211,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f64_kernel(GemmParams p) {
           for (int r = 0; r < 4; ++r) {
             const int row = i0 + wr * 64 + mi * 16 + lk + 4 * r;
             const int col = j0 + wc * 64 + ni * 16 + lr;
-            old[ni][r] = __builtin_nontemporal_load(C + (int64_t)row * p.ldc + col);
+            old[ni][r] = __builtin_nontemporal_load(C + (int64_t)row * ldc + col);
           }
       }
 #pragma unroll
@@ -207,7 +222,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f64_kernel(GemmParams p) {
           const int col = j0 + wc * 64 + ni * 16 + lr;
           double v = p.alpha * acc[mi][ni][r];
           if (has_beta) v = fma(p.beta, old[ni][r], v);
-          if (!(diag_tile && col - j0 > row - i0)) C[(int64_t)row * p.ldc + col] = v;
+          if (!(diag_tile && col - j0 > row - i0)) C[(int64_t)row * ldc + col] = v;
         }
     }
   } else {
@@ -261,8 +276,30 @@ inline int launch_gemm(const GemmParams& p, int batch, hipStream_t s) {
   } else {
     grid = dim3(p.N / GBN, p.M / GBM, batch);
   }
+  if (p.ksplit > 0) {
+    if (EPI != EPI_STORE || p.beta != 0.0 || p.c_lower || p.cyc_lower || p.C2 == nullptr || batch != p.zcnt) {
+      set_error("gemm: K split needs EPI_STORE, beta = 0, no triangle mask, C2 and batch == zcnt");
+      return -2;
+    }
+    grid.z = 2 * batch;
+  }
   gemm_f64_kernel<BT, EPI><<<grid, 256, 0, s>>>(p);
   return check_launch("gemm_f64_kernel");
+}
+
+// C[z] += D[z] over an M×N block per batch entry (row strides ldc / ldd, batch strides sC / sD):
+// the two halves of a K-split product (GemmParams::ksplit), summed in a fixed order.
+__global__ __launch_bounds__(256) void add_into_kernel(double* __restrict__ C, int64_t ldc, int64_t sC,
+                                                       const double* __restrict__ D, int64_t ldd, int64_t sD,
+                                                       int M, int N) {
+  const int z = blockIdx.z;
+  const int row = blockIdx.y;
+  double* c = C + z * sC + (int64_t)row * ldc;
+  const double* d = D + z * sD + (int64_t)row * ldd;
+  for (int j = (blockIdx.x * 256 + threadIdx.x) * 2; j < N; j += gridDim.x * 512) {
+    const d2 a = *reinterpret_cast<const d2*>(c + j), b = *reinterpret_cast<const d2*>(d + j);
+    *reinterpret_cast<d2*>(c + j) = d2{a.x + b.x, a.y + b.y};
+  }
 }
 
 inline GemmParams gemm_params() {

@@ -320,15 +320,48 @@ int launch_panel(double* A, int64_t lda, int k, int64_t n, const double* dinv, h
 // W_kk = L_kk⁻¹): at level g every pair (left = [s·2g, s·2g+g), right = [s·2g+g, s·2g+2g))
 // forms T = L[R, left]·W[left, left], then W[R, left] = −W[R, R]·T — one batched launch per
 // level and product.  T needs (nbk·128/2 + 128)² doubles.
-int trtri_levels(double* A, int64_t lda, int nbk, double* T, hipStream_t s) {
+//
+// The products are triangular in K (T's column block j needs k ≥ j, W21's row block i k ≤ i),
+// so a launch that is a single round of workgroups lasts as long as its longest tile, twice the
+// average: the lower levels ran at 25–33 TF/s.  In a product with at most 256
+// tiles per pair and K ≥ 512, every tile longer than 256 is cut at its middle (GemmParams::
+// ksplit): the low halves go to the destination, the high halves to T2, then add_into_kernel
+// sums them.  The decision
+// depends on the product's shape only, so every caller (gp2d_trtri, both halves of the fused
+// inverse) sums each product in the same order.
+struct TrtriPair { int Ls, Rs, Rn, count; };
+std::vector<TrtriPair> trtri_level_pairs(int nbk, int g) {
+  const int full = nbk / (2 * g);                // pairs whose right part has g blocks
+  const int rem = nbk - full * 2 * g;            // trailing blocks
+  std::vector<TrtriPair> launches;
+  if (full > 0) launches.push_back({0, g, g, full});
+  if (rem > g) launches.push_back({full * 2 * g, full * 2 * g + g, rem - g, 1});
+  return launches;
+}
+// GemmParams::ksplit (tiles with a longer K range are cut in half) for a product with kblocks ×
+// oblocks tiles per pair, 0 = no split
+int trtri_ksplit(int kblocks, int oblocks) {
+  return (kblocks >= 4 && kblocks * oblocks <= 256) ? 2 * NB : 0;
+}
+size_t trtri_split_doubles(int nbk) {   // T2: the largest high half of any split product
+  size_t m = 0;
+  for (int g = 1; g < nbk; g *= 2)
+    for (const TrtriPair& pr : trtri_level_pairs(nbk, g))
+      if (trtri_ksplit(g, pr.Rn) || trtri_ksplit(pr.Rn, g))
+        m = std::max(m, (size_t)pr.count * pr.Rn * NB * g * NB);
+  return m;
+}
+
+int add_into(double* C, int64_t ldc, int64_t sC, const double* D, int64_t ldd, int64_t sD, int M, int N, int count,
+             hipStream_t s) {
+  add_into_kernel<<<dim3((unsigned)((N + 511) / 512), (unsigned)M, (unsigned)count), 256, 0, s>>>(C, ldc, sC, D, ldd,
+                                                                                                  sD, M, N);
+  return check_launch("add_into_kernel");
+}
+
+int trtri_levels(double* A, int64_t lda, int nbk, double* T, double* T2, hipStream_t s) {
   for (int g = 1; g < nbk; g *= 2) {
-    const int full = nbk / (2 * g);                // pairs whose right part has g blocks
-    const int rem = nbk - full * 2 * g;            // trailing blocks
-    struct Pair { int Ls, Rs, Rn, count; };
-    std::vector<Pair> launches;
-    if (full > 0) launches.push_back({0, g, g, full});
-    if (rem > g) launches.push_back({full * 2 * g, full * 2 * g + g, rem - g, 1});
-    for (const Pair& pr : launches) {
+    for (const TrtriPair& pr : trtri_level_pairs(nbk, g)) {
       const int64_t Lo = (int64_t)pr.Ls * NB, Ro = (int64_t)pr.Rs * NB;
       const int bw = g * NB, rh = pr.Rn * NB;
       const int64_t stride = (int64_t)2 * g * NB * (lda + 1);  // next pair's diagonal offset
@@ -339,7 +372,10 @@ int trtri_levels(double* A, int64_t lda, int nbk, double* T, hipStream_t s) {
       p.C = T; p.ldc = bw; p.sC = (int64_t)rh * bw;
       p.M = rh; p.N = bw; p.K = bw; p.b_lower = 1;
       p.cols_first = 1;   // column block j needs k ≥ j: long-K tiles first
+      p.ksplit = trtri_ksplit(g, pr.Rn);
+      if (p.ksplit) { p.zcnt = pr.count; p.C2 = T2; p.ldc2 = bw; p.sC2 = (int64_t)rh * bw; }
       GP2D_CHECK((launch_gemm<false, EPI_STORE>(p, pr.count, s)));
+      if (p.ksplit) GP2D_CHECK(add_into(T, bw, (int64_t)rh * bw, T2, bw, (int64_t)rh * bw, rh, bw, pr.count, s));
       // A[R, L] = −WD · T     WD = A[R, R] (rh × rh lower)
       GemmParams q = gemm_params();
       q.A = A + Ro * lda + Ro; q.lda = lda; q.sA = stride;
@@ -347,7 +383,11 @@ int trtri_levels(double* A, int64_t lda, int nbk, double* T, hipStream_t s) {
       q.C = A + Ro * lda + Lo; q.ldc = lda; q.sC = stride;
       q.M = rh; q.N = bw; q.K = rh; q.a_lower = 1; q.alpha = -1.0;
       q.rev_rows = 1;     // row block i needs k ≤ i: long-K tiles first
+      q.ksplit = trtri_ksplit(pr.Rn, g);
+      if (q.ksplit) { q.zcnt = pr.count; q.C2 = T2; q.ldc2 = bw; q.sC2 = (int64_t)rh * bw; }
       GP2D_CHECK((launch_gemm<false, EPI_STORE>(q, pr.count, s)));
+      if (q.ksplit)
+        GP2D_CHECK(add_into(A + Ro * lda + Lo, lda, stride, T2, bw, (int64_t)rh * bw, rh, bw, pr.count, s));
     }
   }
   return 0;
@@ -364,7 +404,7 @@ size_t trtri_t_doubles(int64_t nbk) { return (size_t)(nbk * NB / 2 + NB) * (size
 // gp2d_potrf + gp2d_trtri.
 int inv_top_split(int nb) { int h = 1; while (2 * h < nb) h *= 2; return h; }
 
-int inv_top_gemm(int kind, double* A, int64_t lda, int nb, double* T2, hipStream_t st) {
+int inv_top_gemm(int kind, double* A, int64_t lda, int nb, double* T2, double* T3, hipStream_t st) {
   const int h = inv_top_split(nb);
   const int64_t Ro = (int64_t)h * NB;
   const int bw = h * NB, rh = (nb - h) * NB;
@@ -375,14 +415,19 @@ int inv_top_gemm(int kind, double* A, int64_t lda, int nb, double* T2, hipStream
     p.C = T2; p.ldc = bw;
     p.M = rh; p.N = bw; p.K = bw; p.b_lower = 1;
     p.cols_first = 1;
+    p.ksplit = trtri_ksplit(h, nb - h);   // as trtri_levels' top level: the same sums
   } else {           // W[R, left] = −W[R, R] · T2
     p.A = A + Ro * lda + Ro; p.lda = lda;
     p.B = T2; p.ldb = bw;
     p.C = A + Ro * lda; p.ldc = lda;
     p.M = rh; p.N = bw; p.K = rh; p.a_lower = 1; p.alpha = -1.0;
     p.rev_rows = 1;
+    p.ksplit = trtri_ksplit(nb - h, h);
   }
-  return launch_gemm<false, EPI_STORE>(p, 1, st);
+  if (p.ksplit) { p.zcnt = 1; p.C2 = T3; p.ldc2 = bw; p.sC2 = (int64_t)rh * bw; }
+  GP2D_CHECK((launch_gemm<false, EPI_STORE>(p, 1, st)));
+  if (p.ksplit) GP2D_CHECK(add_into(p.C, p.ldc, 0, T3, bw, 0, rh, bw, 1, st));
+  return 0;
 }
 }  // namespace
 
@@ -420,6 +465,7 @@ static int potrf_impl(double* A, int64_t n, int64_t lda, double* dinv, int* info
   const int h = fused ? inv_top_split(nb) : 0;
   double* T1 = Tws;                                   // lower levels (one half at a time)
   double* T2 = fused ? Tws + trtri_t_doubles(h) : nullptr;   // top-level T, (nb−h)·128 × h·128
+  double* T3 = fused ? T2 + (size_t)(nb - h) * NB * (size_t)h * NB : nullptr;   // split products' high halves
   // A[j.., j] −= L[j.., p] · L[j, p]ᵀ: block column j receives panel p (skinny K = 128 GEMM,
   // B = the NB rows of block j of the panel)
   auto colupdate = [&](int j, int p, hipStream_t st) -> int {
@@ -438,8 +484,8 @@ static int potrf_impl(double* A, int64_t n, int64_t lda, double* dinv, int* info
     if (fused && nb > 1 && j == h - 1) {   // left half final: W11 and T = L21·W11 under the rest
       GP2D_EV(hipEventRecord((*fc.blk)[0], sc));
       GP2D_EV(hipStreamWaitEvent(si, (*fc.blk)[0], 0));
-      GP2D_CHECK(trtri_levels(A, lda, h, T1, si));
-      GP2D_CHECK(inv_top_gemm(0, A, lda, nb, T2, si));
+      GP2D_CHECK(trtri_levels(A, lda, h, T1, T3, si));
+      GP2D_CHECK(inv_top_gemm(0, A, lda, nb, T2, T3, si));
     }
     return 0;
   };
@@ -490,8 +536,8 @@ static int potrf_impl(double* A, int64_t n, int64_t lda, double* dinv, int* info
     GP2D_EV(hipEventRecord(e_join, sc));
     GP2D_EV(hipStreamWaitEvent(si, e_join, 0));
     double* A22 = A + (int64_t)h * NB * (lda + 1);
-    GP2D_CHECK(trtri_levels(A22, lda, nb - h, T1, si));
-    GP2D_CHECK(inv_top_gemm(1, A, lda, nb, T2, si));
+    GP2D_CHECK(trtri_levels(A22, lda, nb - h, T1, T3, si));
+    GP2D_CHECK(inv_top_gemm(1, A, lda, nb, T2, T3, si));
     GP2D_EV(hipEventRecord(e_join, si));
     GP2D_EV(hipStreamWaitEvent(sc, e_join, 0));
   }
@@ -519,7 +565,8 @@ size_t gp2d_potrf_inv_workspace(int64_t n) {
   const int nb = (int)(n / NB);
   if (nb <= 1) return 0;
   const int h = inv_top_split(nb);
-  return (trtri_t_doubles(h) + (size_t)(nb - h) * NB * (size_t)h * NB) * sizeof(double);
+  return (trtri_t_doubles(h) + (size_t)(nb - h) * NB * (size_t)h * NB +
+          std::max({trtri_split_doubles(h), trtri_split_doubles(nb - h), trtri_split_doubles(nb)})) * sizeof(double);
 }
 
 int gp2d_potrf_inv(double* A, int64_t n, int64_t lda, double* dinv, int* info_dev, void* work, size_t work_bytes,
@@ -532,10 +579,11 @@ int gp2d_potrf_inv(double* A, int64_t n, int64_t lda, double* dinv, int* info_de
 
 // ------------------------------------------------------------------------ TRTRI
 size_t gp2d_trtri_workspace(int64_t n) {
-  // T buffers of the widest level: pairs × (g·NB)² doubles  ≤ n²/4 (+ dinv if not supplied)
+  // T buffers of the widest level: pairs × (g·NB)² doubles  ≤ n²/4 (+ dinv if not supplied,
+  // + the high halves of the K-split products)
   const int64_t nb = n / NB;
   size_t t = (size_t)(n / 2 + NB) * (size_t)(n / 2 + NB) * sizeof(double);
-  return t + (size_t)nb * NB * NB * sizeof(double);
+  return t + (size_t)nb * NB * NB * sizeof(double) + trtri_split_doubles((int)nb) * sizeof(double);
 }
 
 int gp2d_trtri(double* A, int64_t n, int64_t lda, const double* dinv, void* work, size_t work_bytes, void* stream) {
@@ -552,7 +600,7 @@ int gp2d_trtri(double* A, int64_t n, int64_t lda, const double* dinv, void* work
   }
   put_diag_blocks_kernel<<<dim3(NB * NB / 256, nb), 256, 0, s>>>(A, lda, dinv);
   GP2D_CHECK(check_launch("put_diag_blocks_kernel"));
-  return trtri_levels(A, lda, nb, T, s);
+  return trtri_levels(A, lda, nb, T, dwork + (size_t)nb * NB * NB, s);
 }
 
 // ------------------------------------------------------------------------ distributed factor
