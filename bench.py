@@ -486,7 +486,8 @@ def main():
     achieved = kflops / (kms * 1e-3) / 1e12 if kms > 0 else None
     traffic = None   # the committed PMC pass was taken at the headline workload only
     headline = (args.kind, args.ntrain, G, strong) == ("df", 4096, 256, False)
-    pmc_json = args.pmc_json or os.path.join(ROOT, "profiles", f"r02_pmc_traffic_{args.variance}.json")
+    pmc_round = "r03" if args.variance == "ozaki" else "r02"   # the latest PMC pass of each engine
+    pmc_json = args.pmc_json or os.path.join(ROOT, "profiles", f"{pmc_round}_pmc_traffic_{args.variance}.json")
     try:
         with open(pmc_json) as f:
             pmc = json.load(f)
