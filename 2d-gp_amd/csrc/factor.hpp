@@ -367,6 +367,7 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
   };
   // column block cb of L (all 128 rows, zeros above the diagonal) to A, by threads [t0, t0+nt)
   auto store_colblock = [&](int cb, int t0, int nt) {
+    if (tid < t0 || tid >= t0 + nt) return;
     for (int e = tid - t0; e < NB * 16; e += nt) {
       const int r = e >> 4, c = 32 * cb + 2 * (e & 15);
       d2 v = d2{0.0, 0.0};

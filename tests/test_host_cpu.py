@@ -245,3 +245,24 @@ def test_ozaki_epilogue_reduction_exact():
     for K, m in [(8192, 251), (32768, 193), (131071, 197)]:
         bias = ((K << 14) + m - 1) // m * m
         assert bias % m == 0 and bias - (K << 14) >= 0 and bias + (K << 14) < (1 << 32)
+
+
+def test_factor_workspaces_cover_the_split_trtri():
+    """gp2d_trtri / gp2d_potrf_inv workspaces (host functions, no device needed) include room
+    for the high halves of the K-split TRTRI products (the lower levels' products with at most
+    256 tiles per pair) on top of the T buffers, and grow with n."""
+    from gp2d import _native as N
+    L = N.lib()
+    nb_ = 128
+    prev_t = prev_f = 0
+    for n in (128, 256, 640, 1024, 2048, 4096, 8192, 16384, 32768):
+        nb = n // nb_
+        t_base = (n // 2 + nb_) ** 2 * 8 + nb * nb_ * nb_ * 8
+        t = int(L.gp2d_trtri_workspace(n))
+        assert t >= t_base
+        if nb >= 8:   # a level with g >= 4 exists: its products are split
+            assert t > t_base, n
+        f = int(L.gp2d_potrf_inv_workspace(n))
+        assert t >= prev_t and f >= prev_f
+        prev_t, prev_f = t, f
+    assert int(L.gp2d_potrf_inv_workspace(128)) == 0
