@@ -601,10 +601,15 @@ def krige_jobs(jobs, variance: str = "ozaki", chunk: int = 8192, var_mode: str =
 
     fits_ahead = k > 1: up to k fits in flight on k side streams, each queued before the
     predict stream waits for the job ahead of it, so consecutive fits also overlap each other
-    (gp2d_potrf draws a separate internal stream set per call) — for small jobs whose
-    latency-bound fit is longer than their predict (config B)."""
+    (gp2d_potrf draws a separate internal stream set per call).  fits_ahead = 0: each job's fit
+    and predict strictly one after the other on the current stream — the fastest form for small
+    jobs whose latency-bound fit outlasts their predict (config B: a fit beside a predict runs
+    ≈ 2.4× longer)."""
     dev = _require_device(device)
     main = torch.cuda.current_stream(dev)
+    if int(fits_ahead) <= 0:
+        yield from _krige_jobs_serial(jobs, variance, chunk, var_mode, compute_var, jitter, dev, stats)
+        return
     k = max(1, int(fits_ahead))
     sides = [side_stream(dev) for _ in range(k)]
     prev_sets = N.lib().gp2d_factor_sets(k) if k > 1 else None   # one internal factor set per side stream
@@ -649,6 +654,20 @@ def krige_jobs(jobs, variance: str = "ozaki", chunk: int = 8192, var_mode: str =
     finally:
         if prev_sets is not None:
             N.lib().gp2d_factor_sets(prev_sets)
+
+
+def _krige_jobs_serial(jobs, variance, chunk, var_mode, compute_var, jitter, dev, stats):
+    pred = None
+    for job in jobs:
+        kernel, x, y, noise, xg = job
+        note_fit_issued(stats)
+        gp = fit(kernel, x, y, noise, jitter=jitter, device=dev, variance=variance, check=False)
+        if pred is None or not pred.fits(gp):
+            pred = Predictor(gp, chunk)
+        pred.gp = gp
+        out = pred(xg, var_mode=var_mode, compute_var=compute_var)
+        gp.check()
+        yield out
 
 
 # ------------------------------------------------------------------ hyperparameters

@@ -95,7 +95,8 @@ def parse():
     ap.add_argument("--cpu-sample-points", type=int, default=2048)
     ap.add_argument("--pmc-json", default=None)
     ap.add_argument("--fits-ahead", type=int, default=None,
-                    help="N=1 job stream: fits in flight (engine.krige_jobs fits_ahead; default 1, config B 2)")
+                    help="N=1 job stream: fits in flight (engine.krige_jobs fits_ahead; default 1, config B 0 = "
+                         "each job's fit and predict back to back)")
     ap.add_argument("--sweep-concurrent", type=int, default=None,
                     help="config E: settings whose fit + LML chains run concurrently (hyper.sweep concurrent)")
     ap.add_argument("--single-job-dist", type=int, default=0,
@@ -103,8 +104,8 @@ def parse():
     a = ap.parse_args()
     if a.config == "B":
         a.kind, a.ntrain, a.grid = "df", 1024, 128
-        if a.fits_ahead is None:   # the 16-block fit outlasts the 128² predict: keep two fits in flight
-            a.fits_ahead = 2
+        if a.fits_ahead is None:   # the 16-block fit outlasts the 128² predict: jobs back to back
+            a.fits_ahead = 0
     elif a.config == "C":
         a.kind, a.ntrain, a.grid = "mixed", 4096, 256
     elif a.config == "D":
@@ -401,7 +402,7 @@ def main():
 
         def stream(k):   # the shipped API for a sweep of jobs
             return E.krige_jobs(itertools.repeat(job, k), variance=args.variance, chunk=args.chunk, stats=stats,
-                                fits_ahead=args.fits_ahead or 1)
+                                fits_ahead=1 if args.fits_ahead is None else args.fits_ahead)
         api = "engine.krige_jobs"
     trace = os.environ.get("GP2D_BENCH_TRACE") == "1"   # per-step wall times on stderr (diagnostics)
 
@@ -548,7 +549,7 @@ def main():
         "roofline": roof,
         "pipelined": cfg["pipeline"],
         "api": api,
-        "fits_ahead": (args.fits_ahead or 1) if api == "engine.krige_jobs" else None,
+        "fits_ahead": (1 if args.fits_ahead is None else args.fits_ahead) if api == "engine.krige_jobs" else None,
         "unpipelined": unpiped,
         "single_job": single_job,
         "timed_fits": timed_fits,

@@ -29,10 +29,11 @@ JOBS = [(1, 700, 60, "df"), (2, 700, 64, "mixed"), (3, 1500, 50, "df"), (4, 300,
         (5, 1500, 72, "mixed"), (6, 1500, 72, "df")]
 
 
-@pytest.mark.parametrize("variance,ahead", [("ozaki", 1), ("f64", 1), ("ozaki", 2), ("ozaki", 3)])
+@pytest.mark.parametrize("variance,ahead", [("ozaki", 1), ("f64", 1), ("ozaki", 2), ("ozaki", 3), ("ozaki", 0)])
 def test_krige_jobs_bit_identical_to_sequential(variance, ahead):
     """fits_ahead > 1: consecutive fits in flight together, each drawing its own internal
-    factor stream set — still the bits of one job at a time."""
+    factor stream set; fits_ahead = 0: back to back on one stream — still the bits of one job
+    at a time."""
     jobs = [_job(*j) for j in JOBS]
     got = [(m.clone(), v.clone()) for m, v in E.krige_jobs(jobs, variance=variance, chunk=2048, fits_ahead=ahead)]
     assert len(got) == len(jobs)
@@ -42,7 +43,7 @@ def test_krige_jobs_bit_identical_to_sequential(variance, ahead):
         assert torch.equal(m, rm) and torch.equal(v, rv)
 
 
-@pytest.mark.parametrize("ahead", [1, 2])
+@pytest.mark.parametrize("ahead", [0, 1, 2])
 def test_krige_jobs_non_spd_raises_at_its_job(ahead):
     jobs = [_job(1, 500, 40, "df"), _job(2, 500, 40, "df", noise=-100.0), _job(3, 500, 40, "df")]
     gen = E.krige_jobs(jobs, variance="ozaki", chunk=1024, fits_ahead=ahead)
