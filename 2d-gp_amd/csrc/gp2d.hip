@@ -239,6 +239,7 @@ struct FactorSet {
 constexpr int GP2D_FACTOR_CTX = 4;
 FactorStreams g_fs;
 std::atomic<int> g_factor_sets{1};   // sets in use (gp2d_factor_sets); 1: every caller shares one
+thread_local int t_factor_join = 0;   // gp2d_factor_join: this thread's factorisations join on the host
 
 struct FactorCtx {
   hipStream_t crit, bulk, aux, inv;
@@ -542,6 +543,12 @@ static int potrf_impl(double* A, int64_t n, int64_t lda, double* dinv, int* info
     GP2D_EV(hipStreamWaitEvent(sc, e_join, 0));
   }
   GP2D_EV(hipEventRecord(e_join, sc));
+  // The caller's wait below stays pending for the whole chain.  A pending wait on a hardware
+  // queue that the CP services beside crit's, aux's or bulk's slows the chain's dispatches:
+  // a 4096-point fit took 13.4 ms with the caller on the null stream and 15.8–19 ms on
+  // torch's pool streams (tools/probe_single_job.py, profiles/r03_caller_join.txt).  With
+  // gp2d_factor_join(1) the host waits for the chain first, so the wait is enqueued complete.
+  if (t_factor_join) GP2D_EV(hipEventSynchronize(e_join));
   GP2D_EV(hipStreamWaitEvent(s, e_join, 0));
   dim3 zg((unsigned)((n / 2 + 255) / 256), (unsigned)n);
   zero_upper_kernel<<<zg, 256, 0, s>>>(A, n, lda);
@@ -554,6 +561,12 @@ size_t gp2d_potrf_workspace(int64_t) { return 0; }
 int gp2d_factor_sets(int k) {
   const int prev = g_factor_sets.load();
   if (k >= 1) g_factor_sets.store(std::min(k, GP2D_FACTOR_CTX));
+  return prev;
+}
+
+int gp2d_factor_join(int host) {
+  const int prev = t_factor_join;
+  if (host >= 0) t_factor_join = host != 0;
   return prev;
 }
 

@@ -269,7 +269,7 @@ def pending_status(status: torch.Tensor, err=None) -> tuple:
 
 
 def fit(kernel: KernelSpec, x, y, noise: float, jitter: float = 0.0, device=None, variance: str = "f64",
-        check: bool = True, jitchol: int = 0) -> GPFit:
+        check: bool = True, jitchol: int = 0, join: bool | None = None) -> GPFit:
     """K_y = K(x,x) + (noise+jitter)·I → L = chol(K_y) → W = L⁻¹ → α = Wᵀ W y.
 
     jitchol = k > 0: GPy's jitchol retry (GPy.util.linalg.jitchol, maxtries = k; GPy is not
@@ -284,6 +284,13 @@ def fit(kernel: KernelSpec, x, y, noise: float, jitter: float = 0.0, device=None
     Raises numpy.linalg.LinAlgError if K_y is not positive definite (the
     reference's np.linalg.inv / GPy jitchol / sklearn error paths).  check=False returns
     without waiting for the factor (no host sync); the error is raised by GPFit.check().
+
+    join (default: = check): the host waits for the factorisation's chain before it enqueues
+    the rest of the fit (gp2d_factor_join), so the current stream holds no wait pending beside
+    the chain — a pending wait on some of torch's streams slows the chain by up to 40 %
+    (DESIGN.md §6).  It costs nothing when the caller blocks on the result anyway; join=False
+    keeps a check=False fit fully asynchronous, join=True blocks one that has nothing to
+    overlap (a job stream's first fit).
     """
     if jitchol:
         try:
@@ -332,12 +339,18 @@ def fit(kernel: KernelSpec, x, y, noise: float, jitter: float = 0.0, device=None
                             _ptr(A), n, s), "gp2d_assemble")
     dinv = torch.empty((n // NB, NB, NB), dtype=torch.float64, device=dev)
     info = torch.zeros(1, dtype=torch.int32, device=dev)
-    if FUSED_INVERSE:   # factor and inverse in one call, the TRTRI GEMMs overlapped with POTRF
-        wbytes = int(L.gp2d_potrf_inv_workspace(n))
-        work = torch.empty(wbytes // 8 + 1, dtype=torch.float64, device=dev)
-        N.check(L.gp2d_potrf_inv(_ptr(A), n, n, _ptr(dinv), _ptr(info), _ptr(work), wbytes, s), "gp2d_potrf_inv")
-    else:
-        N.check(L.gp2d_potrf(_ptr(A), n, n, _ptr(dinv), _ptr(info), None, 0, s), "gp2d_potrf")
+    prev_join = L.gp2d_factor_join(1 if (check if join is None else join) else 0)
+    try:
+        if FUSED_INVERSE:   # factor and inverse in one call, the TRTRI GEMMs overlapped with POTRF
+            wbytes = int(L.gp2d_potrf_inv_workspace(n))
+            work = torch.empty(wbytes // 8 + 1, dtype=torch.float64, device=dev)
+            N.check(L.gp2d_potrf_inv(_ptr(A), n, n, _ptr(dinv), _ptr(info), _ptr(work), wbytes, s),
+                    "gp2d_potrf_inv")
+        else:
+            N.check(L.gp2d_potrf(_ptr(A), n, n, _ptr(dinv), _ptr(info), None, 0, s), "gp2d_potrf")
+    finally:
+        L.gp2d_factor_join(prev_join)
+    if not FUSED_INVERSE:
         wbytes = int(L.gp2d_trtri_workspace(n))
         work = torch.empty(wbytes // 8 + 1, dtype=torch.float64, device=dev)
         N.check(L.gp2d_trtri(_ptr(A), n, n, _ptr(dinv), _ptr(work), wbytes, s), "gp2d_trtri")
@@ -618,11 +631,15 @@ def krige_jobs(jobs, variance: str = "ozaki", chunk: int = 8192, var_mode: str =
     def queue_fit(job):
         kernel, x, y, noise, _ = job
         side = sides[issued[0] % k]
+        # one fit in flight: the first has no predict to overlap, so it joins on the host (no
+        # wait left pending on the side stream beside its chain, fit(join=...))
+        join = k == 1 and issued[0] == 0
         issued[0] += 1
         side.wait_stream(main)
         note_fit_issued(stats)
         with torch.cuda.stream(side):
-            return side, fit(kernel, x, y, noise, jitter=jitter, device=dev, variance=variance, check=False)
+            return side, fit(kernel, x, y, noise, jitter=jitter, device=dev, variance=variance, check=False,
+                             join=join)
 
     it = iter(jobs)
     queue = collections.deque()   # (job, side stream, gp) with the fit queued

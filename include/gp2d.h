@@ -97,6 +97,13 @@ int gp2d_assemble(const double* xa, int64_t na, int64_t na_pad,
  * streams run concurrently, their latency-bound chains interleaved (engine.krige_jobs
  * fits_ahead).  Each set's enqueue is serialised by its own lock (thread-safe).     */
 int gp2d_factor_sets(int k);
+/* gp2d_factor_join(1): this thread's later gp2d_potrf / gp2d_potrf_inv calls wait on the
+ * host for the factorisation's chain before they enqueue the caller stream's join, so the
+ * caller's hardware queue holds no pending wait while the chain runs (a pending wait there
+ * slows the chain by up to 40 %).  For callers that block on the result
+ * anyway (a synchronous fit, a job stream's first fit); 0 (default) keeps the calls
+ * asynchronous.  A negative argument only queries; returns the previous mode.          */
+int gp2d_factor_join(int host);
 size_t gp2d_potrf_workspace(int64_t n);
 int gp2d_potrf(double* A, int64_t n, int64_t lda, double* dinv, int* info_dev,
                void* work, size_t work_bytes, void* stream);

@@ -55,3 +55,23 @@ def test_krige_jobs_non_spd_raises_at_its_job(ahead):
 
 def test_krige_jobs_empty():
     assert list(E.krige_jobs([])) == []
+
+
+@pytest.mark.parametrize("join", [False, True])
+def test_fit_join_modes_same_bits_on_a_side_stream(join):
+    """fit(join=...) only moves the host wait (gp2d_factor_join): W, α and the predictions are
+    the bits of the default synchronous fit, and the mode is restored after the call."""
+    spec, x, y, noise, xg = _job(7, 900, 48, "mixed")
+    ref = E.fit(spec, x, y, noise, variance="ozaki")
+    rm, rv = E.Predictor(ref, 2048)(xg)
+    side = E.side_stream(x.device)
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        gp = E.fit(spec, x, y, noise, variance="ozaki", check=False, join=join)
+        m, v = E.Predictor(gp, 2048)(xg)
+    torch.cuda.current_stream().wait_stream(side)
+    gp.check()
+    torch.cuda.synchronize()
+    assert E.N.lib().gp2d_factor_join(-1) == 0
+    assert torch.equal(gp.W, ref.W) and torch.equal(gp.alpha, ref.alpha)
+    assert torch.equal(m, rm) and torch.equal(v, rv)

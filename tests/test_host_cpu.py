@@ -266,3 +266,22 @@ def test_factor_workspaces_cover_the_split_trtri():
         assert t >= prev_t and f >= prev_f
         prev_t, prev_f = t, f
     assert int(L.gp2d_potrf_inv_workspace(128)) == 0
+
+
+def test_factor_join_mode_is_per_thread_and_restorable():
+    """gp2d_factor_join (host state only, no device needed): a negative argument queries, the
+    previous mode is returned, and the mode belongs to the calling thread (engine.fit sets and
+    restores it around one factorisation)."""
+    import threading
+    from gp2d import _native as N
+    L = N.lib()
+    assert L.gp2d_factor_join(-1) == 0
+    assert L.gp2d_factor_join(1) == 0
+    assert L.gp2d_factor_join(-1) == 1
+    seen = []
+    t = threading.Thread(target=lambda: seen.append(L.gp2d_factor_join(-1)))
+    t.start()
+    t.join()
+    assert seen == [0]
+    assert L.gp2d_factor_join(0) == 1
+    assert L.gp2d_factor_join(-1) == 0
