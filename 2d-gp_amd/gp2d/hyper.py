@@ -202,10 +202,11 @@ def sweep(kernel: E.KernelSpec, x, y, settings, noise: float = None, jitter: flo
     settings are dealt round-robin over ranks and the results all-reduced (bit-identical to
     one rank).  Returns (lml[S], grad[S, P] or None); a non-PD setting gives -inf.
 
-    concurrent = c > 1: the settings' fit + LML (+ gradient) chains are queued on c streams
-    with no host round trip (engine.fit(check=False), engine.lml_device), so the latency-bound
-    factorisations of c settings interleave on the GPU (each draws its own internal stream
-    set); results are read back 2c settings behind.  Same kernels, same bits as c = 1."""
+    concurrent = c > 1: the settings' fit + LML (+ gradient) are queued on c streams with no
+    host round trip for the results (engine.fit(check=False), engine.lml_device), read back 2c
+    settings behind; each fit joins its chain on the host (fit(join=True)), so setting i's LML
+    and gradient run under setting i+1's factorisation (config E: 60.8–61.2 vs 58.3–59.2
+    settings/s at c = 1; without the join, 41.9).  Same kernels, same bits as c = 1."""
     ws, rank = (dist.get_world_size(), dist.get_rank()) if dist.is_available() and dist.is_initialized() else (1, 0)
     base = get_params(kernel, noise if noise is not None else 0.0)
     S = len(settings)
@@ -256,7 +257,10 @@ def sweep(kernel: E.KernelSpec, x, y, settings, noise: float = None, jitter: flo
             st = streams[j % c]
             st.wait_stream(main)
             with torch.cuda.stream(st):
-                gp = E.fit(k, x, y, nz, jitter=jitter, device=dev, check=False)
+                # joined on the host: the chain never runs with this stream's wait pending
+                # beside it (≈ 40 % slower); what overlaps is the previous
+                # setting's LML + gradient under this setting's chain
+                gp = E.fit(k, x, y, nz, jitter=jitter, device=dev, check=False, join=True)
                 out, g = E.lml_device(gp, eval_gradient)
                 ev = torch.cuda.Event()
                 ev.record(st)

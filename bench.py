@@ -98,7 +98,8 @@ def parse():
                     help="N=1 job stream: fits in flight (engine.krige_jobs fits_ahead; default 1, config B 0 = "
                          "each job's fit and predict back to back)")
     ap.add_argument("--sweep-concurrent", type=int, default=None,
-                    help="config E: settings whose fit + LML chains run concurrently (hyper.sweep concurrent)")
+                    help="config E: streams the settings' fit + LML are queued on (hyper.sweep concurrent; "
+                         "default 2: each setting's LML + gradient under the next setting's fit)")
     ap.add_argument("--single-job-dist", type=int, default=0,
                     help="also time one job with distributed.fit_distributed at N = 1 (always at N > 1)")
     a = ap.parse_args()
@@ -183,7 +184,8 @@ def run_sweep(args, ws, rank, dev):
     settings = config_e_settings()
     ks = E.KernelSpec(kind="df", l_df=5.0)
 
-    conc = args.sweep_concurrent or 1
+    # two streams: each setting's LML + gradient under the next setting's (host-joined) fit
+    conc = args.sweep_concurrent or 2
 
     def sweep():
         return H.sweep(ks, xt, yt, settings, noise=0.0025, eval_gradient=True, device=dev, concurrent=conc)
@@ -212,7 +214,8 @@ def run_sweep(args, ws, rank, dev):
             "data": "synthetic (seeded drifter field, SURVEY.md §8d)",
             "config": {"workload": f"BASELINE config E: 64 (l_df, noise) settings x N_train={args.ntrain}, "
                                    f"div-free, LML + exact gradient per setting, settings dealt over {ws} GPU(s)",
-                       "n_train": args.ntrain, "settings": len(settings), "parallelism": f"settings round robin x{ws}"},
+                       "n_train": args.ntrain, "settings": len(settings), "parallelism": f"settings round robin x{ws}",
+                       "sweep_concurrent": conc},
             "roofline": {"bound": "mfma", "achieved": per_gpu, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": per_gpu / FP64_PEAK_TFLOPS, "traffic": None,
                          "kernel": "whole sweep per GPU: POTRF + TRTRI + W^T W (n^3 FP64 flop per setting) / wall time"},

@@ -210,7 +210,7 @@ def test_optimize_restarts_mixed_and_fix():
     assert fixed.kernel.ratio == 0.5 and fixed.noise == 0.02
 
 
-@pytest.mark.parametrize("concurrent", [1, 3])
+@pytest.mark.parametrize("concurrent", [1, 2, 3])
 def test_sweep_matches_individual_fits(concurrent):
     """concurrent > 1 queues several settings' fit + LML chains on separate streams with no host
     round trip; a non-PD setting still gives -inf (the last setting's negative noise)."""
