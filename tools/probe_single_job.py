@@ -26,6 +26,7 @@ xg = torch.tensor(D.bbox_grid(x1, x2, G, pad=5.0)[2], device="cuda")
 spec = E.KernelSpec(kind="df", l_df=5.0)
 job = (spec, xt, yt, 0.0025, xg)
 main = torch.cuda.current_stream()
+E.FUSED_INVERSE = os.environ.get("PROBE_FUSED") == "1"   # gp2d_potrf_inv instead of potrf + trtri
 side = E.side_stream(xt.device)
 pred = [None]
 
