@@ -46,6 +46,10 @@ struct GemmParams {
   int rev_rows;  // dispatch heavy (large i0) row blocks first (a_lower)
   int xcd_cols;  // 1-D grid: groups of 8 column tiles × all row blocks, column tile = XCD label
   int cols_first;  // 1-D grid, column blocks slow and ascending: heavy-first order for b_lower
+  // stagger > 0 (equal-K tiles, the POTRF SYRK): blocks [256, 512) — the second workgroup of
+  // each CU in the first round — first sleep stagger × 8128 cycles, so the two workgroups of
+  // a CU reach their C read-modify-write at different times instead of all 512 at once
+  int stagger;
   double* P; int64_t ldp; int64_t sP;         // EPI_COLSQ partials [M/BM][N]
   // Block-cyclic column tiles (the distributed factor, dfact.hpp): with jgrp > 0, column tile
   // bj sits jt = (bj / jgrp)·jgrp·jstep + bj % jgrp tiles from C's (and op(B)'s) first column
@@ -102,6 +106,8 @@ __global__ __launch_bounds__(256, 2) void gemm_f64_kernel(GemmParams p) {
     bj = blockIdx.x;
     bi = p.rev_rows ? (int)(gridDim.y - 1 - blockIdx.y) : (int)blockIdx.y;
   }
+  if (p.stagger && blockIdx.x >= 256 && blockIdx.x < 512)
+    for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(127);
   int z = blockIdx.z;
   const bool khigh = p.ksplit > 0 && z >= p.zcnt;   // the k ≥ ksplit half of a split product
   if (khigh) z -= p.zcnt;
@@ -199,21 +205,21 @@ __global__ __launch_bounds__(256, 2) void gemm_f64_kernel(GemmParams p) {
     const int64_t ldc = khigh ? p.ldc2 : p.ldc;
     const bool diag_tile = (p.c_lower && bi == bj) || (p.cyc_lower && bi + p.mask_off == jt);
     const bool has_beta = p.beta != 0.0;
-    // per 16-row group: all 16 C loads in flight together, then the updates and stores
-    // (element-wise load → use → store chains leave one HBM round trip per element)
+    // per 16-row group mi: 16 C loads, then the updates and stores (element-wise load → use →
+    // store chains leave one HBM round trip per element).  GP2D_EPI_PIPE (the default) issues
+    // group mi+1's loads before group mi's updates, so a tile's C read costs one exposed round
+    // trip instead of four; the per-element arithmetic is the same.
+    auto cload = [&](int mi, double (&old)[4][4]) {
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi) {
-      double old[4][4];
-      if (has_beta) {
+      for (int ni = 0; ni < 4; ++ni)
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int row = i0 + wr * 64 + mi * 16 + lk + 4 * r;
-            const int col = j0 + wc * 64 + ni * 16 + lr;
-            old[ni][r] = __builtin_nontemporal_load(C + (int64_t)row * ldc + col);
-          }
-      }
+        for (int r = 0; r < 4; ++r) {
+          const int row = i0 + wr * 64 + mi * 16 + lk + 4 * r;
+          const int col = j0 + wc * 64 + ni * 16 + lr;
+          old[ni][r] = __builtin_nontemporal_load(C + (int64_t)row * ldc + col);
+        }
+    };
+    auto cstore = [&](int mi, const double (&old)[4][4]) {
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni)
 #pragma unroll
@@ -224,6 +230,27 @@ __global__ __launch_bounds__(256, 2) void gemm_f64_kernel(GemmParams p) {
           if (has_beta) v = fma(p.beta, old[ni][r], v);
           if (!(diag_tile && col - j0 > row - i0)) C[(int64_t)row * ldc + col] = v;
         }
+    };
+#ifndef GP2D_EPI_PIPE
+#define GP2D_EPI_PIPE 1
+#endif
+    if (GP2D_EPI_PIPE && has_beta) {
+      double o0[4][4], o1[4][4];
+      cload(0, o0);
+      cload(1, o1);
+      cstore(0, o0);
+      cload(2, o0);
+      cstore(1, o1);
+      cload(3, o1);
+      cstore(2, o0);
+      cstore(3, o1);
+    } else {
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        double old[4][4];
+        if (has_beta) cload(mi, old);
+        cstore(mi, old);
+      }
     }
   } else {
     // column sums of squares of this 128-row slab of V, combined in a fixed order:
