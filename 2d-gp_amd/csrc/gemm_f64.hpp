@@ -46,10 +46,6 @@ struct GemmParams {
   int rev_rows;  // dispatch heavy (large i0) row blocks first (a_lower)
   int xcd_cols;  // 1-D grid: groups of 8 column tiles × all row blocks, column tile = XCD label
   int cols_first;  // 1-D grid, column blocks slow and ascending: heavy-first order for b_lower
-  // stagger > 0 (equal-K tiles, the POTRF SYRK): blocks [256, 512) — the second workgroup of
-  // each CU in the first round — first sleep stagger × 8128 cycles, so the two workgroups of
-  // a CU reach their C read-modify-write at different times instead of all 512 at once
-  int stagger;
   double* P; int64_t ldp; int64_t sP;         // EPI_COLSQ partials [M/BM][N]
   // Block-cyclic column tiles (the distributed factor, dfact.hpp): with jgrp > 0, column tile
   // bj sits jt = (bj / jgrp)·jgrp·jstep + bj % jgrp tiles from C's (and op(B)'s) first column
@@ -106,8 +102,6 @@ __global__ __launch_bounds__(256, 2) void gemm_f64_kernel(GemmParams p) {
     bj = blockIdx.x;
     bi = p.rev_rows ? (int)(gridDim.y - 1 - blockIdx.y) : (int)blockIdx.y;
   }
-  if (p.stagger && blockIdx.x >= 256 && blockIdx.x < 512)
-    for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(127);
   int z = blockIdx.z;
   const bool khigh = p.ksplit > 0 && z >= p.zcnt;   // the k ≥ ksplit half of a split product
   if (khigh) z -= p.zcnt;

@@ -28,9 +28,6 @@ int main() {
     GemmParams q = gemm_params();
     q.A = dA; q.lda = ld; q.B = dA; q.ldb = ld; q.C = dC; q.ldc = ld;
     q.M = m; q.N = m; q.K = K; q.alpha = -1.0; q.beta = 1.0; q.c_lower = 1;
-#ifdef SYRK_STAGGER
-    q.stagger = SYRK_STAGGER;
-#endif
     hipEvent_t e0, e1; (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
     (void)SYRK_LAUNCH(q, 0);
     (void)hipMemcpy(dC, C.data(), C.size() * 8, hipMemcpyHostToDevice);
