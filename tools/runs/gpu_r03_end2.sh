@@ -14,3 +14,6 @@ cp "$(find $R/exact -name '*kernel_stats.csv' | head -n 1)" $R/kernel_stats.csv
 rm -rf $R/exact
 timeout -k 10 240 python -u tools/probe_fit.py 4096 16384 > $R/fit.txt 2>&1 || exit 1
 grep -v amdgpu.ids $R/fit.txt
+# the K = 256 SYRK alone under PMC (clock, MFMA busy, wave states)
+timeout -k 10 300 bash tools/microbench/pmc_syrk.sh > $R/pmc_syrk.txt 2>&1 || { tail -20 $R/pmc_syrk.txt; exit 1; }
+cat $R/pmc_syrk.txt
