@@ -560,8 +560,28 @@ size_t gp2d_potrf_workspace(int64_t) { return 0; }
 
 int gp2d_factor_sets(int k) {
   const int prev = g_factor_sets.load();
-  if (k >= 1) g_factor_sets.store(std::min(k, GP2D_FACTOR_CTX));
+  if (k >= 1) {
+    std::lock_guard<std::mutex> lk(g_fs.mu);
+    g_factor_sets.store(std::min(k, GP2D_FACTOR_CTX));
+    // a new batch of concurrent factorisations: forget which caller stream had which set, so
+    // the next k caller streams are dealt sets 0..k−1 in order of first use (torch's stream
+    // pools hand the same streams out again; a remembered mapping could put two streams of
+    // one batch on the same set, where their chains would queue behind each other)
+    if (k > 1)
+      for (auto& own : g_fs.owner) own.clear();
+  }
   return prev;
+}
+
+int gp2d_factor_set_of(void* stream) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return -1;
+  std::lock_guard<std::mutex> lk(g_fs.mu);
+  if ((int)g_fs.owner.size() <= dev) return -1;
+  const int want = std::max(1, std::min(GP2D_FACTOR_CTX, g_factor_sets.load()));
+  for (const auto& pr : g_fs.owner[dev])
+    if (pr.first == S(stream)) return pr.second < want ? pr.second : -1;
+  return -1;
 }
 
 int gp2d_factor_join(int host) {

@@ -76,12 +76,15 @@ def broadcast_fit(gp: E.GPFit | None, spec: E.KernelSpec, noise: float, x, devic
     else:
         n, ntr, npad = (int(v) for v in layout)
         status = torch.full((1,), -1, dtype=torch.int32, device=dev)
-        if rank == src and error is None and gp is not None:
+        prep_err = gp.pending[2] if (gp is not None and gp.pending is not None) else None
+        if rank == src and error is None and gp is not None and prep_err is None:
             info = gp.extra.get("info_dev")
             if info is not None:
                 status.copy_(info)
             else:
                 status.zero_()
+        # an error the owner's fit deferred to check() (a failed int8 preparation) keeps the
+        # status at −1: the receivers raise at this job too instead of yielding it
         dist.broadcast(status, src)
     packed = torch.empty(_packed_len(n), dtype=torch.float64, device=dev)
     if rank == src and gp is not None and error is None:
@@ -280,7 +283,7 @@ def fit_distributed(spec: E.KernelSpec, x, y, noise: float, device=None, varianc
     t1 = time.perf_counter()
     if not _solo(ws) and emulate is None:
         _allgather_w_columns(A, n, ws, rank, dev)
-        dist.all_reduce(info, op=dist.ReduceOp.MAX)
+        allreduce_first_failure(info)
     E.N.check(L.gp2d_zero_upper(P(A), n, n, sh), "gp2d_zero_upper")
     t2 = time.perf_counter()
     Y = E._pad_obs(y, ntr, npad, bd, dev)
@@ -302,6 +305,18 @@ def fit_distributed(spec: E.KernelSpec, x, y, noise: float, device=None, varianc
     if stats is not None:
         stats.update(host_factor_s=t1 - t0, host_gather_s=t2 - t1)
     return gp
+
+
+def allreduce_first_failure(info: torch.Tensor) -> torch.Tensor:
+    """All-reduce LAPACK-style info words (0 = success, k > 0 = leading minor k not positive)
+    to the FIRST failing minor over the ranks, in place.  A non-SPD panel's NaNs spread into
+    later panels that other ranks own, so a MAX would report the last failure and the message
+    would change with the world size; 0 → INT32_MAX, MIN, back gives the one-rank answer."""
+    big = torch.iinfo(torch.int32).max
+    info.copy_(torch.where(info == 0, torch.full_like(info, big), info))
+    dist.all_reduce(info, op=dist.ReduceOp.MIN)
+    info.copy_(torch.where(info == big, torch.zeros_like(info), info))
+    return info
 
 
 def _allgather_w_columns(A: torch.Tensor, n: int, ws: int, rank: int, dev):
@@ -346,8 +361,10 @@ def krige_jobs_sharded(jobs, variance: str = "ozaki", chunk: int = 8192, var_mod
 
     Per job a rank does 1/world of a fit plus 1/world of the predict, so for a stream of jobs
     the fit — the serial part of a one-job multi-GPU predict — is divided like the grid
-    (DESIGN.md §5).  Every rank must pass the same job sequence (x, y are read on the owner
-    only); a non-SPD K_y raises numpy.linalg.LinAlgError on every rank at that job.  Nothing is
+    (DESIGN.md §5).  Every rank must pass the same job sequence: x with the job's point count
+    on every rank (its size sizes the broadcast), while the values of x and y are read on the
+    owner only; x may be a tensor, an array or a nested list.  A non-SPD K_y raises
+    numpy.linalg.LinAlgError on every rank at that job.  Nothing is
     read ahead before the first next(); `stats` counts the fits this rank issues (with their
     host time stamps, engine.note_fit_issued)."""
     ws, rank = world()
@@ -410,7 +427,7 @@ def krige_jobs_sharded(jobs, variance: str = "ozaki", chunk: int = 8192, var_mod
                 #                          check() also raises a preparation error)
             else:
                 comm.wait_stream(main)
-        ntr = int(np.prod(tuple(x.shape))) // spec.input_dim
+        ntr = E._point_count(x, spec.input_dim)   # every rank passes x with the job's point count
         npad, n = E.fit_layout(spec, ntr, variance)
         with torch.cuda.stream(comm):
             gp = broadcast_fit(gp, spec, noise, x, dev, src=owner, error=err, layout=(n, ntr, npad))

@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import collections
 import ctypes
+import itertools
 import time
 from dataclasses import dataclass, field
 
@@ -597,7 +598,7 @@ def note_fit_issued(stats: dict | None):
 
 def krige_jobs(jobs, variance: str = "ozaki", chunk: int = 8192, var_mode: str = "latent",
                compute_var: bool = True, jitter: float = 0.0, device=None, stats: dict | None = None,
-               fits_ahead: int = 1):
+               fits_ahead: int | None = None):
     """Independent kriging jobs (kernel, x, y, noise, xg), one after another — the reference's
     runKrig.py:1-40 sweep (one GP_laser / krig.kriging fit + grid predict per setting or
     time window) run in one process.  Yields (mean, var) per job, in order, on the current
@@ -617,11 +618,21 @@ def krige_jobs(jobs, variance: str = "ozaki", chunk: int = 8192, var_mode: str =
     (gp2d_potrf draws a separate internal stream set per call).  fits_ahead = 0: each job's fit
     and predict strictly one after the other on the current stream — the fastest form for small
     jobs whose latency-bound fit outlasts their predict (config B: a fit beside a predict runs
-    ≈ 2.4× longer)."""
+    ≈ 2.4× longer).  fits_ahead = None (default): auto_fits_ahead() on the first
+    job's shape — 1 where its predict outlasts its fit enough to hide it, else 0."""
     dev = _require_device(device)
     main = torch.cuda.current_stream(dev)
+    it = iter(jobs)
+    if fits_ahead is None:
+        first = next(it, None)
+        if first is None:
+            return
+        it = itertools.chain([first], it)
+        kernel, x, _, _, xg = first
+        fits_ahead = auto_fits_ahead(kernel, _point_count(x, kernel.input_dim),
+                                     _point_count(xg, kernel.input_dim), variance, compute_var)
     if int(fits_ahead) <= 0:
-        yield from _krige_jobs_serial(jobs, variance, chunk, var_mode, compute_var, jitter, dev, stats)
+        yield from _krige_jobs_serial(it, variance, chunk, var_mode, compute_var, jitter, dev, stats)
         return
     k = max(1, int(fits_ahead))
     sides = [side_stream(dev) for _ in range(k)]
@@ -641,7 +652,6 @@ def krige_jobs(jobs, variance: str = "ozaki", chunk: int = 8192, var_mode: str =
             return side, fit(kernel, x, y, noise, jitter=jitter, device=dev, variance=variance, check=False,
                              join=join)
 
-    it = iter(jobs)
     queue = collections.deque()   # (job, side stream, gp) with the fit queued
 
     def fill(limit):
@@ -671,6 +681,38 @@ def krige_jobs(jobs, variance: str = "ozaki", chunk: int = 8192, var_mode: str =
     finally:
         if prev_sets is not None:
             N.lib().gp2d_factor_sets(prev_sets)
+
+
+def _point_count(x, dim: int) -> int:
+    if isinstance(x, torch.Tensor):
+        return x.numel() // dim
+    return int(np.size(x)) // dim
+
+
+# job-shape model of auto_fits_ahead, fitted to the one-GPU measurements of DESIGN.md §6
+# (profiles/r03_problem_sizes.txt, r03_ring_depth_E_B_ab.txt): a job's predict takes ≈ 1 ms +
+# 48 ms · (M / 65,536) · (N / 4096)² on the Ozaki engine (×2.5 on FP64), its fit ≈ 0.061 ms ·
+# (n / 128)^1.3 (2.24 ms at n = 2048, 13.6 ms at n = 8192), and a fit beside a predict runs
+# ≈ 2.4× longer than alone (its dependent chain is dispatched behind the predict's GEMMs)
+_PRED_MS_REF, _FIT_MS_COEF, _FIT_MS_EXP, _FIT_STRETCH = 48.0, 0.061, 1.3, 2.4
+
+
+def auto_fits_ahead(kernel: KernelSpec, n_train: int, m_grid: int, variance: str = "ozaki",
+                    compute_var: bool = True) -> int:
+    """krige_jobs' default fits in flight for jobs of this shape: 1 (job i+1's fit under job
+    i's predict) when that is faster by the model above, else 0 (each job's fit and predict back
+    to back).  A pipelined job takes max(p, 2.4·f) + the fit's displaced GEMM work (≈ 0.1·p),
+    a serial one f + p, so the overlap pays when p > 1.4·f.  Measured: config B (N = 1024, 128²
+    grid) 4.19e6 points/s back to back vs 2.8–3.3e6 with one fit in flight; the headline
+    (N = 4096, 256²) 55.7 vs 61.3 ms per job with one."""
+    _, n = fit_layout(kernel, max(1, int(n_train)), variance)
+    bd = kernel.block_dim
+    scale = (m_grid / 65536.0) * (n / (2.0 * 4096)) ** 2 * (bd / 2.0)
+    p = (1.0 + _PRED_MS_REF * scale) * (1.0 if variance == "ozaki" else 2.5)
+    if not compute_var:
+        p = 1.0 + 0.1 * (p - 1.0)
+    f = _FIT_MS_COEF * (n / NB) ** _FIT_MS_EXP
+    return 1 if p > (_FIT_STRETCH - 1.0) * f else 0
 
 
 def _krige_jobs_serial(jobs, variance, chunk, var_mode, compute_var, jitter, dev, stats):

@@ -196,7 +196,7 @@ def optimize_restarts(kernel: E.KernelSpec, x, y, noise: float, num_restarts: in
 
 
 def sweep(kernel: E.KernelSpec, x, y, settings, noise: float = None, jitter: float = 0.0, device=None,
-          eval_gradient: bool = False, concurrent: int = 1):
+          eval_gradient: bool = False, concurrent: int | None = None):
     """LML (and gradient) for each hyperparameter setting (a list of get_params-style dicts,
     missing keys taken from kernel/noise) — BASELINE config E.  Under torch.distributed the
     settings are dealt round-robin over ranks and the results all-reduced (bit-identical to
@@ -206,7 +206,9 @@ def sweep(kernel: E.KernelSpec, x, y, settings, noise: float = None, jitter: flo
     host round trip for the results (engine.fit(check=False), engine.lml_device), read back 2c
     settings behind; each fit joins its chain on the host (fit(join=True)), so setting i's LML
     and gradient run under setting i+1's factorisation (config E: 60.8–61.2 vs 58.3–59.2
-    settings/s at c = 1; without the join, 41.9).  Same kernels, same bits as c = 1."""
+    settings/s at c = 1; without the join, 41.9).  Same kernels, same bits as c = 1.
+    concurrent = None (default): auto_concurrent() — 2 when there is a gradient to overlap and
+    this rank holds at least two settings, else 1."""
     ws, rank = (dist.get_world_size(), dist.get_rank()) if dist.is_available() and dist.is_initialized() else (1, 0)
     base = get_params(kernel, noise if noise is not None else 0.0)
     S = len(settings)
@@ -214,7 +216,7 @@ def sweep(kernel: E.KernelSpec, x, y, settings, noise: float = None, jitter: flo
     vals = np.zeros(S)
     grads = np.zeros((S, P))
     mine = list(range(rank, S, ws))
-    c = max(1, int(concurrent))
+    c = auto_concurrent(len(mine), eval_gradient) if concurrent is None else max(1, int(concurrent))
     if c == 1:
         for i in mine:
             p = dict(base)
@@ -234,7 +236,6 @@ def sweep(kernel: E.KernelSpec, x, y, settings, noise: float = None, jitter: flo
         dev = E._require_device(device)
         main = torch.cuda.current_stream(dev)
         streams = [E.side_stream(dev) for _ in range(c)]
-        prev_sets = E.N.lib().gp2d_factor_sets(c)   # one internal factor stream set per stream
         inflight = collections.deque()
 
         def drain(limit):
@@ -250,27 +251,45 @@ def sweep(kernel: E.KernelSpec, x, y, settings, noise: float = None, jitter: flo
                 if g is not None:
                     grads[i] = g.cpu().numpy()
 
-        for j, i in enumerate(mine):
-            p = dict(base)
-            p.update(settings[i])
-            k, nz = set_params(kernel, p)
-            st = streams[j % c]
-            st.wait_stream(main)
-            with torch.cuda.stream(st):
-                # joined on the host: the chain never runs with this stream's wait pending
-                # beside it (≈ 40 % slower); what overlaps is the previous
-                # setting's LML + gradient under this setting's chain
-                gp = E.fit(k, x, y, nz, jitter=jitter, device=dev, check=False, join=True)
-                out, g = E.lml_device(gp, eval_gradient)
-                ev = torch.cuda.Event()
-                ev.record(st)
-            inflight.append((i, gp, out, g, ev))
-            drain(2 * c)
-        drain(0)
-        E.N.lib().gp2d_factor_sets(prev_sets)
+        prev_sets = E.N.lib().gp2d_factor_sets(c)   # one internal factor stream set per stream
+        try:
+            _sweep_concurrent(kernel, x, y, settings, base, mine, jitter, dev, eval_gradient, streams, main,
+                              inflight, drain)
+            drain(0)
+        finally:   # any exception (GP2DError, KeyboardInterrupt, ...) restores the process-wide setting
+            E.N.lib().gp2d_factor_sets(prev_sets)
     if ws > 1:
         vals, grads = allreduce_disjoint(vals, grads, device)
     return vals, (grads if eval_gradient else None)
+
+
+def auto_concurrent(n_settings: int, eval_gradient: bool) -> int:
+    """hyper.sweep's default stream count: two streams overlap setting i's K_y⁻¹ + gradient
+    contractions (≈ 3.4 ms at N = 4096) with setting i+1's fit chain (config E: 60.6–61.2 vs
+    58.3–59.9 settings/s, profiles/r03_ring_depth_E_B_ab.txt); the LML alone (0.045 ms) has
+    nothing to overlap, and a single setting has no next one."""
+    return 2 if (eval_gradient and n_settings >= 2) else 1
+
+
+def _sweep_concurrent(kernel, x, y, settings, base, mine, jitter, dev, eval_gradient, streams, main, inflight,
+                      drain):
+    c = len(streams)
+    for j, i in enumerate(mine):
+        p = dict(base)
+        p.update(settings[i])
+        k, nz = set_params(kernel, p)
+        st = streams[j % c]
+        st.wait_stream(main)
+        with torch.cuda.stream(st):
+            # joined on the host: the chain never runs with this stream's wait pending
+            # beside it (≈ 40 % slower, DESIGN.md §0); what overlaps is the previous
+            # setting's LML + gradient under this setting's chain
+            gp = E.fit(k, x, y, nz, jitter=jitter, device=dev, check=False, join=True)
+            out, g = E.lml_device(gp, eval_gradient)
+            ev = torch.cuda.Event()
+            ev.record(st)
+        inflight.append((i, gp, out, g, ev))
+        drain(2 * c)
 
 
 def allreduce_disjoint(vals: np.ndarray, grads: np.ndarray, device=None):

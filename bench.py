@@ -8,8 +8,8 @@ scaling): the same 256×256 job grid sharded over the N ranks, job j fitted on r
 and its factor broadcast over RCCL (distributed.krige_jobs_sharded); --scaling weak gives
 each rank its own 256×256 block with a replicated fit instead.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
-    torchrun --nproc-per-node N bench.py --gpus N ...
+    python bench.py [--gpus N] [--steps K] [--warmup W]   (N > 1: starts the N ranks itself)
+    torchrun --nproc-per-node N bench.py --gpus N ...     (--gpus must equal WORLD_SIZE)
 
 Rank 0 prints ONE JSON line (the driver contract) with `roofline` (dominant
 kernel: the variance contraction, timed live with HIP events on its stream) and
@@ -95,18 +95,16 @@ def parse():
     ap.add_argument("--cpu-sample-points", type=int, default=2048)
     ap.add_argument("--pmc-json", default=None)
     ap.add_argument("--fits-ahead", type=int, default=None,
-                    help="N=1 job stream: fits in flight (engine.krige_jobs fits_ahead; default 1, config B 0 = "
-                         "each job's fit and predict back to back)")
+                    help="N=1 job stream: fits in flight (engine.krige_jobs fits_ahead; default: the library's "
+                         "engine.auto_fits_ahead for the job shape — 0 = each job's fit and predict back to back)")
     ap.add_argument("--sweep-concurrent", type=int, default=None,
                     help="config E: streams the settings' fit + LML are queued on (hyper.sweep concurrent; "
-                         "default 2: each setting's LML + gradient under the next setting's fit)")
+                         "default: the library's hyper.auto_concurrent)")
     ap.add_argument("--single-job-dist", type=int, default=0,
                     help="also time one job with distributed.fit_distributed at N = 1 (always at N > 1)")
     a = ap.parse_args()
     if a.config == "B":
         a.kind, a.ntrain, a.grid = "df", 1024, 128
-        if a.fits_ahead is None:   # the 16-block fit outlasts the 128² predict: jobs back to back
-            a.fits_ahead = 0
     elif a.config == "C":
         a.kind, a.ntrain, a.grid = "mixed", 4096, 256
     elif a.config == "D":
@@ -121,6 +119,50 @@ def parse():
     return a
 
 
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` (N > 1) run without a launcher: start the N rank processes as ONE
+    child `torch.distributed.run` (127.0.0.1 rendezvous, a free port) with this script's own
+    arguments, before this process touches the GPU (the parent never initialises HIP and never
+    execs), relay rank 0's JSON line to stdout and return the child's exit code.  The driver's
+    command shape (`python3 bench.py --gpus N ...`) then measures N GPUs by itself; the
+    reference's own parallelism is the job array, runKrig.py:7,14-17."""
+    import signal
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    print(f"bench.py: --gpus {n} without WORLD_SIZE: launching {n} rank processes ({' '.join(cmd[1:7])} ...)",
+          file=sys.stderr, flush=True)
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, start_new_session=True)
+    try:
+        for line in proc.stdout:   # rank 0 prints the one JSON line; anything else goes to stderr
+            (sys.stdout if line.lstrip().startswith("{") else sys.stderr).write(line)
+            sys.stdout.flush()
+        return proc.wait()
+    except BaseException:
+        os.killpg(proc.pid, signal.SIGTERM)   # the child's own process group: the ranks go with it
+        proc.wait()
+        raise
+
+
+def check_world(args) -> int | None:
+    """World-size contract of --gpus, checked before any GPU call: returns the exit code of a
+    run that must not proceed in this process (a self-launched N-rank child's, or 2 for a
+    --gpus that contradicts the launcher's WORLD_SIZE), None to run here."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is None:
+        return launch_ranks(args.gpus) if args.gpus > 1 else None
+    if int(ws) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={ws} ranks", file=sys.stderr,
+              flush=True)
+        return 2
+    return None
+
+
 def setup_dist(args):
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     if is_multi(ws):
@@ -131,7 +173,7 @@ def setup_dist(args):
         backend = os.environ.get("GP2D_DIST_BACKEND", "nccl")
         kw = {"device_id": torch.device("cuda", local)} if backend == "nccl" else {}
         dist.init_process_group(backend, **kw)
-        return ws, dist.get_rank(), torch.device("cuda", local)
+        return dist.get_world_size(), dist.get_rank(), torch.device("cuda", local)
     return 1, 0, torch.device("cuda", 0)
 
 
@@ -184,8 +226,8 @@ def run_sweep(args, ws, rank, dev):
     settings = config_e_settings()
     ks = E.KernelSpec(kind="df", l_df=5.0)
 
-    # two streams: each setting's LML + gradient under the next setting's (host-joined) fit
-    conc = args.sweep_concurrent or 2
+    # None: the library's default (hyper.auto_concurrent)
+    conc = args.sweep_concurrent
 
     def sweep():
         return H.sweep(ks, xt, yt, settings, noise=0.0025, eval_gradient=True, device=dev, concurrent=conc)
@@ -208,14 +250,15 @@ def run_sweep(args, ws, rank, dev):
         out = {
             "metric": f"hyperparameter settings/sec (fit + LML + gradient), 64-setting sweep, N_train={args.ntrain}, "
                       "div-free 2D kernel",
-            "value": len(settings) * args.steps / elapsed, "unit": "settings/s", "n_gpus": ws,
+            "value": len(settings) * args.steps / elapsed, "unit": "settings/s", "n_gpus": ws, "world_size": ws,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps,
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (seeded drifter field, SURVEY.md §8d)",
             "config": {"workload": f"BASELINE config E: 64 (l_df, noise) settings x N_train={args.ntrain}, "
                                    f"div-free, LML + exact gradient per setting, settings dealt over {ws} GPU(s)",
                        "n_train": args.ntrain, "settings": len(settings), "parallelism": f"settings round robin x{ws}",
-                       "sweep_concurrent": conc},
+                       "sweep_concurrent": conc if conc is not None else
+                       H.auto_concurrent(len(range(rank, len(settings), ws)), True)},
             "roofline": {"bound": "mfma", "achieved": per_gpu, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": per_gpu / FP64_PEAK_TFLOPS, "traffic": None,
                          "kernel": "whole sweep per GPU: POTRF + TRTRI + W^T W (n^3 FP64 flop per setting) / wall time"},
@@ -266,6 +309,11 @@ def single_job_distributed(args, ws, spec, xt, yt, noise, xg, m_all, dev, pred_c
 
 def main():
     args = parse()
+    if args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    rc = check_world(args)
+    if rc is not None:
+        sys.exit(rc)
     ws, rank, dev = setup_dist(args)
     if args.config == "E":
         return run_sweep(args, ws, rank, dev)
@@ -405,7 +453,7 @@ def main():
 
         def stream(k):   # the shipped API for a sweep of jobs
             return E.krige_jobs(itertools.repeat(job, k), variance=args.variance, chunk=args.chunk, stats=stats,
-                                fits_ahead=1 if args.fits_ahead is None else args.fits_ahead)
+                                fits_ahead=args.fits_ahead)
         api = "engine.krige_jobs"
     trace = os.environ.get("GP2D_BENCH_TRACE") == "1"   # per-step wall times on stderr (diagnostics)
 
@@ -492,10 +540,15 @@ def main():
     headline = (args.kind, args.ntrain, G, strong) == ("df", 4096, 256, False)
     pmc_round = "r03" if args.variance == "ozaki" else "r02"   # the latest PMC pass of each engine
     pmc_json = args.pmc_json or os.path.join(ROOT, "profiles", f"{pmc_round}_pmc_traffic_{args.variance}.json")
+    traffic_source = None
     try:
         with open(pmc_json) as f:
             pmc = json.load(f)
         traffic = pmc.get("hbm_bytes_per_launch") if (headline or args.pmc_json) else None
+        if traffic is not None:   # a separate builder run of rocprofv3 --pmc, not measured in this run
+            traffic_source = (f"{os.path.relpath(pmc_json, ROOT)}: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes "
+                              f"(separate runs, {pmc.get('round', os.path.basename(pmc_json)[:3])}) of this kernel at "
+                              "this workload; not measured inside this bench run")
     except (OSError, ValueError):
         pass
     if args.variance == "ozaki":
@@ -508,7 +561,8 @@ def main():
         ex = achieved * nmod * efrac if achieved else None
         roof = {"bound": "mfma", "achieved": ex, "peak": INT8_PEAK_TOPS,
                 "unit": "TOP/s (int8)", "frac": (ex / INT8_PEAK_TOPS) if ex else None,
-                "traffic": traffic, "kernel": f"igemm_nt_mod_kernel x{nmod} moduli (Ozaki-II variance, exact)",
+                "traffic": traffic, "traffic_source": traffic_source,
+                "kernel": f"igemm_nt_mod_kernel x{nmod} moduli (Ozaki-II variance, exact)",
                 "launches": klaunch * nmod, "avg_launch_ms": (kms / klaunch / nmod) if klaunch else None,
                 "ops_per_launch": (kflops * efrac / klaunch) if klaunch else None,
                 "executed_fraction_of_dense": efrac,
@@ -522,6 +576,7 @@ def main():
     else:
         roof = {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": (achieved / FP64_PEAK_TFLOPS) if achieved else None, "traffic": traffic,
+                "traffic_source": traffic_source,
                 "kernel": "gemm_f64_kernel<NN,COLSQ> (variance ‖L⁻¹k*‖²)",
                 "launches": klaunch, "avg_launch_ms": (kms / klaunch) if klaunch else None,
                 "flops_per_launch": (kflops / klaunch) if klaunch else None}
@@ -531,6 +586,7 @@ def main():
         "value": value,
         "unit": "points/s",
         "n_gpus": ws,
+        "world_size": ws,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
@@ -552,7 +608,8 @@ def main():
         "roofline": roof,
         "pipelined": cfg["pipeline"],
         "api": api,
-        "fits_ahead": (1 if args.fits_ahead is None else args.fits_ahead) if api == "engine.krige_jobs" else None,
+        "fits_ahead": (E.auto_fits_ahead(spec, args.ntrain, m, args.variance) if args.fits_ahead is None
+                       else args.fits_ahead) if api == "engine.krige_jobs" else None,
         "unpipelined": unpiped,
         "single_job": single_job,
         "timed_fits": timed_fits,

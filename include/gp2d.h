@@ -95,8 +95,13 @@ int gp2d_assemble(const double* xa, int64_t na, int64_t na_pad,
  * gp2d_factor_sets(k) (k ≤ 4, returns the previous k) puts k sets in use — a caller
  * stream keeps the set it first drew — so factorisations issued on different caller
  * streams run concurrently, their latency-bound chains interleaved (engine.krige_jobs
- * fits_ahead).  Each set's enqueue is serialised by its own lock (thread-safe).     */
+ * fits_ahead).  Each set's enqueue is serialised by its own lock (thread-safe).
+ * A call with k > 1 starts a new batch: the caller-stream → set map is cleared, so the
+ * next k caller streams get sets 0..k−1 in order of first use.                       */
 int gp2d_factor_sets(int k);
+/* gp2d_factor_set_of: the internal stream set `stream`'s factorisations currently draw
+ * (0..k−1), or −1 if the stream has none in use (diagnostics and tests).            */
+int gp2d_factor_set_of(void* stream);
 /* gp2d_factor_join(1): this thread's later gp2d_potrf / gp2d_potrf_inv calls wait on the
  * host for the factorisation's chain before they enqueue the caller stream's join, so the
  * caller's hardware queue holds no pending wait while the chain runs (a pending wait there

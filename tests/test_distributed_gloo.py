@@ -139,3 +139,42 @@ def test_bcast_fit_failure_raises_on_every_rank(tmp_path):
         raised, bad = open(os.path.join(tmp_path, f"fail{i}.txt")).read().split()
         assert raised == "LinAlgError", i
         assert bad == "ValueError", i
+
+
+def _info_worker(rank, world, port, out_dir):
+    """allreduce_first_failure: the first failing leading minor over the ranks (not the last)."""
+    import sys
+    for p in (ROOT, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from gp2d import distributed as GD
+    cases = [(0, 0, 0), (0, 513, 513), (700, 513, 513), (513, 0, 513), (300, 900, 300)]
+    got = []
+    for a, b, _ in cases:
+        info = torch.tensor([a if rank == 0 else b], dtype=torch.int32)
+        got.append(int(GD.allreduce_first_failure(info).item()))
+    with open(os.path.join(out_dir, f"info{rank}.txt"), "w") as f:
+        f.write(" ".join(map(str, got)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_info_allreduce_reports_first_failure(tmp_path):
+    world = 2
+    mp.spawn(_info_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    want = "0 513 513 513 300"
+    for i in range(world):
+        assert open(os.path.join(tmp_path, f"info{i}.txt")).read() == want, i
+
+
+def test_point_count_accepts_lists_arrays_tensors():
+    """krige_jobs_sharded sizes a job's broadcast from x on every rank: x may be a nested list
+    (engine.fit accepts them through _as_points), an array or a tensor."""
+    from gp2d import engine as E
+    pts = [[0.0, 1.0], [2.0, 3.0], [4.0, 5.0]]
+    assert E._point_count(pts, 2) == 3
+    assert E._point_count(np.asarray(pts), 2) == 3
+    assert E._point_count(torch.tensor(pts), 2) == 3
+    assert E._point_count([[0.0, 1.0, 2.0]] * 5, 3) == 5

@@ -91,3 +91,22 @@ def test_bench_multi_rank_paths_under_rccl():
     assert d["api"] == "distributed.krige_jobs_sharded" and d["scaling"] == "strong"
     assert d["timed_fits"]["issued_in_window"] == d["timed_fits"]["issued_total"] == 3
     assert d["single_job"]["distributed_fit"]["ms"] > 0
+
+
+def test_bench_gpus2_self_launch():
+    """`python bench.py --gpus 2` with NO launcher (the driver's command shape) starts the two
+    rank processes itself (one child torch.distributed.run) and reports n_gpus = world_size = 2
+    (gloo: RCCL refuses two ranks on the one card of this box)."""
+    env = dict(os.environ, GP2D_DIST_BACKEND="gloo")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--ntrain", "256", "--grid", "64",
+           "--steps", "4", "--warmup", "1", "--chunk", "1024"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=200, cwd=ROOT, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["world_size"] == 2 and d["scaling"] == "strong"
+    assert d["timed_fits"]["issued_in_window"] == d["timed_fits"]["issued_total"] == 4
+    assert abs(d["value"] - 64 * 64 / (d["ms_per_step"] * 1e-3)) / d["value"] < 1e-6

@@ -122,6 +122,35 @@ def test_config_d_rank0_shard(golden):
     assert elem_mean(mu_s, g["mean"]) < GATE
 
 
+def test_config_d_distributed_fit_rank0_shard(golden):
+    """Config D through the path bench.py's `single_job.distributed_fit` times at every N > 1:
+    distributed.fit_distributed (block-cyclic POTRF + TRTRI over 256-column super-blocks) at
+    P = 1 on N_train = 16384 (mixed, as D), then rank 0's shard of the 512² grid — against the
+    reference fixture with the same normwise and elementwise gates as the engine.fit path
+    (/root/reference/krig.py:541-557: one model's large grid, predicted slice by slice)."""
+    from gp2d import distributed as GD
+    g = golden("config_d_rank0.npz")
+    x1, x2, u, v = D.synthetic_tracks(16384, seed=2016)
+    assert np.allclose([x1.sum(), x2.sum()], g["x_sum"], rtol=0, atol=0)
+    _, _, xg_all = D.bbox_grid(x1, x2, 512, pad=5.0)
+    lo, hi = D.shard_range(xg_all.shape[0], 8, 0)
+    shard = xg_all[lo:hi]
+    ks = E.KernelSpec(kind="mixed", l_df=5.0, l_cf=5.0, ratio=float(g["rate"]))
+    gp = GD.fit_distributed(ks, torch.tensor(np.stack([x1, x2], 1), device="cuda"),
+                            torch.tensor(np.concatenate([u, v]), device="cuda"), 0.0025, variance="ozaki")
+    mu, var = E.Predictor(gp, 8192)(torch.tensor(shard, device="cuda"))
+    m = shard.shape[0]
+    mu_s, var_s = _at(mu, g["idx"], m), _at(var, g["idx"], m)
+    del gp
+    torch.cuda.empty_cache()
+    ev = elem_var(var_s, g["var"])
+    print(f"D (fit_distributed, P = 1): mean {rel(mu_s, g['mean']):.2e} var {rel(var_s, g['var']):.2e} "
+          f"var elementwise {ev:.2e}")
+    assert rel(mu_s, g["mean"]) < GATE and rel(var_s, g["var"]) < GATE
+    assert ev < GATE
+    assert elem_mean(mu_s, g["mean"]) < GATE
+
+
 def test_config_e_sweep_share(golden):
     """Config E: one rank's 8 of the 64 settings at N_train = 4096 through hyper.sweep (the
     call each of the 8 ranks makes): LML of all 8, gradient of 2, against the reference-

@@ -255,6 +255,11 @@ def _dfit_problem(n):
     return x, y, np.stack([GX.reshape(-1), GY.reshape(-1)], 1)
 
 
+def _sha(t):
+    import hashlib
+    return np.frombuffer(hashlib.sha256(t.contiguous().cpu().numpy().tobytes()).digest(), np.uint8)
+
+
 def _dfit_worker(rank, world, port, out_dir, n, kind, noise):
     for p in (ROOT, PKG):
         if p not in sys.path:
@@ -273,7 +278,7 @@ def _dfit_worker(rank, world, port, out_dir, n, kind, noise):
         gp = GD.fit_distributed(spec, torch.tensor(x, device=dev), torch.tensor(y, device=dev), noise, dev)
         lo, hi, mean, var = GD.predict_shard(E.Predictor(gp, 1024), torch.tensor(xg, device=dev))
         fm, fv = GD.gather_shards(xg.shape[0], 2, lo, hi, mean, var, dev)
-        out = dict(W=gp.W.cpu().numpy(), alpha=gp.alpha.cpu().numpy(), mean=fm.cpu().numpy(),
+        out = dict(W_sha=_sha(gp.W), alpha=gp.alpha.cpu().numpy(), mean=fm.cpu().numpy(),
                    var=fv.cpu().numpy(), nmod=int(gp.extra["ozaki"][2]), raised=0)
     except np.linalg.LinAlgError:
         out = dict(raised=1)
@@ -283,12 +288,13 @@ def _dfit_worker(rank, world, port, out_dir, n, kind, noise):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n,kind", [(1024, "df"), (700, "mixed")])
+@pytest.mark.parametrize("n,kind", [(1024, "df"), (700, "mixed"), (4096, "df")])
 def test_distributed_fit_two_ranks_bit_identical(tmp_path, n, kind):
     """fit_distributed over two ranks (block-cyclic POTRF + TRTRI, a panel broadcast per
     256-column super-block, W columns all-gathered): both ranks hold the bits of the one-rank
-    run of the same algorithm (W, α, and the sharded posterior), and agree with engine.fit's
-    factor and posterior to 1e-12 / 1e-10 (relative, normwise)."""
+    run of the same algorithm (W by SHA-256, α, and the sharded posterior), and agree with
+    engine.fit's factor and posterior to 1e-12 / 1e-10 (relative, normwise).  N = 4096
+    (n = 8192: 32 super-columns, 16 per rank) is the headline's size."""
     from gp2d import distributed as GD
     from gp2d import engine as E
     world = 2
@@ -302,7 +308,7 @@ def test_distributed_fit_two_ranks_bit_identical(tmp_path, n, kind):
     assert W1.shape[0] // 256 >= 6                                 # both ranks own super-columns
     for i in range(world):
         assert int(r[i]["raised"]) == 0
-        assert np.array_equal(r[i]["W"], W1), i
+        assert np.array_equal(r[i]["W_sha"], _sha(gp1.W)), i
         assert np.array_equal(r[i]["alpha"], gp1.alpha.cpu().numpy()), i
         assert np.array_equal(r[i]["mean"], mu1) and np.array_equal(r[i]["var"], var1), i
     assert np.array_equal(np.triu(W1, 1), np.zeros_like(W1))       # W = L⁻¹ is lower-triangular
@@ -338,3 +344,94 @@ def test_distributed_fit_one_rank_lookahead_and_f64():
     mu, var = (t.cpu().numpy() for t in E.Predictor(gp, 1024)(xg))
     assert np.linalg.norm(mu1 - mu) / np.linalg.norm(mu) < 1e-10
     assert np.linalg.norm(var1 - var) / np.linalg.norm(var) < 1e-10
+
+
+def _prep_fail_worker(rank, world, port, out_dir):
+    """Job 1 (owned by rank 1): the owner's int8 preparation fails after a successful POTRF
+    (fault injected into engine.ozaki_prepare inside that one fit).  The owner defers the error
+    to check(); the status word it broadcasts must say "failed" (−1), so BOTH ranks raise at
+    job 1 after yielding job 0 and neither waits in a later collective."""
+    for p in (ROOT, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from gp2d import _native as N
+    from gp2d import distributed as GD
+    from gp2d import engine as E
+    jobs = _jobs()[:3]
+    real_fit, real_prep = E.fit, E.ozaki_prepare
+    calls = [0]
+
+    def fit(*a, **k):
+        calls[0] += 1
+        if rank == 1 and calls[0] == 1:   # rank 1's first fit is job 1
+
+            def bad_prep(gp, diag_add=None):
+                raise N.GP2DError("injected: gp2d_ozaki_prepare_async failed")
+            E.ozaki_prepare = bad_prep
+            try:
+                return real_fit(*a, **k)
+            finally:
+                E.ozaki_prepare = real_prep
+        return real_fit(*a, **k)
+
+    E.fit = fit
+    done, raised = 0, "none"
+    try:
+        for _ in GD.krige_jobs_sharded(jobs, chunk=1024):
+            done += 1
+    except Exception as e:   # noqa: BLE001 — the type is what the test checks
+        raised = type(e).__name__
+    torch.cuda.synchronize()
+    with open(os.path.join(out_dir, f"prep{rank}.txt"), "w") as f:
+        f.write(f"{done} {raised}")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_round_robin_owner_preparation_error_raises_on_every_rank(tmp_path):
+    world = 2
+    _spawn(_prep_fail_worker, world, str(tmp_path))
+    got = [open(os.path.join(tmp_path, f"prep{i}.txt")).read().split() for i in range(world)]
+    assert got[1] == ["1", "GP2DError"], got        # the owner: its own deferred error
+    assert got[0] == ["1", "RuntimeError"], got     # the receiver: "failed on the rank that owned it"
+
+
+def _list_worker(rank, world, port, out_dir):
+    """krige_jobs_sharded with x, y, xg given as nested Python lists on every rank (engine.fit
+    accepts lists): the receivers size the broadcast from the list."""
+    for p in (ROOT, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from gp2d import distributed as GD
+    jobs = [(s, x.tolist(), y.tolist(), nz, xg) for s, x, y, nz, xg in _jobs()[:2]]
+    res = {}
+    for j, (lo, hi, mean, var) in enumerate(GD.krige_jobs_sharded(jobs, chunk=1024)):
+        res[f"lo{j}"], res[f"hi{j}"] = lo, hi
+        res[f"mean{j}"], res[f"var{j}"] = mean.cpu().numpy(), var.cpu().numpy()
+    np.savez(os.path.join(out_dir, f"list{rank}.npz"), **res)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_round_robin_jobs_list_inputs(tmp_path):
+    from gp2d import distributed as GD
+    from gp2d import engine as E
+    world = 2
+    _spawn(_list_worker, world, str(tmp_path))
+    r = [np.load(os.path.join(tmp_path, f"list{i}.npz")) for i in range(world)]
+    for j, (spec, x, y, noise, xg) in enumerate(_jobs()[:2]):
+        gp = E.fit(spec, x, y, noise, variance="ozaki")
+        mu, var = (t.cpu().numpy() for t in E.Predictor(gp, 1024)(xg))
+        m = xg.shape[0]
+        assert np.array_equal(GD.assemble_from_shards(
+            m, 2, [(int(r[i][f"lo{j}"]), int(r[i][f"hi{j}"]), r[i][f"mean{j}"]) for i in range(world)]), mu), j
+        assert np.array_equal(GD.assemble_from_shards(
+            m, 2, [(int(r[i][f"lo{j}"]), int(r[i][f"hi{j}"]), r[i][f"var{j}"]) for i in range(world)]), var), j

@@ -29,7 +29,8 @@ JOBS = [(1, 700, 60, "df"), (2, 700, 64, "mixed"), (3, 1500, 50, "df"), (4, 300,
         (5, 1500, 72, "mixed"), (6, 1500, 72, "df")]
 
 
-@pytest.mark.parametrize("variance,ahead", [("ozaki", 1), ("f64", 1), ("ozaki", 2), ("ozaki", 3), ("ozaki", 0)])
+@pytest.mark.parametrize("variance,ahead", [("ozaki", 1), ("f64", 1), ("ozaki", 2), ("ozaki", 3), ("ozaki", 0),
+                                            ("ozaki", None)])
 def test_krige_jobs_bit_identical_to_sequential(variance, ahead):
     """fits_ahead > 1: consecutive fits in flight together, each drawing its own internal
     factor stream set; fits_ahead = 0: back to back on one stream — still the bits of one job
@@ -75,3 +76,39 @@ def test_fit_join_modes_same_bits_on_a_side_stream(join):
     assert E.N.lib().gp2d_factor_join(-1) == 0
     assert torch.equal(gp.W, ref.W) and torch.equal(gp.alpha, ref.alpha)
     assert torch.equal(m, rm) and torch.equal(v, rv)
+
+
+def test_factor_sets_deal_fresh_sets_to_a_new_batch():
+    """gp2d_factor_sets(k > 1) starts a new batch: streams that drew set 0 at k = 1 (torch's
+    pools hand the same streams out again) get distinct sets in the batch, so the batch's
+    factorisations overlap instead of queueing on one set."""
+    L = E.N.lib()
+    spec, x, y, noise, _ = _job(9, 300, 8, "df")
+    sides = [E.side_stream(x.device) for _ in range(3)]
+    prev = L.gp2d_factor_sets(1)
+    try:
+        for st in sides:   # every stream first seen at k = 1: set 0
+            st.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(st):
+                E.fit(spec, x, y, noise)
+            assert L.gp2d_factor_set_of(st.cuda_stream) == 0
+        L.gp2d_factor_sets(2)
+        got = []
+        for st in sides[1:]:   # a batch of two, in the order krige_jobs / hyper.sweep use them
+            with torch.cuda.stream(st):
+                E.fit(spec, x, y, noise)
+            got.append(L.gp2d_factor_set_of(st.cuda_stream))
+        assert sorted(got) == [0, 1], got
+    finally:
+        L.gp2d_factor_sets(prev)
+    torch.cuda.synchronize()
+
+
+def test_auto_fits_ahead_picks_the_measured_modes():
+    """The library's job-shape rule (engine.auto_fits_ahead): config B's small jobs run back to
+    back, the headline / C / D shapes pipelined."""
+    df, mixed = E.KernelSpec(kind="df"), E.KernelSpec(kind="mixed", ratio=0.5)
+    assert E.auto_fits_ahead(df, 1024, 128 * 128) == 0
+    assert E.auto_fits_ahead(df, 4096, 256 * 256) == 1
+    assert E.auto_fits_ahead(mixed, 4096, 256 * 256) == 1
+    assert E.auto_fits_ahead(mixed, 16384, 512 * 512) == 1
