@@ -233,7 +233,7 @@ struct FactorStreams {
 struct FactorSet {
   std::mutex enqueue;                     // one factorisation enqueue at a time per set
   hipStream_t crit = nullptr, bulk = nullptr, aux = nullptr, inv = nullptr;
-  std::vector<hipEvent_t> ev;             // 5 fixed events
+  std::vector<hipEvent_t> ev;             // 6 fixed events
   std::vector<hipEvent_t> blk;            // one per block column (fused inverse)
 };
 constexpr int GP2D_FACTOR_CTX = 4;
@@ -285,7 +285,7 @@ int factor_streams(FactorCtx& c, int nblk, hipStream_t caller) {
         hipStreamCreateWithPriority(&f->inv, hipStreamNonBlocking, lo) != hipSuccess) {
       set_error("hipStreamCreate failed"); return -1;
     }
-    f->ev.resize(5);
+    f->ev.resize(6);
     for (auto& e : f->ev)
       if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) { set_error("hipEventCreate failed"); return -1; }
     sets.push_back(std::move(f));
@@ -434,6 +434,24 @@ int inv_top_gemm(int kind, double* A, int64_t lda, int nb, double* T2, double* T
 
 #define GP2D_EV(call) do { if ((call) != hipSuccess) { set_error(#call " failed"); return -1; } } while (0)
 
+namespace {
+// Trailing-update schedule of potrf_impl: G panels per SYRK (K = 128·G) and whether the SYRK
+// is split into the next group's head and the rest.  Measured (profiles/r04_potrf_sched_ab*.jsonl,
+// engine.fit at N_train = 1024 … 16384): four panels with the split tie the pairs where the fit
+// is chain-bound (N ≤ 4096: 2.2 / 4.8 / 13.4 ms) and win where the SYRK dominates (N = 8192:
+// 61.2 vs 63.9 ms; config D: 399 vs 417 ms); eight panels (K = 1024) gain nothing over four.
+// GP2D_POTRF_G (2 | 4 | 8) / GP2D_POTRF_SPLIT override the choice (measurement only).
+struct PotrfSchedule { int G; bool split; };
+PotrfSchedule potrf_schedule(int nb) {
+  PotrfSchedule ps{nb > 0 ? 4 : 2, true};
+  static const char* eg = std::getenv("GP2D_POTRF_G");
+  static const char* es = std::getenv("GP2D_POTRF_SPLIT");
+  if (eg && (std::atoi(eg) == 2 || std::atoi(eg) == 4 || std::atoi(eg) == 8)) ps.G = std::atoi(eg);
+  if (es) ps.split = std::atoi(es) != 0;
+  return ps;
+}
+}  // namespace
+
 // Right-looking blocked Cholesky (NB = 128) with look-ahead on internal streams and the
 // trailing update delayed over pairs of panels:
 //   crit: for pair (k, k+1): block column k+1 ← panel k, factor k+1; block column k+2 ←
@@ -458,7 +476,8 @@ static int potrf_impl(double* A, int64_t n, int64_t lda, double* dinv, int* info
   std::lock_guard<std::mutex> enqueue_lock(*fc.enqueue);
   hipStream_t sc = fc.crit, sb = fc.bulk, sa = fc.aux, si = fc.inv;
   std::vector<hipEvent_t>& ev = *fc.ev;
-  hipEvent_t e_pan = ev[0], e_syrk = ev[1], e_join = ev[2], e_start = ev[3], e_aux = ev[4];
+  hipEvent_t e_pan = ev[0], e_syrk = ev[1], e_join = ev[2], e_start = ev[3];
+  hipEvent_t e_auxc[2] = {ev[4], ev[5]};   // aux's first update of an even / odd block column
   GP2D_EV(hipEventRecord(e_join, s));
   GP2D_EV(hipStreamWaitEvent(sc, e_join, 0));
   GP2D_EV(hipStreamWaitEvent(sb, e_join, 0));
@@ -491,45 +510,83 @@ static int potrf_impl(double* A, int64_t n, int64_t lda, double* dinv, int* info
     return 0;
   };
   GP2D_CHECK(factor(0));
-  // Delayed trailing updates: panels are consumed in pairs, so the bulk SYRK runs with K = 256
-  // (half the launches and half the C read/write traffic per flop of K = 128 updates).  Per
-  // pair (k, k+1), block column k+2 gets both panels through two skinny updates on crit and
-  // columns ≥ k+3 get them through one SYRK on bulk.  Block column k+2's update by panel k
-  // needs neither panel k+1 nor its factor, so it runs on `aux` under factor(k+1)'s
-  // single-workgroup diagonal kernel instead of after it.
-  int k = 0;
-  while (k + 1 < nb) {
-    if (k + 2 < nb) {
-      GP2D_EV(hipEventRecord(e_start, sc));   // panel k final, earlier SYRKs into column k+2 done
-      GP2D_EV(hipStreamWaitEvent(sa, e_start, 0));
-      GP2D_CHECK(colupdate(k + 2, k, sa));
-      GP2D_EV(hipEventRecord(e_aux, sa));
-      GP2D_CHECK(colupdate(k + 1, k, sc));   // columns ≤ k+1 of earlier panels arrived by earlier SYRKs
-      GP2D_CHECK(factor(k + 1));
-      GP2D_EV(hipEventRecord(e_pan, sc));   // panels k, k+1 done
-      GP2D_EV(hipStreamWaitEvent(sb, e_pan, 0));
-      const int64_t f0 = (int64_t)(k + 3) * NB;
-      if (f0 < n) {
-        GemmParams q = gemm_params();
-        q.A = A + f0 * lda + (int64_t)k * NB; q.lda = lda;   // rows ≥ k+3 of panels k, k+1
-        q.B = q.A; q.ldb = lda;
-        q.C = A + f0 * lda + f0; q.ldc = lda;
-        q.M = (int)(n - f0); q.N = q.M; q.K = 2 * NB;
-        q.alpha = -1.0; q.beta = 1.0; q.c_lower = 1;
-        GP2D_CHECK((launch_gemm<true, EPI_STORE>(q, 1, sb)));
+  // Delayed trailing updates over groups of G panels (potrf_schedule: G = 4 with a head/rest
+  // split; G = 2 unsplit is the round-3 schedule).  Group q = panels P..P+g−1 (panel P factored on entry;
+  // block columns P+1..P+g hold every panel < P):
+  //   crit  prefix: for r = P..P+g−1: block column r+1 ← panel r (skinny K = 128 update), then
+  //         factor(r+1) — the last one, block column P+g, is the next group's first panel and is
+  //         factored while the group's SYRK runs (one-column look-ahead);
+  //   aux:  as soon as panel r is final, block columns r+2..P+g ← panel r, so each column's
+  //         older panels arrive under the diagonal kernel of its predecessor (same-column
+  //         updates are ordered: crit waits for aux's last update of a column before its own);
+  //   bulk: once panel P+g−1 is final, columns ≥ P+g+1 ← panels P..P+g−1 in ONE K = 128·g SYRK —
+  //         g = 2 halves the launches and the C read-modify-write traffic per flop of K = 128
+  //         updates; g = 4 again (the tile runs 58 vs 51 TF/s at K = 512 than at 256, m = 32640,
+  //         profiles/r03_syrk_k512_ab.txt) — split (`split`) into a head, the next group's g
+  //         block columns, and the rest, so the next group's prefix (the chain of g−1 diagonal
+  //         blocks, during which the chip would otherwise idle) waits for the head only and runs
+  //         beside the rest.
+  // Regions: crit/aux write block columns ≤ P+g, the head columns P+g+1..P+2g, the rest the
+  // columns beyond; bulk is in order, so the rest of group q precedes the head of group q+1,
+  // which covers columns it also updates.
+  const PotrfSchedule ps = potrf_schedule(nb);
+  hipEvent_t e_head = e_syrk;   // with split: the head's event; the rest needs no event of its own
+  int P = 0;
+  while (P + 1 < nb) {
+    const int g = std::min(ps.G, nb - 1 - P);   // panels P..P+g−1, look-ahead column P+g ≤ nb−1
+    for (int r = P; r < P + g; ++r) {
+      // panel r is final (factored on crit; for r = P after the previous group's head / SYRK
+      // reached columns P+1..P+g, which crit waited for)
+      GP2D_EV(hipEventRecord(e_start, sc));
+      if (r + 2 <= P + g) {   // aux: columns r+2.., the next one first (crit waits for it at r+1)
+        GP2D_EV(hipStreamWaitEvent(sa, e_start, 0));
+        for (int c = r + 2; c <= P + g; ++c) {
+          GP2D_CHECK(colupdate(c, r, sa));
+          if (c == r + 2) GP2D_EV(hipEventRecord(e_auxc[c & 1], sa));
+        }
       }
-      GP2D_EV(hipEventRecord(e_syrk, sb));
-      GP2D_EV(hipStreamWaitEvent(sc, e_aux, 0));
-      GP2D_CHECK(colupdate(k + 2, k + 1, sc));
-      GP2D_CHECK(factor(k + 2));
-      // block column k+3 must have received this pair's SYRK before crit updates it
-      GP2D_EV(hipStreamWaitEvent(sc, e_syrk, 0));
-      k += 2;
-    } else {   // last block column: only panel k is outstanding
-      GP2D_CHECK(colupdate(k + 1, k, sc));
-      GP2D_CHECK(factor(k + 1));
-      k += 1;
+      if (r == P + g - 1) {   // the group's panels are final: its trailing update on bulk
+        GP2D_EV(hipEventRecord(e_pan, sc));
+        GP2D_EV(hipStreamWaitEvent(sb, e_pan, 0));
+        const int64_t f0 = (int64_t)(P + g + 1) * NB;
+        if (f0 < n) {
+          const int hw = ps.split ? std::min<int>(g, (int)((n - f0) / NB)) : 0;   // head block columns
+          GemmParams q = gemm_params();
+          q.lda = lda; q.ldb = lda; q.ldc = lda;
+          q.K = g * NB; q.alpha = -1.0; q.beta = 1.0;
+          if (hw > 0) {   // head: block columns [P+g+1, P+g+1+hw), every row below, lower tiles
+            q.A = A + f0 * lda + (int64_t)P * NB;
+            q.B = q.A;
+            q.C = A + f0 * lda + f0;
+            q.M = (int)(n - f0); q.N = hw * NB;
+            q.cyc_lower = 1; q.mask_off = 0;
+            GP2D_CHECK((launch_gemm<true, EPI_STORE>(q, 1, sb)));
+            GP2D_EV(hipEventRecord(e_head, sb));
+            q.cyc_lower = 0;
+          }
+          const int64_t f1 = f0 + (int64_t)hw * NB;
+          if (f1 < n) {   // the rest (or, unsplit, the whole trailing matrix): lower tiles
+            q.A = A + f1 * lda + (int64_t)P * NB;
+            q.B = q.A;
+            q.C = A + f1 * lda + f1;
+            q.M = (int)(n - f1); q.N = q.M; q.c_lower = 1;
+            GP2D_CHECK((launch_gemm<true, EPI_STORE>(q, 1, sb)));
+          }
+          if (hw == 0) GP2D_EV(hipEventRecord(e_head, sb));
+        } else {
+          GP2D_EV(hipEventRecord(e_head, sb));
+        }
+      }
+      // block column r+1 ≥ P+2 received panels P..r−1 on aux (the last of them recorded as the
+      // first update of batch r−1); the same-column updates must not overlap
+      if (r > P) GP2D_EV(hipStreamWaitEvent(sc, e_auxc[(r + 1) & 1], 0));
+      GP2D_CHECK(colupdate(r + 1, r, sc));
+      GP2D_CHECK(factor(r + 1));
     }
+    // the next group's columns P+g+1..P+2g must have received this group's head (the whole
+    // SYRK when unsplit) before crit or aux update them
+    GP2D_EV(hipStreamWaitEvent(sc, e_head, 0));
+    P += g;
   }
   GP2D_EV(hipEventRecord(e_join, sb));
   GP2D_EV(hipStreamWaitEvent(sc, e_join, 0));

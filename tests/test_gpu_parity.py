@@ -4,6 +4,8 @@ Tolerances (north_star): fp64 posterior mean / variance within 1e-10 relative,
 measured normwise (max |a−b| / max |b|) per output vector; covariance entries
 within 1e-13 relative to the matrix max-norm.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -212,3 +214,53 @@ def test_jitchol_retry(variance):
     assert torch.equal(a[1], b[1]) or variance == "ozaki"   # (the ozaki CRT may poison both alike: NaN ≠ NaN)
     # a well-posed fit reports no jitter
     assert E.fit(ks, x[:60], y[:120], noise=0.01, variance=variance, jitchol=5).extra["jitchol"] == 0.0
+
+
+_SCHED_CHILD = r'''
+import ctypes, hashlib, json, sys
+import numpy as np, torch
+sys.path[:0] = sys.argv[2:4]
+from gp2d import _native as N
+L_ = N.lib()
+out = {}
+for n in json.loads(sys.argv[1]):
+    rng = np.random.default_rng(n)
+    X = rng.normal(size=(n, n))
+    K = X @ X.T / n + np.eye(n) * 0.5
+    A = torch.tensor(K, device="cuda")
+    dinv = torch.empty((n // 128, 128, 128), dtype=torch.float64, device="cuda")
+    info = torch.zeros(1, dtype=torch.int32, device="cuda")
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())
+    N.check(L_.gp2d_potrf(P(A), n, n, P(dinv), P(info), None, 0, s), "potrf")
+    Lg = A.cpu().numpy()
+    Lr = np.linalg.cholesky(K)
+    out[n] = dict(info=int(info.item()), upper=float(np.abs(np.triu(Lg, 1)).max()),
+                  rel=float(np.abs(Lg - Lr).max() / np.abs(Lr).max()),
+                  sha=hashlib.sha256(Lg.tobytes()).hexdigest())
+print(json.dumps(out))
+'''
+
+
+def test_potrf_trailing_schedules():
+    """Every trailing-update schedule of potrf_impl — pairs (K = 256), four panels (K = 512)
+    and four panels with the head/rest split (the large-n default) — against LAPACK at block
+    counts 1, 2, 3, 5, 9, 21 (ragged last groups); the split changes no bits (each tile gets
+    the same K = 512 sum, only in another launch)."""
+    import json
+    import subprocess
+    import sys
+    from conftest import PKG, ROOT
+    sizes = [128, 256, 384, 640, 1152, 2688]
+    res = {}
+    for G, split in [(2, 0), (4, 0), (4, 1)]:
+        env = dict(os.environ, GP2D_POTRF_G=str(G), GP2D_POTRF_SPLIT=str(split))
+        out = subprocess.run([sys.executable, "-c", _SCHED_CHILD, json.dumps(sizes), ROOT, PKG], env=env,
+                             capture_output=True, text=True, timeout=120)
+        assert out.returncode == 0, out.stderr[-2000:]
+        res[(G, split)] = json.loads(out.stdout.strip().splitlines()[-1])
+        for n, r in res[(G, split)].items():
+            assert r["info"] == 0 and r["upper"] == 0.0, (G, split, n, r)
+            assert r["rel"] < 1e-13, (G, split, n, r)
+    for n in map(str, sizes):
+        assert res[(4, 0)][n]["sha"] == res[(4, 1)][n]["sha"], n
