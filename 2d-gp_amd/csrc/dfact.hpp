@@ -1,32 +1,45 @@
 // dfact.hpp — device helpers of the distributed factor (one job's POTRF + TRTRI over several
 // GPUs; host side gp2d.hip gp2d_dfact_*, gp2d/distributed.py fit_distributed).
 //
-// 1-D block-cyclic by 256-column super-blocks: rank s mod P owns super-column s.  Every rank
+// 1-D block-cyclic by 512-column super-blocks: rank s mod P owns super-column s.  Every rank
 // holds the whole n×n K_y but reads and writes only its own super-columns, which end up holding
 // W = L⁻¹ (right-looking TRTRI fused into the right-looking POTRF: at step s every rank applies
 // the broadcast panel [D_s = L_ss⁻¹; L21] to its trailing K_y columns AND to its W columns
-// J ≤ s: X[s] = D_s·R[s], R[t>s] −= L[t,s]·X[s]).  The GEMMs run on gemm_f64_kernel with
+// J ≤ s: X[s] = D_s·R[s] (out of place, D_s = L_ss⁻¹ shipped in the panel), R[t>s] −= L[t,s]·X[s]).  The GEMMs run on gemm_f64_kernel with
 // block-cyclic column tiles (GemmParams::jgrp / jstep / cyc_lower).
 #pragma once
 #include "common.hpp"
 
 namespace gp2d {
 
-constexpr int DF_SB = 256;   // super-block width (two 128-wide GEMM tiles)
+constexpr int DF_SB = 512;           // super-block width: four 128-wide GEMM tiles, so every
+constexpr int DF_SBT = DF_SB / 128;  // trailing update is a K = 512 product (the SYRK tile runs
+                                     // 58 vs 51 TF/s at K = 512 than at K = 256)
 
 // Column block s of A becomes the s-th block column of the identity (rows of the super-block:
 // I, every other row: 0): the TRTRI's initial right-hand side R[:, s] = E_s, written once the
-// owner has read its K_y panel.  One thread per element pair, two rows per workgroup.
-__global__ __launch_bounds__(256) void dfact_reset_col_kernel(double* __restrict__ A, int64_t n, int64_t lda,
-                                                              int64_t c0) {
-  const int64_t i = 2 * (int64_t)blockIdx.x + (threadIdx.x >> 7);
-  const int c = 2 * (int)(threadIdx.x & 127);
+// owner has read its K_y panel.  One row per workgroup, one element pair per thread.
+__global__ __launch_bounds__(DF_SB / 2) void dfact_reset_col_kernel(double* __restrict__ A, int64_t n, int64_t lda,
+                                                                    int64_t c0) {
+  const int64_t i = blockIdx.x;
+  const int c = 2 * (int)threadIdx.x;
   if (i >= n) return;
   const int64_t r = i - c0;             // row within the super-block, if any
   d2 v;
   v.x = (r == c) ? 1.0 : 0.0;
   v.y = (r == c + 1) ? 1.0 : 0.0;
   *reinterpret_cast<d2*>(A + i * lda + c0 + c) = v;
+}
+
+// X[i][col] = T[i][col] for the DF_SB rows of a super-block and this rank's owned super-columns
+// (the q-th at column (first + q·P)·DF_SB): the out-of-place TRTRI step's result copied back.
+// One workgroup per (owned super-column, row), one element pair per thread.
+__global__ __launch_bounds__(DF_SB / 2) void dfact_copy_owned_kernel(const double* __restrict__ T, int64_t ldt,
+                                                                     double* __restrict__ X, int64_t ldx, int first,
+                                                                     int P) {
+  const int64_t col = (int64_t)(first + (int)blockIdx.x * P) * DF_SB + 2 * threadIdx.x;
+  const int64_t i = blockIdx.y;
+  *reinterpret_cast<d2*>(X + i * ldx + col) = *reinterpret_cast<const d2*>(T + i * ldt + col);
 }
 
 // A failed diagonal block reports its local leading-minor order in *tmp; the first failure

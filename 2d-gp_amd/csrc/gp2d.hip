@@ -443,7 +443,8 @@ namespace {
 // GP2D_POTRF_G (2 | 4 | 8) / GP2D_POTRF_SPLIT override the choice (measurement only).
 struct PotrfSchedule { int G; bool split; };
 PotrfSchedule potrf_schedule(int nb) {
-  PotrfSchedule ps{nb > 0 ? 4 : 2, true};
+  (void)nb;
+  PotrfSchedule ps{4, true};
   static const char* eg = std::getenv("GP2D_POTRF_G");
   static const char* es = std::getenv("GP2D_POTRF_SPLIT");
   if (eg && (std::atoi(eg) == 2 || std::atoi(eg) == 4 || std::atoi(eg) == 8)) ps.G = std::atoi(eg);
@@ -694,30 +695,37 @@ int gp2d_trtri(double* A, int64_t n, int64_t lda, const double* dinv, void* work
 }
 
 // ------------------------------------------------------------------------ distributed factor
-// One job's POTRF + TRTRI over P ranks (dfact.hpp): 256-column super-blocks dealt block-
+// One job's POTRF + TRTRI over P ranks (dfact.hpp): 512-column super-blocks dealt block-
 // cyclically, a panel broadcast per step by the caller.  Every GEMM below is gemm_f64_kernel;
 // the per-element arithmetic does not depend on P (each tile sums the same K range in the same
 // order), so any P gives the bits of P = 1.
+int gp2d_dfact_sb(void) { return DF_SB; }
+
 size_t gp2d_dfact_panel_doubles(int64_t n) { return (size_t)(n > 0 ? n : 0) * DF_SB; }
 
-size_t gp2d_dfact_workspace(int64_t) {
-  // the two 128×128 inverse diagonal blocks of a super-block and one int
-  return (size_t)2 * NB * NB * sizeof(double) + 64;
+// workspace layout (doubles): the DF_SBT inverted 128×128 diagonal blocks | an int status
+// word (64 B) | the head's TRTRI buffers (T, T2) | the TRTRI step's out-of-place X[s]
+// (DF_SB rows × n, at A's column positions)
+static size_t dfact_ws_dinv() { return (size_t)DF_SBT * NB * NB; }
+static size_t dfact_ws_trtri() { return trtri_t_doubles(DF_SBT) + trtri_split_doubles(DF_SBT) + 8; }
+size_t gp2d_dfact_workspace(int64_t n) {
+  return (dfact_ws_dinv() + 8 + dfact_ws_trtri() + (size_t)DF_SB * (size_t)(n > 0 ? n : 0)) * sizeof(double);
 }
 
 static int dfact_args(const double* A, int64_t n, int64_t lda, int s) {
   GP2D_REQUIRE(A != nullptr, "dfact: NULL matrix");
-  GP2D_REQUIRE(n > 0 && n % DF_SB == 0, "dfact: n must be a positive multiple of 256");
+  GP2D_REQUIRE(n > 0 && n % DF_SB == 0, "dfact: n must be a positive multiple of 512");
   GP2D_REQUIRE(n <= INT32_MAX && lda >= n && lda % 2 == 0, "dfact: lda must be >= n and even");
   GP2D_REQUIRE(s >= 0 && (int64_t)s * DF_SB < n, "dfact: super-block index out of range");
   return 0;
 }
 
-// Owner's step: super-column s (rows s·256..n) factored on ONE stream — diagonal block 0,
-// its panel TRSM down to row n, the column update of sub-column 1 by sub-column 0, diagonal
-// block 1, its panel TRSM — then copied into the panel buffer with the head's diagonal blocks
-// replaced by their inverses: head = [[D0, ·], [L10, D1]] (D_i = L_ii⁻¹; the upper right block
-// is never read).  Receivers apply D_s = L_ss⁻¹ as D0, then L10, then D1 (gp2d_dfact_invstep).
+// Owner's step: super-column s (rows s·512..n) factored on ONE stream, a right-looking
+// Cholesky over its four 128-wide sub-columns — diagonal block j (Cholesky + inverse D_j),
+// its panel TRSM down to row n, the updates of sub-columns j+1..3 by sub-column j — then
+// copied into the panel buffer with its 512×512 head replaced by D_s = L_ss⁻¹ (the diagonal
+// blocks D_j put in, the off-diagonal blocks by the in-place recursive-doubling TRTRI on the
+// head).  Receivers apply D_s in one K = 512 product (gp2d_dfact_invstep).
 int gp2d_dfact_panel(double* A, int64_t n, int64_t lda, int s, double* panel, int* info_dev, void* work,
                      size_t work_bytes, void* stream) {
   GP2D_CHECK(dfact_args(A, n, lda, s));
@@ -726,34 +734,38 @@ int gp2d_dfact_panel(double* A, int64_t n, int64_t lda, int s, double* panel, in
   hipStream_t st = S(stream);
   const int64_t s0 = (int64_t)s * DF_SB;
   double* As = A + s0 * lda + s0;                  // the super-column from its diagonal down
-  const int64_t rows = n - s0;                     // ≥ 256
-  double* dinv = static_cast<double*>(work);       // [2][128][128]
-  int* tmp = reinterpret_cast<int*>(dinv + 2 * NB * NB);
+  const int64_t rows = n - s0;                     // ≥ 512
+  double* dinv = static_cast<double*>(work);       // [DF_SBT][128][128]
+  int* tmp = reinterpret_cast<int*>(dinv + dfact_ws_dinv());
+  double* T = dinv + dfact_ws_dinv() + 8;
+  double* T2 = T + trtri_t_doubles(DF_SBT);
   GP2D_EV(hipMemsetAsync(tmp, 0, sizeof(int), st));
-  potrf_diag_kernel<<<1, 256, 0, st>>>(As, lda, 0, dinv, tmp, 0);
-  GP2D_CHECK(check_launch("potrf_diag_kernel"));
-  double* P0 = As + (int64_t)NB * lda;             // rows below diagonal block 0, sub-column 0
-  gemm_f64_panel_kernel<<<(unsigned)((rows - NB) / PNL_R), 256, 0, st>>>(P0, lda, dinv, NB, P0, lda, 1.0, 0.0);
-  GP2D_CHECK(check_launch("gemm_f64_panel_kernel"));
-  double* C1 = P0 + NB;                            // sub-column 1 from row s0 + 128 down
-  gemm_f64_panel_kernel<<<(unsigned)((rows - NB) / PNL_R), 256, 0, st>>>(P0, lda, P0, lda, C1, lda, -1.0, 1.0);
-  GP2D_CHECK(check_launch("gemm_f64_panel_kernel"));
-  potrf_diag_kernel<<<1, 256, 0, st>>>(As, lda, NB, dinv, tmp, 0);
-  GP2D_CHECK(check_launch("potrf_diag_kernel"));
-  if (rows > DF_SB) {
-    double* P1 = C1 + (int64_t)NB * lda;           // rows below diagonal block 1, sub-column 1
-    gemm_f64_panel_kernel<<<(unsigned)((rows - DF_SB) / PNL_R), 256, 0, st>>>(P1, lda, dinv + NB * NB, NB, P1, lda,
-                                                                             1.0, 0.0);
+  for (int j = 0; j < DF_SBT; ++j) {
+    const int64_t c0 = (int64_t)j * NB;
+    potrf_diag_kernel<<<1, 256, 0, st>>>(As, lda, (int)c0, dinv, tmp, 0);
+    GP2D_CHECK(check_launch("potrf_diag_kernel"));
+    const int64_t below = rows - c0 - NB;
+    if (below <= 0) continue;
+    double* Pj = As + (c0 + NB) * lda + c0;        // sub-column j below its diagonal block
+    gemm_f64_panel_kernel<<<(unsigned)(below / PNL_R), 256, 0, st>>>(Pj, lda, dinv + j * NB * NB, NB, Pj, lda,
+                                                                    1.0, 0.0);
     GP2D_CHECK(check_launch("gemm_f64_panel_kernel"));
+    for (int j2 = j + 1; j2 < DF_SBT; ++j2) {      // sub-column j2 (rows ≥ its diagonal) −= L_j · L_j[j2 rows]ᵀ
+      const int64_t r2 = (int64_t)j2 * NB;
+      const double* Lp = As + r2 * lda + c0;
+      gemm_f64_panel_kernel<<<(unsigned)((rows - r2) / PNL_R), 256, 0, st>>>(Lp, lda, Lp, lda, As + r2 * lda + r2,
+                                                                            lda, -1.0, 1.0);
+      GP2D_CHECK(check_launch("gemm_f64_panel_kernel"));
+    }
   }
   dfact_info_kernel<<<1, 64, 0, st>>>(info_dev, tmp, s0);
   GP2D_CHECK(check_launch("dfact_info_kernel"));
   GP2D_EV(hipMemcpy2DAsync(panel, DF_SB * sizeof(double), As, lda * sizeof(double), DF_SB * sizeof(double), rows,
                            hipMemcpyDeviceToDevice, st));
-  for (int b = 0; b < 2; ++b)
-    GP2D_EV(hipMemcpy2DAsync(panel + (int64_t)b * NB * DF_SB + b * NB, DF_SB * sizeof(double), dinv + b * NB * NB,
-                             NB * sizeof(double), NB * sizeof(double), NB, hipMemcpyDeviceToDevice, st));
-  return 0;
+  // head: D_j on the diagonal, then W[R, L] = −W[R, R]·(L[R, L]·W[L, L]) level by level
+  put_diag_blocks_kernel<<<dim3(NB * NB / 256, DF_SBT), 256, 0, st>>>(panel, DF_SB, dinv);
+  GP2D_CHECK(check_launch("put_diag_blocks_kernel"));
+  return trtri_levels(panel, DF_SB, DF_SBT, T, T2, st);
 }
 
 // first owned super-column ≥ t (rank r of P), and how many owned ones lie in [t, t_hi)
@@ -771,7 +783,7 @@ int gp2d_dfact_update(double* A, int64_t n, int64_t lda, int s, const double* pa
   int first, count;
   dfact_owned(std::max(t_lo, s + 1), std::min(t_hi, nsb), nranks, rank, first, count);
   if (count == 0) return 0;
-  // A[rows ≥ t·256, t] −= L21[t rows..] · L21[t block]ᵀ for the owned t, lower tiles only
+  // A[rows ≥ t·512, t] −= L21[t rows..] · L21[t block]ᵀ for the owned t, lower tiles only (K = 512)
   const int64_t r0 = (int64_t)(s + 1) * DF_SB;
   const double* L21 = panel + (int64_t)DF_SB * DF_SB;   // global row r0 + i at panel row i
   GemmParams q = gemm_params();
@@ -780,57 +792,53 @@ int gp2d_dfact_update(double* A, int64_t n, int64_t lda, int s, const double* pa
   q.C = A + r0 * lda + (int64_t)first * DF_SB; q.ldc = lda;
   q.M = (int)(n - r0); q.N = count * DF_SB; q.K = DF_SB;
   q.alpha = -1.0; q.beta = 1.0;
-  q.jgrp = DF_SB / GBN; q.jstep = nranks;
-  q.cyc_lower = 1; q.mask_off = 2 * (s + 1) - 2 * first;
+  q.jgrp = DF_SBT; q.jstep = nranks;
+  q.cyc_lower = 1; q.mask_off = DF_SBT * (s + 1) - DF_SBT * first;
   return launch_gemm<true, EPI_STORE>(q, 1, S(stream));
 }
 
 int gp2d_dfact_invstep(double* A, int64_t n, int64_t lda, int s, const double* panel, int nranks, int rank,
-                       void* stream) {
+                       void* work, size_t work_bytes, void* stream) {
   GP2D_CHECK(dfact_args(A, n, lda, s));
   GP2D_REQUIRE(panel != nullptr, "dfact_invstep: NULL panel");
   GP2D_REQUIRE(nranks >= 1 && rank >= 0 && rank < nranks, "dfact_invstep: bad rank / world size");
+  GP2D_REQUIRE(work != nullptr && work_bytes >= gp2d_dfact_workspace(n), "dfact_invstep: workspace too small");
   hipStream_t st = S(stream);
   const int64_t s0 = (int64_t)s * DF_SB;
   if (s % nranks == rank) {   // this rank's W column block s starts as the identity block column
-    dfact_reset_col_kernel<<<(unsigned)((n + 1) / 2), 256, 0, st>>>(A, n, lda, s0);
+    dfact_reset_col_kernel<<<(unsigned)n, DF_SB / 2, 0, st>>>(A, n, lda, s0);
     GP2D_CHECK(check_launch("dfact_reset_col_kernel"));
   }
   int first, count;
   dfact_owned(0, s + 1, nranks, rank, first, count);
   if (count == 0) return 0;
-  double* Xs = A + s0 * lda + (int64_t)first * DF_SB;   // rows of super-block s, owned columns ≤ s
-  auto cyc = [&](GemmParams& q) { q.jgrp = DF_SB / GBN; q.jstep = nranks; };
-  // X[s] = D_s · R[s] with D_s = [[D0, 0], [−D1·L10·D0, D1]], as a block forward substitution:
-  // X_lo = D0·R_lo, R_hi −= L10·X_lo, X_hi = D1·R_hi.  The in-place products are one 128-row tile
-  // per column tile, which reads its whole K range before it stores.
-  auto prod = [&](const double* Aop, double* Bc, double alpha, double beta, double* Cc) -> int {
+  // X[s] = D_s · R[s] out of place into Xt (DF_SB × n, A's column positions; D_s lower: row
+  // block i reads k < 128(i+1)), then R[t > s] −= L21 · X[s] from Xt, then Xt → X[s]
+  double* Xt = static_cast<double*>(work) + dfact_ws_dinv() + 8 + dfact_ws_trtri();
+  double* Xs = A + s0 * lda;
+  auto cyc = [&](GemmParams& q) { q.jgrp = DF_SBT; q.jstep = nranks; };
+  {
     GemmParams q = gemm_params();
-    q.A = Aop; q.lda = DF_SB;
-    q.B = Bc; q.ldb = lda;
-    q.C = Cc; q.ldc = lda;
-    q.M = NB; q.N = count * DF_SB; q.K = NB;
-    q.alpha = alpha; q.beta = beta;
+    q.A = panel; q.lda = DF_SB;
+    q.B = Xs + (int64_t)first * DF_SB; q.ldb = lda;
+    q.C = Xt + (int64_t)first * DF_SB; q.ldc = n;
+    q.M = DF_SB; q.N = count * DF_SB; q.K = DF_SB; q.a_lower = 1;
     cyc(q);
-    return launch_gemm<false, EPI_STORE>(q, 1, st);
-  };
-  double* Xlo = Xs;
-  double* Xhi = Xs + (int64_t)NB * lda;
-  GP2D_CHECK(prod(panel, Xlo, 1.0, 0.0, Xlo));                                   // D0
-  GP2D_CHECK(prod(panel + (int64_t)NB * DF_SB, Xlo, -1.0, 1.0, Xhi));            // L10
-  GP2D_CHECK(prod(panel + (int64_t)NB * DF_SB + NB, Xhi, 1.0, 0.0, Xhi));       // D1
+    GP2D_CHECK((launch_gemm<false, EPI_STORE>(q, 1, st)));
+  }
   const int64_t rows = n - s0 - DF_SB;
   if (rows > 0) {   // R[t > s] −= L21 · X[s]
     GemmParams q = gemm_params();
     q.A = panel + (int64_t)DF_SB * DF_SB; q.lda = DF_SB;
-    q.B = Xs; q.ldb = lda;
-    q.C = Xs + (int64_t)DF_SB * lda; q.ldc = lda;
+    q.B = Xt + (int64_t)first * DF_SB; q.ldb = n;
+    q.C = Xs + (int64_t)DF_SB * lda + (int64_t)first * DF_SB; q.ldc = lda;
     q.M = (int)rows; q.N = count * DF_SB; q.K = DF_SB;
     q.alpha = -1.0; q.beta = 1.0;
     cyc(q);
     GP2D_CHECK((launch_gemm<false, EPI_STORE>(q, 1, st)));
   }
-  return 0;
+  dfact_copy_owned_kernel<<<dim3((unsigned)count, DF_SB), DF_SB / 2, 0, st>>>(Xt, n, Xs, lda, first, nranks);
+  return check_launch("dfact_copy_owned_kernel");
 }
 
 int gp2d_copy2d(double* dst, int64_t ldd, const double* src, int64_t lds, int64_t rows, int64_t cols,

@@ -12,7 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GP2D_LIB", os.path.join(_HERE, "libgp2d.so"))
-ABI_VERSION = 6          # GP2D_ABI_VERSION in include/gp2d.h
+ABI_VERSION = 7          # GP2D_ABI_VERSION in include/gp2d.h
 
 FAMILY_VECTOR2D, FAMILY_ARD_RBF, FAMILY_VECTOR_ST = 0, 1, 2
 KIND_SCALAR, KIND_DIVFREE, KIND_CURLFREE, KIND_MIXED = 0, 1, 2, 3
@@ -31,7 +31,7 @@ EXPORTS = (
     "gp2d_lml_grad_workspace", "gp2d_lml_grad",
     "gp2d_kernel_grad_count", "gp2d_kernel_grad_workspace", "gp2d_kernel_grad",
     "gp2d_gemm", "gp2d_transpose", "gp2d_bcast",
-    "gp2d_dfact_panel_doubles", "gp2d_dfact_workspace", "gp2d_dfact_panel", "gp2d_dfact_update",
+    "gp2d_dfact_sb", "gp2d_dfact_panel_doubles", "gp2d_dfact_workspace", "gp2d_dfact_panel", "gp2d_dfact_update",
     "gp2d_dfact_invstep", "gp2d_copy2d", "gp2d_zero_upper", "gp2d_pack_lower_doubles", "gp2d_pack_lower",
     "gp2d_timing_enable", "gp2d_timing_read", "gp2d_last_error",
 )
@@ -113,11 +113,12 @@ _SIGS = {
     "gp2d_gemm": (_I, [_I, _I64, _I64, _I64, _D, _P, _I64, _P, _I64, _D, _P, _I64, _P]),
     "gp2d_transpose": (_I, [_P, _I64, _I64, _P, _P]),
     "gp2d_bcast": (_I, [_P, _SZ, _I, _P, _P]),
+    "gp2d_dfact_sb": (_I, []),
     "gp2d_dfact_panel_doubles": (_SZ, [_I64]),
     "gp2d_dfact_workspace": (_SZ, [_I64]),
     "gp2d_dfact_panel": (_I, [_P, _I64, _I64, _I, _P, _P, _P, _SZ, _P]),
     "gp2d_dfact_update": (_I, [_P, _I64, _I64, _I, _P, _I, _I, _I, _I, _P]),
-    "gp2d_dfact_invstep": (_I, [_P, _I64, _I64, _I, _P, _I, _I, _P]),
+    "gp2d_dfact_invstep": (_I, [_P, _I64, _I64, _I, _P, _I, _I, _P, _SZ, _P]),
     "gp2d_copy2d": (_I, [_P, _I64, _P, _I64, _I64, _I64, _P]),
     "gp2d_zero_upper": (_I, [_P, _I64, _I64, _P]),
     "gp2d_pack_lower_doubles": (_SZ, [_I64]),

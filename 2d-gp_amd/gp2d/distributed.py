@@ -168,7 +168,20 @@ def fit_sharded(spec: E.KernelSpec, x, y, noise: float, device, mode: str = "bca
     return gp
 
 
-SB = 256   # super-block width of the distributed factor (csrc/dfact.hpp DF_SB)
+def super_block() -> int:
+    """Super-block width of the distributed factor (csrc/dfact.hpp DF_SB, gp2d_dfact_sb)."""
+    return int(E.N.lib().gp2d_dfact_sb())
+
+
+def dfact_layout(spec: E.KernelSpec, n_train: int):
+    """(padded point count, matrix order n) of a distributed fit: engine.fit's ozaki layout with
+    n rounded up to a multiple of the super-block (the padded points add identity rows)."""
+    sb = super_block()
+    npad, n = E.fit_layout(spec, n_train, "ozaki")
+    bd = spec.block_dim
+    step = max(1, sb // bd)
+    npad = (npad + step - 1) // step * step
+    return npad, bd * npad
 
 
 def _owned_blocks(nsb: int, ws: int, r: int):
@@ -181,7 +194,7 @@ def fit_distributed(spec: E.KernelSpec, x, y, noise: float, device=None, varianc
     """ONE job's fit spread over all ranks (the config-D single job: /root/reference/krig.py:541-557
     predicts one model's large grid): every rank assembles K_y, then a 1-D block-cyclic POTRF
     fused with the right-looking TRTRI (include/gp2d.h gp2d_dfact_*) — rank s mod P factors
-    super-column s (256 wide), broadcasts the panel [L_ss⁻¹; L21] (torch.distributed: RCCL under
+    super-column s (512 wide), broadcasts the panel [L_ss⁻¹; L21] (torch.distributed: RCCL under
     'nccl'), and every rank applies it to its own K_y columns (POTRF trailing update) and to its
     own W = L⁻¹ columns (TRTRI step).  The owned W columns are then all-gathered (lower parts only,
     ≈ n²/2 doubles in all), so every rank ends with the full W, α and the ozaki residue planes,
@@ -216,7 +229,8 @@ def fit_distributed(spec: E.KernelSpec, x, y, noise: float, device=None, varianc
     ntr = X.shape[0]
     if ntr < 1:
         raise ValueError("need at least one training point")
-    npad, n = E.fit_layout(spec, ntr, "ozaki")   # n a multiple of 256 (the super-block)
+    npad, n = dfact_layout(spec, ntr)   # n a multiple of the super-block
+    SB = super_block()
     if variance == "ozaki" and n >= 131072:
         raise ValueError(f"the ozaki variance engine supports n < 131072; got n = {n}")
     perm = None
@@ -275,7 +289,7 @@ def fit_distributed(spec: E.KernelSpec, x, y, noise: float, device=None, varianc
         E.N.check(L.gp2d_dfact_update(P(A), n, n, s, P(buf), ws, rank, rest_lo, nsb, sh), "gp2d_dfact_update")
         if not lookahead and nxt < nsb and nxt % ws == rank:
             factor(nxt)
-        E.N.check(L.gp2d_dfact_invstep(P(A), n, n, s, P(buf), ws, rank, sh), "gp2d_dfact_invstep")
+        E.N.check(L.gp2d_dfact_invstep(P(A), n, n, s, P(buf), ws, rank, P(work), wbytes, sh), "gp2d_dfact_invstep")
         ev = torch.cuda.Event()
         ev.record(main)
         done[s] = ev
@@ -321,8 +335,9 @@ def allreduce_first_failure(info: torch.Tensor) -> torch.Tensor:
 
 def _allgather_w_columns(A: torch.Tensor, n: int, ws: int, rank: int, dev):
     """Every rank's W super-columns to every rank: super-column t travels as its rows
-    [256·t, n) (the part below the diagonal block's top; W is zero above it)."""
+    [SB·t, n) (the part below the diagonal block's top; W is zero above it)."""
     L = E.N.lib()
+    SB = super_block()
     P, sh = E._ptr, E._stream_handle(dev)
     nsb = n // SB
     sizes = [sum((n - t * SB) * SB for t in _owned_blocks(nsb, ws, r)) for r in range(ws)]

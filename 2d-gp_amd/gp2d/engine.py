@@ -519,6 +519,22 @@ class Predictor:
         else:
             self.wbytes = int(N.lib().gp2d_predict_workspace(gp.n, self.chunk, bd))
         self.work = torch.empty(self.wbytes // 8 + 1, dtype=torch.float64, device=gp.device)
+        self._grid = None   # (the caller's grid tensor, its version, Morton order, the grid in that order)
+
+    def _grid_order(self, xg, G: torch.Tensor):
+        """Morton order of the grid and the grid in that order.  A job stream predicts the same
+        device grid job after job (the reference's per-window krig.predict on one grid): for the
+        same tensor object, unmodified since (its version counter), the order of the previous call
+        is reused — the tensor is held, so its memory cannot be reused by another grid."""
+        c = self._grid
+        st = torch.cuda.current_stream(G.device)
+        if isinstance(xg, torch.Tensor) and c is not None and c[0] is xg and c[1] == xg._version \
+                and c[3].shape == G.shape and c[4] == st:   # made on this stream: ordered before
+            return c[2], c[3]
+        order = morton_order(G)
+        Gs = G[order].contiguous()
+        self._grid = (xg, xg._version, order, Gs, st) if isinstance(xg, torch.Tensor) and xg.is_cuda else None
+        return order, Gs
 
     def fits(self, gp: GPFit) -> bool:
         """True if this workspace serves `gp` as is: same matrix order, engine and block size
@@ -552,8 +568,10 @@ class Predictor:
             order = None
             Gs, ms, vs = G, mean, var
             if compute_var and m > 1:
-                order = planes.order if use_planes else morton_order(G)
-                Gs = planes.xg if use_planes else G[order].contiguous()
+                if use_planes:
+                    order, Gs = planes.order, planes.xg
+                else:
+                    order, Gs = self._grid_order(xg, G)
                 ms = torch.empty(bd * m, dtype=torch.float64, device=gp.device)
                 vs = torch.empty(bd * m, dtype=torch.float64, device=gp.device)
             rc = -3

@@ -303,7 +303,7 @@ def single_job_distributed(args, ws, spec, xt, yt, noise, xg, m_all, dev, pred_c
         dist.all_reduce(dts, op=dist.ReduceOp.MAX)
     ms = 1e3 * float(dts[0].item()) / reps
     return {"ms": ms, "value": m_all / (ms * 1e-3), "reps": reps, "fit_ms": 1e3 * float(dts[1].item()),
-            "fit": f"distributed.fit_distributed over {ws} rank(s): 256-column block-cyclic POTRF + TRTRI, "
+            "fit": f"distributed.fit_distributed over {ws} rank(s): 512-column block-cyclic POTRF + TRTRI, "
                    "panel broadcasts, W columns all-gathered"}
 
 

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define GP2D_ABI_VERSION 6
+#define GP2D_ABI_VERSION 7
 
 /* kernel families */
 #define GP2D_FAMILY_VECTOR2D 0   /* 2×2 matrix-valued SE kernels on (x1, x2)          */
@@ -262,20 +262,23 @@ int gp2d_transpose(const double* A, int64_t n, int64_t lda, double* At, void* st
 /* ---- multi-GPU: one job's factor over P GPUs -----------
  * Replaces, for one large job, the single-GPU gp2d_potrf + gp2d_trtri pair (np.linalg.inv,
  * GP_laser.py:118; the factor of GPy's GPRegression inside krig.py:411 / :541-557, whose
- * D-sized grid the reference predicts slice by slice).  1-D block-cyclic over 256-column
- * super-blocks: rank s mod P owns super-column s.  Every rank holds the whole n×n K_y
- * (n a multiple of 256, assembled by gp2d_assemble) and touches only its own super-columns;
- * the caller broadcasts one panel per step (any transport: RCCL, gloo, gp2d_bcast).  Step s:
+ * D-sized grid the reference predicts slice by slice).  1-D block-cyclic over SB-column
+ * super-blocks (SB = gp2d_dfact_sb() = 512): rank s mod P owns super-column s.  Every rank
+ * holds the whole n×n K_y (n a multiple of SB, assembled by gp2d_assemble) and touches only
+ * its own super-columns; the caller broadcasts one panel per step (any transport: RCCL,
+ * gloo, gp2d_bcast).  Step s:
  *   owner of s:  gp2d_dfact_panel(A, n, lda, s, panel, info, work, ...)
- *                → panel = [D_s = L_ss⁻¹ (256×256, lower); L21 = L[(s+1)·256.., s] ((n−s·256−256)×256)],
- *                  row-major with leading dim 256, gp2d_dfact_panel_doubles(n) doubles at most;
+ *                → panel = [D_s = L_ss⁻¹ (SB×SB, lower); L21 = L[(s+1)·SB.., s] ((n−s·SB−SB)×SB)],
+ *                  row-major with leading dim SB, gp2d_dfact_panel_doubles(n) doubles at most;
  *                  *info_dev (device int) receives the global order of a non-PD minor (LAPACK style);
- *   broadcast the first (n − 256·s)·256 doubles of `panel` from rank s mod P;
+ *   broadcast the first (n − SB·s)·SB doubles of `panel` from rank s mod P;
  *   every rank:  gp2d_dfact_update(A, n, lda, s, panel, P, rank, t_lo, t_hi, ...)
- *                  POTRF trailing update of the owned super-columns t ∈ [max(t_lo, s+1), t_hi)
+ *                  POTRF trailing update (K = SB) of the owned super-columns t ∈ [max(t_lo, s+1), t_hi)
  *                  (the next owner updates t = s+1 first, a look-ahead);
- *                gp2d_dfact_invstep(A, n, lda, s, panel, P, rank, ...)
- *                  TRTRI step: the owned W columns J ≤ s (column block s reset to E_s first).
+ *                gp2d_dfact_invstep(A, n, lda, s, panel, P, rank, work, work_bytes, ...)
+ *                  TRTRI step: the owned W columns J ≤ s (column block s reset to E_s first):
+ *                  X[s] = D_s·R[s] and R[t > s] −= L21·X[s], both K = SB products; `work` as for
+ *                  gp2d_dfact_panel (gp2d_dfact_workspace(n) bytes, ≈ SB·n doubles).
  * After the last step every owned super-column holds its columns of W = L⁻¹, zero above its
  * diagonal block.  Per-element arithmetic is independent of P (P = 2 gives the bits of P = 1).
  * gp2d_copy2d: dst[rows×cols] = src (leading dims in doubles; hipMemcpy2DAsync) — the panel and
@@ -285,6 +288,7 @@ int gp2d_transpose(const double* A, int64_t n, int64_t lda, double* At, void* st
  *   rb of the lower-triangular n×n W keeps columns [0, 128·(rb+1)), blocks stored one after the
  *   other (gp2d_pack_lower_doubles(n) = 128²·nb(nb+1)/2 doubles, ≈ n²/2); unpack = 1 writes them
  *   back (the rest of W is left as it is).                                                  */
+int gp2d_dfact_sb(void);
 size_t gp2d_dfact_panel_doubles(int64_t n);
 size_t gp2d_dfact_workspace(int64_t n);
 int gp2d_dfact_panel(double* A, int64_t n, int64_t lda, int s, double* panel, int* info_dev, void* work,
@@ -292,7 +296,7 @@ int gp2d_dfact_panel(double* A, int64_t n, int64_t lda, int s, double* panel, in
 int gp2d_dfact_update(double* A, int64_t n, int64_t lda, int s, const double* panel, int nranks, int rank,
                       int t_lo, int t_hi, void* stream);
 int gp2d_dfact_invstep(double* A, int64_t n, int64_t lda, int s, const double* panel, int nranks, int rank,
-                       void* stream);
+                       void* work, size_t work_bytes, void* stream);
 int gp2d_copy2d(double* dst, int64_t ldd, const double* src, int64_t lds, int64_t rows, int64_t cols,
                 void* stream);
 int gp2d_zero_upper(double* A, int64_t n, int64_t lda, void* stream);

@@ -291,10 +291,10 @@ def _dfit_worker(rank, world, port, out_dir, n, kind, noise):
 @pytest.mark.parametrize("n,kind", [(1024, "df"), (700, "mixed"), (4096, "df")])
 def test_distributed_fit_two_ranks_bit_identical(tmp_path, n, kind):
     """fit_distributed over two ranks (block-cyclic POTRF + TRTRI, a panel broadcast per
-    256-column super-block, W columns all-gathered): both ranks hold the bits of the one-rank
+    512-column super-block, W columns all-gathered): both ranks hold the bits of the one-rank
     run of the same algorithm (W by SHA-256, α, and the sharded posterior), and agree with
     engine.fit's factor and posterior to 1e-12 / 1e-10 (relative, normwise).  N = 4096
-    (n = 8192: 32 super-columns, 16 per rank) is the headline's size."""
+    (n = 8192: 16 super-columns, 8 per rank) is the headline's size."""
     from gp2d import distributed as GD
     from gp2d import engine as E
     world = 2
@@ -305,7 +305,7 @@ def test_distributed_fit_two_ranks_bit_identical(tmp_path, n, kind):
     gp1 = GD.fit_distributed(spec, x, y, 0.0025)                  # world 1: no process group here
     mu1, var1 = (t.cpu().numpy() for t in E.Predictor(gp1, 1024)(xg))
     W1 = gp1.W.cpu().numpy()
-    assert W1.shape[0] // 256 >= 6                                 # both ranks own super-columns
+    assert W1.shape[0] // GD.super_block() >= 3                    # both ranks own super-columns
     for i in range(world):
         assert int(r[i]["raised"]) == 0
         assert np.array_equal(r[i]["W_sha"], _sha(gp1.W)), i

@@ -112,3 +112,21 @@ def test_auto_fits_ahead_picks_the_measured_modes():
     assert E.auto_fits_ahead(df, 4096, 256 * 256) == 1
     assert E.auto_fits_ahead(mixed, 4096, 256 * 256) == 1
     assert E.auto_fits_ahead(mixed, 16384, 512 * 512) == 1
+
+
+def test_predictor_reuses_the_grid_order_only_for_the_same_grid():
+    """Predictor caches the Morton order of a device grid across calls with the same tensor
+    (a job stream's fixed grid); the bits equal a fresh Predictor's, and an in-place change of
+    the grid (its version counter) or another tensor recomputes the order."""
+    spec, x, y, noise, xg = _job(21, 600, 40, "df")
+    gp = E.fit(spec, x, y, noise, variance="ozaki")
+    pr = E.Predictor(gp, 1024)
+    m1, v1 = (t.clone() for t in pr(xg))
+    m2, v2 = (t.clone() for t in pr(xg))
+    assert torch.equal(m1, m2) and torch.equal(v1, v2) and pr._grid[0] is xg
+    fm, fv = E.Predictor(gp, 1024)(xg.clone())
+    assert torch.equal(m1, fm) and torch.equal(v1, fv)
+    xg.mul_(0.5)                        # in place: version bump, the cached order is stale
+    m3, v3 = pr(xg)
+    rm, rv = E.Predictor(gp, 1024)(xg.clone())
+    assert torch.equal(m3, rm) and torch.equal(v3, rv)

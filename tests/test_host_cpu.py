@@ -24,7 +24,7 @@ def test_library_exports_every_header_symbol():
     for s in syms:
         assert hasattr(L, s), s
     assert set(syms) == set(_native.EXPORTS)
-    assert L.gp2d_abi_version() == _native.ABI_VERSION == 6
+    assert L.gp2d_abi_version() == _native.ABI_VERSION == 7
     assert L.gp2d_padded_points(1) == 64 and L.gp2d_padded_points(64) == 64 and L.gp2d_padded_points(65) == 128
 
 
@@ -61,19 +61,22 @@ def test_argument_errors_are_reported():
     rc = L.gp2d_bcast(one, 8, -1, one, None)
     assert rc < 0 and b"root" in L.gp2d_last_error()
     # distributed factor (one job over several GPUs): argument checks before any device work
-    assert L.gp2d_dfact_panel_doubles(1024) == 1024 * 256
-    assert L.gp2d_dfact_workspace(1024) >= 2 * 128 * 128 * 8
-    rc = L.gp2d_dfact_panel(one, 384, 384, 0, one, one, one, 1 << 30, None)
-    assert rc < 0 and b"multiple of 256" in L.gp2d_last_error()
-    rc = L.gp2d_dfact_panel(one, 512, 512, 2, one, one, one, 1 << 30, None)
+    assert L.gp2d_dfact_sb() == 512
+    assert L.gp2d_dfact_panel_doubles(1024) == 1024 * 512
+    assert L.gp2d_dfact_workspace(1024) >= (4 * 128 * 128 + 512 * 1024) * 8
+    rc = L.gp2d_dfact_panel(one, 768, 768, 0, one, one, one, 1 << 30, None)
+    assert rc < 0 and b"multiple of 512" in L.gp2d_last_error()
+    rc = L.gp2d_dfact_panel(one, 1024, 1024, 2, one, one, one, 1 << 30, None)
     assert rc < 0 and b"out of range" in L.gp2d_last_error()
-    rc = L.gp2d_dfact_panel(one, 512, 512, 0, one, one, one, 8, None)
+    rc = L.gp2d_dfact_panel(one, 1024, 1024, 0, one, one, one, 8, None)
     assert rc < 0 and b"workspace" in L.gp2d_last_error()
-    rc = L.gp2d_dfact_update(one, 512, 512, 0, one, 2, 2, 0, 2, None)
+    rc = L.gp2d_dfact_update(one, 1024, 1024, 0, one, 2, 2, 0, 2, None)
     assert rc < 0 and b"rank" in L.gp2d_last_error()
-    rc = L.gp2d_dfact_invstep(one, 512, 510, 0, one, 1, 0, None)
+    rc = L.gp2d_dfact_invstep(one, 1024, 1022, 0, one, 1, 0, one, 1 << 30, None)
     assert rc < 0 and b"lda" in L.gp2d_last_error()
-    assert L.gp2d_dfact_update(one, 512, 512, 1, one, 1, 0, 0, 2, None) == 0   # no super-column after the last
+    rc = L.gp2d_dfact_invstep(one, 1024, 1024, 0, one, 1, 0, one, 8, None)
+    assert rc < 0 and b"workspace" in L.gp2d_last_error()
+    assert L.gp2d_dfact_update(one, 1024, 1024, 1, one, 1, 0, 0, 2, None) == 0   # no super-column after the last
     assert L.gp2d_copy2d(None, 1, None, 1, 0, 4, None) == 0
     rc = L.gp2d_copy2d(one, 2, one, 4, 3, 4, None)
     assert rc < 0 and b"leading dimension" in L.gp2d_last_error()

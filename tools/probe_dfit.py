@@ -36,7 +36,7 @@ def chain_ms(spec, xt, dev):
     the owners' sequence that no rank can overlap (broadcast latency excluded)."""
     L = E.N.lib()
     P, sh = E._ptr, E._stream_handle(dev)
-    npad, n = E.fit_layout(spec, xt.shape[0], "ozaki")
+    npad, n = GD.dfact_layout(spec, xt.shape[0])
     A = torch.empty((n, n), dtype=torch.float64, device=dev)
     desc = spec.desc()
     import ctypes
@@ -46,7 +46,7 @@ def chain_ms(spec, xt, dev):
     wb = int(L.gp2d_dfact_workspace(n))
     work = torch.empty(wb // 8 + 1, dtype=torch.float64, device=dev)
     info = torch.zeros(1, dtype=torch.int32, device=dev)
-    nsb = n // 256
+    nsb = n // GD.super_block()
 
     def run():
         E.N.check(L.gp2d_dfact_panel(P(A), n, n, 0, P(pan), P(info), P(work), wb, sh), "panel")
