@@ -253,18 +253,28 @@ def fit_distributed(spec: E.KernelSpec, x, y, noise: float, device=None, varianc
     comm = E.side_stream(dev)
     t0 = time.perf_counter()
 
-    factored = {}   # s → main-stream event after the owner's gp2d_dfact_panel(s)
-    done = {}       # s → main-stream event after step s's last read of its panel buffer
+    factored = {}   # s → event after the owner's gp2d_dfact_panel(s) (main or crit stream)
+    done = {}       # s → events after step s's last reads of its panel buffer (main, inv)
+    # lookahead: the owners' chain of panel factorisations on `crit`, and the TRTRI steps (W
+    # columns ≤ s) on `inv` beside the POTRF trailing updates (K_y columns > s) on main — the
+    # regions are disjoint, and the TRTRI step's small D_s product no longer idles the chip
+    crit = E.side_stream(dev) if lookahead else main
+    inv = E.side_stream(dev) if lookahead else main
 
-    def factor(s):   # owner of s: panel s into its buffer, on the main stream
-        E.N.check(L.gp2d_dfact_panel(P(A), n, n, s, P(panels[s % 2]), P(info), P(work), wbytes, sh),
-                  "gp2d_dfact_panel")
-        ev = torch.cuda.Event()
-        ev.record(main)
+    def wait_done(st, s):
+        for ev in done.get(s, ()):
+            st.wait_event(ev)
+
+    def factor(s, st):   # owner of s: panel s into its buffer, on stream st
+        with torch.cuda.stream(st):
+            E.N.check(L.gp2d_dfact_panel(P(A), n, n, s, P(panels[s % 2]), P(info), P(work), wbytes,
+                                         E._stream_handle(dev)), "gp2d_dfact_panel")
+            ev = torch.cuda.Event()
+            ev.record(st)
         factored[s] = ev
 
     if rank == 0:
-        factor(0)
+        factor(0, main)
     for s in range(nsb):
         owner = s % ws
         buf = panels[s % 2]
@@ -273,26 +283,45 @@ def fit_distributed(spec: E.KernelSpec, x, y, noise: float, device=None, varianc
             # the buffer's previous user (step s − 2) is done; the owner's panel s is written —
             # the broadcast does not wait for the rest of step s − 1 (it overlaps it)
             if s >= 2:
-                comm.wait_event(done.pop(s - 2))
+                wait_done(comm, s - 2)
+                done.pop(s - 2)
             if owner == rank:
                 comm.wait_event(factored.pop(s))
             with torch.cuda.stream(comm):
                 dist.broadcast(buf[:rows * SB], owner)
             main.wait_stream(comm)
+        elif s in factored:   # one rank: the panel was factored on the chain stream
+            main.wait_event(factored.pop(s))
         nxt = s + 1
         rest_lo = nxt
         if lookahead and nxt < nsb and nxt % ws == rank:
-            # look-ahead: bring super-column s+1 up to date and factor it before the rest of step s
+            # look-ahead: bring super-column s+1 up to date with panel s, then factor it on the
+            # chain stream while the rest of step s (trailing update, TRTRI step) runs on main
             E.N.check(L.gp2d_dfact_update(P(A), n, n, s, P(buf), ws, rank, nxt, nxt + 1, sh), "gp2d_dfact_update")
-            factor(nxt)
+            ev = torch.cuda.Event()
+            ev.record(main)
+            crit.wait_event(ev)
+            wait_done(crit, nxt - 2)   # its panel buffer was last read by step nxt − 2
+            factor(nxt, crit)
             rest_lo = nxt + 1
+        if inv is not main:   # the TRTRI step needs panel s (and the owner's factor of it) only
+            ev = torch.cuda.Event()
+            ev.record(main)
+            inv.wait_event(ev)
         E.N.check(L.gp2d_dfact_update(P(A), n, n, s, P(buf), ws, rank, rest_lo, nsb, sh), "gp2d_dfact_update")
         if not lookahead and nxt < nsb and nxt % ws == rank:
-            factor(nxt)
-        E.N.check(L.gp2d_dfact_invstep(P(A), n, n, s, P(buf), ws, rank, P(work), wbytes, sh), "gp2d_dfact_invstep")
-        ev = torch.cuda.Event()
-        ev.record(main)
-        done[s] = ev
+            factor(nxt, main)
+        with torch.cuda.stream(inv):
+            E.N.check(L.gp2d_dfact_invstep(P(A), n, n, s, P(buf), ws, rank, P(work), wbytes, E._stream_handle(dev)),
+                      "gp2d_dfact_invstep")
+        evs = []
+        for st in ([main, inv] if inv is not main else [main]):
+            ev = torch.cuda.Event()
+            ev.record(st)
+            evs.append(ev)
+        done[s] = evs
+    main.wait_stream(crit)   # the chain's last panel (and its info word) before the gather
+    main.wait_stream(inv)
     del panels, work
     t1 = time.perf_counter()
     if not _solo(ws) and emulate is None:

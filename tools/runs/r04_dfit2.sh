@@ -1,0 +1,8 @@
+# distributed factor: chain on its own stream (look-ahead) — parity, timing, kernel trace
+set -o pipefail
+R=gpurun_out/r04_dfit2
+mkdir -p $R
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+timeout -k 10 500 python -u -m pytest tests/test_gpu_distributed.py tests/test_gpu_configs.py -x -v -k "distributed or dfit" --timeout 300 --timeout-method thread > $R/tests.log 2>&1 || exit 1
+timeout -k 10 300 python -u tools/probe_dfit.py --sizes 4096,16384 --reps 3 --emulate 8 > $R/probe.log 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace -d $R/trace -o run -- python -u tools/probe_dfit.py --sizes 16384 --reps 1 --emulate 8 > $R/trace.log 2>&1 || exit 1
