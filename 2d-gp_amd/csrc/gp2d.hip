@@ -971,6 +971,12 @@ size_t gp2d_ozaki_wres_bytes(int64_t n) {
   return nm > 0 ? (size_t)nm * (size_t)n * (size_t)n : 0;
 }
 
+static int launch_w_res(const double* W, int64_t n, int64_t ldw, const OzakiConsts& oc, int8_t* wres,
+                        const double* rowscale, hipStream_t s) {
+  ozaki_w_res_kernel<<<dim3((unsigned)(n / 64), (unsigned)(n / 256)), 256, 0, s>>>(W, n, ldw, oc, wres, rowscale);
+  return check_launch("ozaki_w_res_kernel");
+}
+
 int gp2d_ozaki_prepare(const double* W, int64_t n, int64_t ldw, const gp2d_kernel_t* k, int8_t* wres,
                        double* rowscale, int* nmod_out, void* stream) {
   GP2D_CHECK(validate_ozaki_kernel(k));
@@ -978,7 +984,7 @@ int gp2d_ozaki_prepare(const double* W, int64_t n, int64_t ldw, const gp2d_kerne
   GP2D_REQUIRE(nmod_out != nullptr, "ozaki: nmod_out is NULL");
   hipStream_t s = S(stream);
   double* l1 = reinterpret_cast<double*>(wres);  // scratch: the planes are written afterwards
-  ozaki_w_scale_kernel<<<(unsigned)n, 256, 0, s>>>(W, n, ldw, rowscale, l1);
+  ozaki_w_scale_kernel<<<(unsigned)n, 256, 0, s>>>(W, n, ldw, rowscale, l1, 0.0, 0, 0);
   GP2D_CHECK(check_launch("ozaki_w_scale_kernel"));
   std::vector<double> hl1((size_t)n), hs((size_t)n);
   if (hipMemcpyAsync(hl1.data(), l1, sizeof(double) * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -1010,8 +1016,9 @@ int gp2d_ozaki_prepare(const double* W, int64_t n, int64_t ldw, const gp2d_kerne
   GP2D_REQUIRE(nmod > 0, "ozaki: row bound exceeds the modulus table");
   OzakiConsts oc;
   GP2D_CHECK(make_ozaki_consts(nmod, k, oc));
-  ozaki_w_res_kernel<<<(unsigned)n, 256, 0, s>>>(W, n, ldw, oc, wres, rowscale);
-  GP2D_CHECK(check_launch("ozaki_w_res_kernel"));
+  ozaki_rowscale_final_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(rowscale, n, oc.M, oc.sB);
+  GP2D_CHECK(check_launch("ozaki_rowscale_final_kernel"));
+  GP2D_CHECK(launch_w_res(W, n, ldw, oc, wres, rowscale, s));
   *nmod_out = nmod;
   return 0;
 }
@@ -1026,13 +1033,12 @@ int gp2d_ozaki_prepare_async(const double* W, int64_t n, int64_t ldw, const gp2d
   const int nmod = gp2d_ozaki_nmod_apriori(n, k, diag_add);
   GP2D_REQUIRE(nmod > 0, "ozaki: a-priori bound exceeds the modulus table");
   hipStream_t s = S(stream);
-  double* l1 = reinterpret_cast<double*>(wres);  // scratch (unused here), overwritten below
-  ozaki_w_scale_kernel<<<(unsigned)n, 256, 0, s>>>(W, n, ldw, rowscale, l1);
-  GP2D_CHECK(check_launch("ozaki_w_scale_kernel"));
   OzakiConsts oc;
   GP2D_CHECK(make_ozaki_consts(nmod, k, oc));
-  ozaki_w_res_kernel<<<(unsigned)n, 256, 0, s>>>(W, n, ldw, oc, wres, rowscale);
-  GP2D_CHECK(check_launch("ozaki_w_res_kernel"));
+  // no L1 norms (the count is a-priori): one pass over W for the row exponents, one for the planes
+  ozaki_w_scale_kernel<<<(unsigned)n, 256, 0, s>>>(W, n, ldw, rowscale, nullptr, oc.M, oc.sB, 1);
+  GP2D_CHECK(check_launch("ozaki_w_scale_kernel"));
+  GP2D_CHECK(launch_w_res(W, n, ldw, oc, wres, rowscale, s));
   *nmod_out = nmod;
   return 0;
 }

@@ -88,7 +88,8 @@ __device__ __forceinline__ double block_reduce(double v, double* red, bool is_ma
 }
 
 __global__ __launch_bounds__(256) void ozaki_w_scale_kernel(const double* __restrict__ W, int64_t n, int64_t ldw,
-                                                            double* __restrict__ rowscale, double* __restrict__ l1) {
+                                                            double* __restrict__ rowscale, double* __restrict__ l1,
+                                                            double M, int sB, int final_scale) {
   __shared__ double red[256];
   const int64_t i = blockIdx.x;
   const int tid = threadIdx.x;
@@ -99,41 +100,61 @@ __global__ __launch_bounds__(256) void ozaki_w_scale_kernel(const double* __rest
   const int e = (mx > 0.0) ? ilogb(mx) : 0;    // 2^e ≤ mx < 2^{e+1}
   const int si = OZ_PW - 1 - e;                // |W·2^si| < 2^OZ_PW
   double sum = 0.0;
-  for (int64_t k = tid; k <= i; k += 256) sum += fabs(rint(ldexp(w[k], si)));
-  sum = block_reduce(sum, red, false);
+  if (l1 != nullptr) {   // the row's L1 norm (the data-driven moduli count only)
+    for (int64_t k = tid; k <= i; k += 256) sum += fabs(rint(ldexp(w[k], si)));
+    sum = block_reduce(sum, red, false);
+  }
   if (tid == 0) {
-    rowscale[i] = (double)si;
-    l1[i] = sum;
+    // final_scale: the CRT's row scale M·2^{−s_i−s_B} (s_i recoverable exactly by ilogb, as
+    // ozaki_row_exp does); otherwise s_i itself, for the host's row bounds
+    rowscale[i] = final_scale ? ldexp(M, -si - sB) : (double)si;
+    if (l1 != nullptr) l1[i] = sum;
   }
 }
 
-// Pass 2: residue planes Wres[l] (int8, slab-blocked, zeros above the diagonal) and the
-// final rowscale[i] = M·2^{−s_i−s_B}.
+// s_i → the final row scale M·2^{−s_i−s_B} (the data-driven path, once M is known)
+__global__ __launch_bounds__(256) void ozaki_rowscale_final_kernel(double* __restrict__ rowscale, int64_t n, double M,
+                                                                   int sB) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) rowscale[i] = ldexp(M, -(int)rowscale[i] - sB);
+}
+
+// s_i from the final row scale: ldexp keeps the mantissa, so the exponents differ by s_i + s_B
+__device__ __forceinline__ int ozaki_row_exp(double rowscale_i, const OzakiConsts& oc) {
+  return ilogb(oc.M) - ilogb(rowscale_i) - oc.sB;
+}
+
+// Pass 2: residue planes Wres[l] (int8, slab-blocked, zeros above the diagonal).  One
+// workgroup per (256-row block bi, 64-wide k slab ks) with ks < 4·(bi+1) (the GEMM, a_lower,
+// never reads past its diagonal tile): a wave covers 4 rows × 64 k per step — 16 lanes per row,
+// 4 consecutive k per lane, 32 B of each row read contiguously — and writes, per modulus, the
+// 4 rows' 64-B runs of the slab tile: 256 contiguous bytes per wave store (the per-row form
+// wrote four 64-B pieces 16 KB apart).
 __global__ __launch_bounds__(256) void ozaki_w_res_kernel(const double* __restrict__ W, int64_t n, int64_t ldw,
                                                           OzakiConsts oc, int8_t* __restrict__ wres,
-                                                          double* __restrict__ rowscale) {
-  const int64_t i = blockIdx.x;
-  const int tid = threadIdx.x;
-  const double* w = W + i * ldw;
-  const int si = (int)rowscale[i];
-  __syncthreads();
-  if (tid == 0) rowscale[i] = ldexp(oc.M, -si - oc.sB);
-  // 4 consecutive k per thread → one packed dword store per plane.  Only k < the end of the
-  // row's 256-row block is written: the GEMM (a_lower) never reads past its diagonal tile.
-  const int64_t kend = std::min<int64_t>(n, (i / 256 + 1) * 256);
-  for (int64_t k0 = (int64_t)tid * 4; k0 < kend; k0 += 1024) {
+                                                          const double* __restrict__ rowscale) {
+  const int64_t bi = blockIdx.y, ks = blockIdx.x;
+  if (ks * 64 >= (bi + 1) * 256) return;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t k0 = ks * 64 + 4 * (lane & 15);
+  const int64_t plane = n * n;
+#pragma unroll 1
+  for (int it = 0; it < 16; ++it) {
+    const int64_t i = bi * 256 + wv * 64 + it * 4 + (lane >> 4);
+    const int si = ozaki_row_exp(rowscale[i], oc);
+    const double* w = W + i * ldw + k0;
+    const d2 p0 = *reinterpret_cast<const d2*>(w), p1 = *reinterpret_cast<const d2*>(w + 2);
+    const double v[4] = {p0.x, p0.y, p1.x, p1.y};
     double x[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int64_t k = k0 + u;
-      x[u] = (k <= i && k < n) ? rint(ldexp(w[k], si)) : 0.0;
-    }
+    for (int u = 0; u < 4; ++u) x[u] = (k0 + u <= i) ? rint(ldexp(v[u], si)) : 0.0;
+    int8_t* dst = wres + slab_offset(i, k0, n);
     for (int l = 0; l < oc.nmod; ++l) {
       const double m = (double)oc.m[l];
       uint32_t packed = 0;
 #pragma unroll
       for (int u = 0; u < 4; ++u) packed |= residue_byte(x[u], m, oc.inv_m[l]) << (8 * u);   // |x| < 2^pW
-      *reinterpret_cast<uint32_t*>(wres + (int64_t)l * n * n + slab_offset(i, k0, n)) = packed;
+      *reinterpret_cast<uint32_t*>(dst + (int64_t)l * plane) = packed;
     }
   }
 }
