@@ -136,11 +136,14 @@ __device__ __forceinline__ double ard_value(const ArdParams& p, const double* a,
 // row points so that the column point's coordinates are loaded once.
 constexpr int ASM_ROWS = 16;
 
+// j_off / col_comp (gp2d_assemble_cols): column points start at j_off and only the columns of
+// component col_comp (0: u, 1: v; −1: both) are written — the same per-element arithmetic.
 __global__ __launch_bounds__(256) void assemble_vec_kernel(
     const double* __restrict__ xa, int64_t na, int64_t na_pad,
     const double* __restrict__ xb, int64_t nb, int64_t nb_pad,
-    VecParams p, double diag_add, int symmetric, double* __restrict__ out, int64_t ld) {
-  const int64_t j = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
+    VecParams p, double diag_add, int symmetric, double* __restrict__ out, int64_t ld, int64_t j_off = 0,
+    int col_comp = -1) {
+  const int64_t j = j_off + (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
   const int ty = threadIdx.x >> 6;
   const bool jv = j < nb;
   double b0 = 0.0, b1 = 0.0, b2 = 0.0;
@@ -161,10 +164,14 @@ __global__ __launch_bounds__(256) void assemble_vec_kernel(
     }
     double* r0 = out + i * ld;
     double* r1 = out + (na_pad + i) * ld;
-    r0[j] = k11;
-    r0[nb_pad + j] = k12;
-    r1[j] = k12;
-    r1[nb_pad + j] = k22;
+    if (col_comp != 1) {
+      r0[j] = k11;
+      r1[j] = k12;
+    }
+    if (col_comp != 0) {
+      r0[nb_pad + j] = k12;
+      r1[nb_pad + j] = k22;
+    }
   }
 }
 

@@ -42,6 +42,58 @@ __global__ __launch_bounds__(DF_SB / 2) void dfact_copy_owned_kernel(const doubl
   *reinterpret_cast<d2*>(X + i * ldx + col) = *reinterpret_cast<const d2*>(T + i * ldt + col);
 }
 
+// α from the owned columns (fit_distributed): z = W·y = Σ_t W[:, t]·y[t] in super-column order,
+// then α[t] = W[:, t]ᵀ·z — every piece computed from one super-column, the same for any P.  One
+// launch covers `count` super-columns t = t0 + q·dt (blockIdx.y = q).
+// zpart[q][i] = Σ_{k ∈ super-column t, k ≤ i} W[i][k]·y[k] (0 above the super-block): one wave per
+// row, 8 columns per lane in a fixed order, a fixed shuffle reduction.
+__global__ __launch_bounds__(256) void dfact_zpart_kernel(const double* __restrict__ W, int64_t n, int64_t ldw,
+                                                          int t0, int dt, const double* __restrict__ y,
+                                                          double* __restrict__ zpart) {
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int64_t c0 = (int64_t)(t0 + (int)blockIdx.y * dt) * DF_SB;
+  if (i >= n) return;
+  double s = 0.0;
+  if (i >= c0) {
+    const double* w = W + i * ldw + c0;
+#pragma unroll
+    for (int u = 0; u < DF_SB / 64; ++u) {
+      const int64_t k = c0 + lane + 64 * u;
+      s += (k <= i) ? w[lane + 64 * u] * y[k] : 0.0;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (lane == 0) zpart[(int64_t)blockIdx.y * n + i] = s;
+}
+
+// part[q][seg][c] = Σ_{i ∈ [c0 + 128·seg, +128), i ≥ c0 + c} W[i][c0 + c]·z[i] (0 for segments below
+// the super-block's rows): one thread per column of the super-column (reads of a row coalesced
+// over the threads); the n/128 segments are summed afterwards in a fixed order.
+__global__ __launch_bounds__(256) void dfact_alpha_part_kernel(const double* __restrict__ W, int64_t n, int64_t ldw,
+                                                               int t0, int dt, const double* __restrict__ z,
+                                                               double* __restrict__ part) {
+  const int c = (int)blockIdx.x * 256 + (int)threadIdx.x;   // < DF_SB
+  const int64_t seg = blockIdx.y, q = blockIdx.z;
+  const int64_t c0 = (int64_t)(t0 + (int)q * dt) * DF_SB;
+  const int64_t r0 = seg * 128, col = c0 + c;
+  double s = 0.0;
+  if (r0 + 128 > c0)
+    for (int64_t i = (r0 > col ? r0 : col); i < r0 + 128; ++i) s += W[i * ldw + col] * z[i];
+  part[(q * (n / 128) + seg) * DF_SB + c] = s;
+}
+
+// out[q][c] = Σ_seg part[q][seg][c] in segment order
+__global__ __launch_bounds__(256) void dfact_alpha_sum_kernel(const double* __restrict__ part, int64_t nseg,
+                                                              double* __restrict__ out) {
+  const int c = (int)blockIdx.x * 256 + (int)threadIdx.x;
+  const int64_t q = blockIdx.y;
+  const double* p = part + q * nseg * DF_SB + c;
+  double s = 0.0;
+  for (int64_t g = 0; g < nseg; ++g) s += p[g * DF_SB];
+  out[q * DF_SB + c] = s;
+}
+
 // A failed diagonal block reports its local leading-minor order in *tmp; the first failure
 // of the whole factorisation is kept in *info as a global order.
 __global__ void dfact_info_kernel(int* __restrict__ info, const int* __restrict__ tmp, int64_t off) {

@@ -208,6 +208,23 @@ int gp2d_assemble(const double* xa, int64_t na, int64_t na_pad, const double* xb
   return assemble_impl(xa, na, na_pad, xb, nb, nb_pad, k, diag_add, symmetric, out, ld, S(stream));
 }
 
+int gp2d_assemble_cols(const double* x, int64_t n, int64_t n_pad, const gp2d_kernel_t* k, double diag_add,
+                       double* out, int64_t ld, int64_t c0, int64_t ncols, void* stream) {
+  GP2D_CHECK(validate_kernel(k));
+  GP2D_REQUIRE(is_vector_family(k), "assemble_cols: vector kernel families only");
+  GP2D_REQUIRE(n_pad % PT_TILE == 0 && n >= 0 && n <= n_pad, "assemble_cols: bad point counts");
+  GP2D_REQUIRE(ld >= 2 * n_pad, "assemble_cols: ld too small");
+  GP2D_REQUIRE(c0 >= 0 && ncols >= 0 && c0 % 64 == 0 && ncols % 64 == 0 && c0 + ncols <= 2 * n_pad &&
+                   (ncols == 0 || c0 / n_pad == (c0 + ncols - 1) / n_pad),
+               "assemble_cols: the column range must be 64-aligned and inside one component");
+  if (ncols == 0 || n_pad == 0) return 0;
+  const int comp = (int)(c0 / n_pad);
+  dim3 grid((unsigned)(ncols / 64), (unsigned)((n_pad + ASM_ROWS - 1) / ASM_ROWS));
+  assemble_vec_kernel<<<grid, 256, 0, S(stream)>>>(x, n, n_pad, x, n, n_pad, make_vec_params(k), diag_add, 1, out, ld,
+                                                   c0 - (int64_t)comp * n_pad, comp);
+  return check_launch("assemble_cols");
+}
+
 }  // extern "C"
 
 // ------------------------------------------------------------------------ POTRF
@@ -839,6 +856,47 @@ int gp2d_dfact_invstep(double* A, int64_t n, int64_t lda, int s, const double* p
   }
   dfact_copy_owned_kernel<<<dim3((unsigned)count, DF_SB), DF_SB / 2, 0, st>>>(Xt, n, Xs, lda, first, nranks);
   return check_launch("dfact_copy_owned_kernel");
+}
+
+static int dfact_blocks_args(const double* W, int64_t n, int64_t ldw, int t0, int dt, int count) {
+  GP2D_CHECK(dfact_args(W, n, ldw, t0));
+  GP2D_REQUIRE(count >= 1 && dt >= 1 && (int64_t)(t0 + (count - 1) * dt) * DF_SB < n,
+               "dfact: super-column list out of range");
+  return 0;
+}
+
+int gp2d_dfact_zpart(const double* W, int64_t n, int64_t ldw, int t0, int dt, int count, const double* y,
+                     double* zpart, void* stream) {
+  GP2D_CHECK(dfact_blocks_args(W, n, ldw, t0, dt, count));
+  GP2D_REQUIRE(y != nullptr && zpart != nullptr, "dfact_zpart: NULL vector");
+  dfact_zpart_kernel<<<dim3((unsigned)((n + 3) / 4), (unsigned)count), 256, 0, S(stream)>>>(W, n, ldw, t0, dt, y,
+                                                                                          zpart);
+  return check_launch("dfact_zpart_kernel");
+}
+
+int gp2d_dfact_zsum(const double* parts, int nparts, int64_t n, double* z, void* stream) {
+  GP2D_REQUIRE(parts != nullptr && z != nullptr && nparts >= 1 && n > 0, "dfact_zsum: bad arguments");
+  sum_segments_kernel<<<(unsigned)((n + 255) / 256), 256, 0, S(stream)>>>(parts, nparts, n, z);
+  return check_launch("sum_segments_kernel");
+}
+
+size_t gp2d_dfact_alpha_workspace(int64_t n, int count) {
+  return (size_t)(count > 0 ? count : 0) * (size_t)((n > 0 ? n : 0) / 128) * DF_SB * sizeof(double);
+}
+
+int gp2d_dfact_alpha_blocks(const double* W, int64_t n, int64_t ldw, int t0, int dt, int count, const double* z,
+                            double* alpha, void* work, size_t work_bytes, void* stream) {
+  GP2D_CHECK(dfact_blocks_args(W, n, ldw, t0, dt, count));
+  GP2D_REQUIRE(z != nullptr && alpha != nullptr, "dfact_alpha_blocks: NULL vector");
+  GP2D_REQUIRE(work != nullptr && work_bytes >= gp2d_dfact_alpha_workspace(n, count),
+               "dfact_alpha_blocks: workspace too small");
+  const int64_t nseg = n / 128;
+  double* part = static_cast<double*>(work);
+  dfact_alpha_part_kernel<<<dim3(DF_SB / 256, (unsigned)nseg, (unsigned)count), 256, 0, S(stream)>>>(W, n, ldw, t0,
+                                                                                                   dt, z, part);
+  GP2D_CHECK(check_launch("dfact_alpha_part_kernel"));
+  dfact_alpha_sum_kernel<<<dim3(DF_SB / 256, (unsigned)count), 256, 0, S(stream)>>>(part, nseg, alpha);
+  return check_launch("dfact_alpha_sum_kernel");
 }
 
 int gp2d_copy2d(double* dst, int64_t ldd, const double* src, int64_t lds, int64_t rows, int64_t cols,

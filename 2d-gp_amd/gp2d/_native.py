@@ -32,7 +32,8 @@ EXPORTS = (
     "gp2d_kernel_grad_count", "gp2d_kernel_grad_workspace", "gp2d_kernel_grad",
     "gp2d_gemm", "gp2d_transpose", "gp2d_bcast",
     "gp2d_dfact_sb", "gp2d_dfact_panel_doubles", "gp2d_dfact_workspace", "gp2d_dfact_panel", "gp2d_dfact_update",
-    "gp2d_dfact_invstep", "gp2d_copy2d", "gp2d_zero_upper", "gp2d_pack_lower_doubles", "gp2d_pack_lower",
+    "gp2d_dfact_invstep", "gp2d_dfact_zpart", "gp2d_dfact_zsum", "gp2d_dfact_alpha_workspace", "gp2d_dfact_alpha_blocks",
+    "gp2d_assemble_cols", "gp2d_copy2d", "gp2d_zero_upper", "gp2d_pack_lower_doubles", "gp2d_pack_lower",
     "gp2d_timing_enable", "gp2d_timing_read", "gp2d_last_error",
 )
 
@@ -119,6 +120,11 @@ _SIGS = {
     "gp2d_dfact_panel": (_I, [_P, _I64, _I64, _I, _P, _P, _P, _SZ, _P]),
     "gp2d_dfact_update": (_I, [_P, _I64, _I64, _I, _P, _I, _I, _I, _I, _P]),
     "gp2d_dfact_invstep": (_I, [_P, _I64, _I64, _I, _P, _I, _I, _P, _SZ, _P]),
+    "gp2d_dfact_zpart": (_I, [_P, _I64, _I64, _I, _I, _I, _P, _P, _P]),
+    "gp2d_dfact_zsum": (_I, [_P, _I, _I64, _P, _P]),
+    "gp2d_dfact_alpha_workspace": (_SZ, [_I64, _I]),
+    "gp2d_dfact_alpha_blocks": (_I, [_P, _I64, _I64, _I, _I, _I, _P, _P, _P, _SZ, _P]),
+    "gp2d_assemble_cols": (_I, [_P, _I64, _I64, _KP, _D, _P, _I64, _I64, _I64, _P]),
     "gp2d_copy2d": (_I, [_P, _I64, _P, _I64, _I64, _I64, _P]),
     "gp2d_zero_upper": (_I, [_P, _I64, _I64, _P]),
     "gp2d_pack_lower_doubles": (_SZ, [_I64]),

@@ -241,10 +241,20 @@ def fit_distributed(spec: E.KernelSpec, x, y, noise: float, device=None, varianc
     sh = E._stream_handle(dev)
     P = E._ptr
     desc = spec.desc()
-    A = torch.empty((n, n), dtype=torch.float64, device=dev)
-    E.N.check(L.gp2d_assemble(P(X), ntr, npad, P(X), ntr, npad, ctypes.byref(desc), float(noise + jitter), 1,
-                              P(A), n, sh), "gp2d_assemble")
     nsb = n // SB
+    multi = emulate is not None or not _solo(ws)
+    mine = _owned_blocks(nsb, ws, rank)
+    A = torch.empty((n, n), dtype=torch.float64, device=dev)
+    if multi and spec.is_vector:
+        # a rank reads and writes only its own super-columns: assemble just those (each 256-column
+        # half lies inside one component), the same arithmetic as the full symmetric assembly
+        for t in mine:
+            for c0 in (t * SB, t * SB + SB // 2):
+                E.N.check(L.gp2d_assemble_cols(P(X), ntr, npad, ctypes.byref(desc), float(noise + jitter), P(A), n,
+                                               c0, SB // 2, sh), "gp2d_assemble_cols")
+    else:
+        E.N.check(L.gp2d_assemble(P(X), ntr, npad, P(X), ntr, npad, ctypes.byref(desc), float(noise + jitter), 1,
+                                  P(A), n, sh), "gp2d_assemble")
     pdoubles = int(L.gp2d_dfact_panel_doubles(n))
     panels = [torch.empty(pdoubles, dtype=torch.float64, device=dev) for _ in range(2)]
     wbytes = int(L.gp2d_dfact_workspace(n))
@@ -327,17 +337,18 @@ def fit_distributed(spec: E.KernelSpec, x, y, noise: float, device=None, varianc
     if not _solo(ws) and emulate is None:
         _allgather_w_columns(A, n, ws, rank, dev)
         allreduce_first_failure(info)
-    E.N.check(L.gp2d_zero_upper(P(A), n, n, sh), "gp2d_zero_upper")
+    if multi:
+        # W = L⁻¹ is zero above each super-block's diagonal block: the owned columns were reset
+        # to the identity block column (zeros above), the gathered ones carry stale K_y there
+        for t in range(nsb):
+            if t % ws != rank and t > 0:
+                A[:t * SB, t * SB:(t + 1) * SB].zero_()
     t2 = time.perf_counter()
     Y = E._pad_obs(y, ntr, npad, bd, dev)
     if perm is not None:
         for c in range(bd):
             Y[c * npad:c * npad + ntr] = Y[c * npad:c * npad + ntr][perm]
-    alpha = torch.empty(n, dtype=torch.float64, device=dev)
-    pbytes = int(L.gp2d_potrs_workspace(n))
-    pwork = torch.empty(pbytes // 8 + 1, dtype=torch.float64, device=dev)
-    E.N.check(L.gp2d_potrs_inv(P(A), n, n, P(Y), P(alpha), P(pwork), pbytes, sh), "gp2d_potrs_inv")
-    del pwork
+    alpha = _alpha_owned(A, n, Y, ws, rank, nsb, SB, dev, collective=not _solo(ws) and emulate is None)
     gp = E.GPFit(kernel=spec, noise=float(noise), x=X, n_train=ntr, n_pad=npad, W=A, alpha=alpha, device=dev,
                  y=Y, perm=perm)
     if emulate is not None:
@@ -348,6 +359,55 @@ def fit_distributed(spec: E.KernelSpec, x, y, noise: float, device=None, varianc
     if stats is not None:
         stats.update(host_factor_s=t1 - t0, host_gather_s=t2 - t1)
     return gp
+
+
+def _alpha_owned(A: torch.Tensor, n: int, Y: torch.Tensor, ws: int, rank: int, nsb: int, SB: int, dev,
+                 collective: bool) -> torch.Tensor:
+    """α = Wᵀ(W y) from this rank's super-columns only (gp2d_dfact_zpart / _zsum / _alpha_blocks):
+    z = Σ_t W[:, t]·y[t] over the super-columns in t order (each rank's partials gathered), then
+    α[t] = W[:, t]ᵀ·z for the owned t, gathered.  Every piece is computed from one super-column
+    in a fixed order, so any world size gives the bits of one rank; each rank reads 1/P of W
+    twice instead of all of it."""
+    L = E.N.lib()
+    P, sh = E._ptr, E._stream_handle(dev)
+    mine = _owned_blocks(nsb, ws, rank) if (collective or ws > 1) else list(range(nsb))
+    cap = (nsb + ws - 1) // ws if (collective or ws > 1) else nsb
+    dt = ws if (collective or ws > 1) else 1
+    zp = torch.zeros((cap, n), dtype=torch.float64, device=dev)
+    if mine:
+        E.N.check(L.gp2d_dfact_zpart(P(A), n, n, mine[0], dt, len(mine), P(Y), P(zp), sh), "gp2d_dfact_zpart")
+    if collective:
+        allz = torch.empty((ws, cap, n), dtype=torch.float64, device=dev)
+        _all_gather(allz, zp, ws)
+        order = torch.tensor([(t % ws) * cap + t // ws for t in range(nsb)], device=dev)
+        parts = allz.view(ws * cap, n).index_select(0, order).contiguous()
+    elif ws > 1:   # emulate: this rank's partials only (the emulated factor is not W either)
+        parts = zp[:len(mine)].contiguous()
+    else:
+        parts = zp
+    z = torch.empty(n, dtype=torch.float64, device=dev)
+    E.N.check(L.gp2d_dfact_zsum(P(parts), parts.shape[0], n, P(z), sh), "gp2d_dfact_zsum")
+    ab = torch.zeros((cap, SB), dtype=torch.float64, device=dev)
+    if mine:
+        wb = int(L.gp2d_dfact_alpha_workspace(n, len(mine)))
+        work = torch.empty(wb // 8 + 1, dtype=torch.float64, device=dev)
+        E.N.check(L.gp2d_dfact_alpha_blocks(P(A), n, n, mine[0], dt, len(mine), P(z), P(ab), P(work), wb, sh),
+                  "gp2d_dfact_alpha_blocks")
+    if not collective:
+        if ws > 1:
+            return torch.zeros(n, dtype=torch.float64, device=dev)
+        return ab.reshape(-1)[:n].contiguous()
+    alla = torch.empty((ws, cap, SB), dtype=torch.float64, device=dev)
+    _all_gather(alla, ab, ws)
+    order = torch.tensor([(t % ws) * cap + t // ws for t in range(nsb)], device=dev)
+    return alla.view(ws * cap, SB).index_select(0, order).reshape(-1).contiguous()
+
+
+def _all_gather(out: torch.Tensor, t: torch.Tensor, ws: int):
+    if dist.get_backend() == "nccl":
+        dist.all_gather_into_tensor(out, t)
+    else:   # gloo (the CPU / shared-card rehearsals)
+        dist.all_gather(list(out.unbind(0)), t)
 
 
 def allreduce_first_failure(info: torch.Tensor) -> torch.Tensor:

@@ -297,6 +297,25 @@ int gp2d_dfact_update(double* A, int64_t n, int64_t lda, int s, const double* pa
                       int t_lo, int t_hi, void* stream);
 int gp2d_dfact_invstep(double* A, int64_t n, int64_t lda, int s, const double* panel, int nranks, int rank,
                        void* work, size_t work_bytes, void* stream);
+/* α = K_y⁻¹y = Wᵀ(W y) from the owned super-columns (each rank reads only its columns of W),
+ * for the `count` super-columns t = t0 + q·dt in one launch each:
+ * gp2d_dfact_zpart: zpart[q][i] = Σ_{k in super-column t, k ≤ i} W[i][k]·y[k] (count × n; 0 above
+ *   the super-block); z = Σ_t zpart_t summed in t order by gp2d_dfact_zsum (gather every rank's
+ *   partials first).
+ * gp2d_dfact_alpha_blocks: alpha[q][c] = Σ_{i ≥ t·SB+c} W[i][t·SB+c]·z[i], c < SB (work:
+ *   gp2d_dfact_alpha_workspace(n, count) bytes).  Both orders are fixed, so any P gives the bits
+ *   of P = 1.
+ * gp2d_assemble_cols: columns [c0, c0+ncols) of the symmetric K_y = K(x, x) + diag_add·I (vector
+ *   families; c0, ncols multiples of 64, inside one component) — the same arithmetic as
+ *   gp2d_assemble(symmetric = 1); a rank of the distributed factor assembles only its columns.  */
+int gp2d_dfact_zpart(const double* W, int64_t n, int64_t ldw, int t0, int dt, int count, const double* y,
+                     double* zpart, void* stream);
+int gp2d_dfact_zsum(const double* parts, int nparts, int64_t n, double* z, void* stream);  /* z = Σ parts[p] in p order */
+size_t gp2d_dfact_alpha_workspace(int64_t n, int count);
+int gp2d_dfact_alpha_blocks(const double* W, int64_t n, int64_t ldw, int t0, int dt, int count, const double* z,
+                            double* alpha, void* work, size_t work_bytes, void* stream);
+int gp2d_assemble_cols(const double* x, int64_t n, int64_t n_pad, const gp2d_kernel_t* k, double diag_add,
+                       double* out, int64_t ld, int64_t c0, int64_t ncols, void* stream);
 int gp2d_copy2d(double* dst, int64_t ldd, const double* src, int64_t lds, int64_t rows, int64_t cols,
                 void* stream);
 int gp2d_zero_upper(double* A, int64_t n, int64_t lda, void* stream);
