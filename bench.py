@@ -538,8 +538,10 @@ def main():
     achieved = kflops / (kms * 1e-3) / 1e12 if kms > 0 else None
     traffic = None   # the committed PMC pass was taken at the headline workload only
     headline = (args.kind, args.ntrain, G, strong) == ("df", 4096, 256, False)
-    pmc_round = "r03" if args.variance == "ozaki" else "r02"   # the latest PMC pass of each engine
-    pmc_json = args.pmc_json or os.path.join(ROOT, "profiles", f"{pmc_round}_pmc_traffic_{args.variance}.json")
+    # the latest committed PMC pass of this engine (profiles/rNN_pmc_traffic_<engine>.json)
+    import glob
+    found = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r[0-9][0-9]_pmc_traffic_{args.variance}.json")))
+    pmc_json = args.pmc_json or (found[-1] if found else "")
     traffic_source = None
     try:
         with open(pmc_json) as f:
@@ -547,7 +549,7 @@ def main():
         traffic = pmc.get("hbm_bytes_per_launch") if (headline or args.pmc_json) else None
         if traffic is not None:   # a separate builder run of rocprofv3 --pmc, not measured in this run
             traffic_source = (f"{os.path.relpath(pmc_json, ROOT)}: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes "
-                              f"(separate runs, {pmc.get('round', os.path.basename(pmc_json)[:3])}) of this kernel at "
+                              f"(separate runs, {pmc.get('round', os.path.basename(pmc_json).split('_')[0])}) of this kernel at "
                               "this workload; not measured inside this bench run")
     except (OSError, ValueError):
         pass
