@@ -288,3 +288,18 @@ def test_factor_join_mode_is_per_thread_and_restorable():
     assert seen == [0]
     assert L.gp2d_factor_join(0) == 1
     assert L.gp2d_factor_join(-1) == 0
+
+
+def test_job_shape_defaults_live_in_the_library():
+    """engine.auto_fits_ahead / hyper.auto_concurrent: config B's small jobs
+    run back to back, the headline / C / D shapes pipelined; a sweep overlaps only when there is a
+    gradient and a next setting — and bench.py carries no per-config override."""
+    from gp2d import engine as E
+    from gp2d import hyper as H
+    df, mixed = E.KernelSpec(kind="df"), E.KernelSpec(kind="mixed", ratio=0.5)
+    assert E.auto_fits_ahead(df, 1024, 128 * 128) == 0
+    assert E.auto_fits_ahead(df, 4096, 256 * 256) == 1
+    assert E.auto_fits_ahead(mixed, 16384, 512 * 512) == 1
+    assert H.auto_concurrent(8, True) == 2 and H.auto_concurrent(8, False) == 1 and H.auto_concurrent(1, True) == 1
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    assert "a.fits_ahead = 0" not in src and "sweep_concurrent or 2" not in src
