@@ -206,6 +206,17 @@ def cpu_baseline(x, y, xg, kind, l, noise, sample_pts):
                       f"grid points ({t2 - t1:.2f} s), predict extrapolated linearly; OpenBLAS threads={cores}"}
 
 
+def _pmc_round(path: str, pmc: dict) -> str:
+    """The round a PMC pass belongs to: its 'round' field, else the rNN prefix of the file or of
+    its directory (profiles/r04_pmc_traffic_ozaki.json, gpurun_out/r04/pmc_traffic_ozaki.json)."""
+    import re
+    for part in (pmc.get("round"), os.path.basename(path), os.path.basename(os.path.dirname(path))):
+        m = re.match(r"(r\d\d)", part or "")
+        if m:
+            return m.group(1)
+    return "round unknown"
+
+
 def config_e_settings():
     """BASELINE config E's 64 settings: l_df on 8 log-spaced values in [2, 12] km x noise on 8
     log-spaced values in [1e-3, 5e-2] (the same grid as the committed config-E fixture)."""
@@ -549,7 +560,7 @@ def main():
         traffic = pmc.get("hbm_bytes_per_launch") if (headline or args.pmc_json) else None
         if traffic is not None:   # a separate builder run of rocprofv3 --pmc, not measured in this run
             traffic_source = (f"{os.path.relpath(pmc_json, ROOT)}: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes "
-                              f"(separate runs, {pmc.get('round', os.path.basename(pmc_json).split('_')[0])}) of this kernel at "
+                              f"(separate runs, {_pmc_round(pmc_json, pmc)}) of this kernel at "
                               "this workload; not measured inside this bench run")
     except (OSError, ValueError):
         pass
