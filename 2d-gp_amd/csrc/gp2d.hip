@@ -1114,18 +1114,6 @@ static size_t oz_list_bytes(int64_t n, int64_t chunk) {
   return sizeof(int) * (size_t)(nbj * ks + nbj * (ks / 4 + 1));
 }
 
-// the second mean-partials buffer (chunk parity): the next chunk's K* kernel writes its
-// partials while the CRT stream's finalize still reads this chunk's
-static size_t oz_pm2_bytes(int64_t n, int64_t chunk) {
-  const int64_t ncols = 2 * round_up(chunk < 1 ? 1 : chunk, IBN);
-  return 256 + sizeof(double) * (size_t)std::max<int64_t>(n / 2 / OZ_KS_T + 1, n / OZ_CRT_ROWS + 1) * (size_t)ncols;
-}
-// its place: after the slab lists, 256-byte aligned
-static double* oz_pm2_at(const int* skip, int64_t n, int64_t chunk) {
-  const uintptr_t a = reinterpret_cast<uintptr_t>(skip) + oz_list_bytes(n, chunk);
-  return reinterpret_cast<double*>((a + 255) & ~(uintptr_t)255);
-}
-
 size_t gp2d_predict_ozaki_workspace(int64_t n, int64_t chunk) {
   const int nm = ozaki_nmod_for(n);
   if (nm <= 0) return 0;
@@ -1133,53 +1121,7 @@ size_t gp2d_predict_ozaki_workspace(int64_t n, int64_t chunk) {
   const int64_t ncols = 2 * cp;
   return 2 * (size_t)nm * (size_t)n * (size_t)ncols                        // Bres + Cres planes
          + sizeof(double) * ((size_t)(n / 2 / OZ_KS_T + 1) + (size_t)(n / OZ_CRT_ROWS + 1)) * ncols
-         + oz_flag_bytes(n, chunk) + oz_list_bytes(n, chunk) + oz_pm2_bytes(n, chunk);
-}
-
-// ---- the CRT stream: chunk c's CRT + finalize run beside chunk c+1's K* kernel (VALU-bound
-// residue generation beside an HBM-read-bound reconstruction) instead of after it.  One stream
-// per device, created lazily at the caller's priority; a predict holds its mutex across its
-// enqueue sequence (the two events are reused call after call).
-}  // extern "C"
-namespace {
-struct CrtStream {
-  std::mutex mu;
-  hipStream_t s = nullptr;
-  hipEvent_t e_gemm = nullptr, e_crt = nullptr;
-};
-std::mutex g_crt_mu;
-std::vector<std::unique_ptr<CrtStream>> g_crt;
-int g_crt_side = -1;   // -1: from GP2D_OZ_CRT_SIDE (default on)
-
-CrtStream* crt_stream(hipStream_t caller) {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) { set_error("hipGetDevice failed"); return nullptr; }
-  std::lock_guard<std::mutex> lk(g_crt_mu);
-  if (g_crt_side < 0) {
-    const char* e = std::getenv("GP2D_OZ_CRT_SIDE");
-    g_crt_side = (e == nullptr || std::atoi(e) != 0) ? 1 : 0;
-  }
-  if ((int)g_crt.size() <= dev) g_crt.resize(dev + 1);
-  if (!g_crt[dev]) {
-    auto c = std::make_unique<CrtStream>();
-    int prio = 0;
-    if (caller == nullptr || hipStreamGetPriority(caller, &prio) != hipSuccess) prio = 0;
-    if (hipStreamCreateWithPriority(&c->s, hipStreamNonBlocking, prio) != hipSuccess ||
-        hipEventCreateWithFlags(&c->e_gemm, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->e_crt, hipEventDisableTiming) != hipSuccess) {
-      set_error("ozaki: creating the CRT stream failed");
-      return nullptr;
-    }
-    g_crt[dev] = std::move(c);
-  }
-  return g_crt[dev].get();
-}
-}  // namespace
-extern "C" {
-
-void gp2d_ozaki_set_crt_side(int on) {
-  std::lock_guard<std::mutex> lk(g_crt_mu);
-  g_crt_side = on ? 1 : 0;
+         + oz_flag_bytes(n, chunk) + oz_list_bytes(n, chunk);
 }
 
 void gp2d_ozaki_set_skip(int on) { g_oz_skip = on ? 1 : 0; }
@@ -1194,8 +1136,8 @@ static int predict_ozaki_impl(const int8_t* wres, const double* rowscale, int nm
                               const double* alpha, const double* xtr, int64_t ntr,
                               int64_t ntr_pad, const double* xg, int64_t m, const gp2d_kernel_t* k, int var_mode,
                               double noise, int compute_var, double* mean, double* var, int64_t chunk,
-                              int8_t* bres, uint8_t* cres, double* pm0, double* pm1, double* P, uint8_t* flags,
-                              int* skip, const int8_t* pre, size_t pre_stride, size_t pre_flags, hipStream_t s) {
+                              int8_t* bres, uint8_t* cres, double* pm, double* P, uint8_t* flags, int* skip,
+                              const int8_t* pre, size_t pre_stride, size_t pre_flags, hipStream_t s) {
   OzakiConsts oc;
   GP2D_CHECK(make_ozaki_consts(nmod, k, oc));
   const int nm = oc.nmod;
@@ -1209,21 +1151,8 @@ static int predict_ozaki_impl(const int8_t* wres, const double* rowscale, int nm
   const VecParams vp = make_vec_params(k);
   OzakiConsts oc_mean_only = oc;
   oc_mean_only.nmod = 0;   // mean only: K*·α without the residue planes
-  // the CRT stream (variance only, more than one chunk): chunk c's CRT and finalize follow its
-  // GEMMs there while chunk c+1's K* kernel runs on s; chunk c+1's GEMMs (which overwrite the
-  // residue planes cres) wait for chunk c's CRT.  The mean partials alternate between pm0 / pm1.
-  CrtStream* cs = nullptr;
-  std::unique_lock<std::mutex> cs_lock;
-  if (compute_var && m > chunk) {
-    cs = crt_stream(s);
-    if (cs == nullptr) return -1;
-    if (!g_crt_side) cs = nullptr;
-    else cs_lock = std::unique_lock<std::mutex>(cs->mu);
-  }
-  hipStream_t sc = cs ? cs->s : s;
   int64_t ci = 0;
   for (int64_t c0 = 0; c0 < m; c0 += chunk, ++ci) {
-    double* pm = (cs && (ci & 1)) ? pm1 : pm0;
     const int64_t cv = std::min<int64_t>(chunk, m - c0);
     const int64_t cp = round_up(cv, IBN);   // whole 256-row tiles per component half (B aliasing)
     const int64_t ncols = 2 * cp;
@@ -1250,7 +1179,6 @@ static int predict_ozaki_impl(const int8_t* wres, const double* rowscale, int nm
         if (g_timing.on) { e0 = g_timing.get(); e1 = g_timing.get(); hipEventRecord(e0, s); }
       }
       const dim3 ggrid((unsigned)(ncols / IBN), (unsigned)(n / IBM));
-      if (cs && ci > 0) GP2D_EV(hipStreamWaitEvent(s, cs->e_crt, 0));   // chunk c−1's CRT has read cres
       for (int l = 0; l < nm; ++l) {
         const int8_t* Al = wres + (size_t)l * n * n;
         const int8_t* Bl = B + (size_t)l * bplane;
@@ -1267,22 +1195,13 @@ static int predict_ozaki_impl(const int8_t* wres, const double* rowscale, int nm
         const double nv = 2.0 * (double)ntr;
         g_timing.flops.push_back(2.0 * (double)cv * nv * nv);  // FP64-equivalent algorithmic flop
       }
-      if (cs) {
-        GP2D_EV(hipEventRecord(cs->e_gemm, s));
-        GP2D_EV(hipStreamWaitEvent(sc, cs->e_gemm, 0));
-      }
       const dim3 cgrid((unsigned)((ncols + OZ_CRT_BCOLS - 1) / OZ_CRT_BCOLS), (unsigned)npseg);
-      ozaki_crt_colsq_kernel<<<cgrid, 256, 0, sc>>>(cres, n, ncols, oc, rowscale, P);
+      ozaki_crt_colsq_kernel<<<cgrid, 256, 0, s>>>(cres, n, ncols, oc, rowscale, P);
       GP2D_CHECK(check_launch("ozaki_crt_colsq_kernel"));
-      if (cs) GP2D_EV(hipEventRecord(cs->e_crt, sc));
     }
-    predict_finalize_kernel<<<(unsigned)((ncols + 63) / 64), 64, 0, sc>>>(
+    predict_finalize_kernel<<<(unsigned)((ncols + 63) / 64), 64, 0, s>>>(
         pm, nmseg, P, npseg, ncols, cp, cv, c0, m, kss, add, clip, compute_var, mean, var);
     GP2D_CHECK(check_launch("predict_finalize_kernel"));
-  }
-  if (cs) {   // the caller's stream joins the last chunk's CRT and finalize
-    GP2D_EV(hipEventRecord(cs->e_crt, sc));
-    GP2D_EV(hipStreamWaitEvent(s, cs->e_crt, 0));
   }
   return 0;
 }
@@ -1313,9 +1232,8 @@ int gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int nmod, int
   double* P = pm + (size_t)(n / 2 / OZ_KS_T + 1) * ncols_max;
   uint8_t* flags = reinterpret_cast<uint8_t*>(P + (size_t)(n / OZ_CRT_ROWS + 1) * ncols_max);
   int* skip = reinterpret_cast<int*>(flags + oz_flag_bytes(n, chunk));
-  double* pm1 = oz_pm2_at(skip, n, chunk);
   return predict_ozaki_impl(wres, rowscale, nmod, n, alpha, xtr, ntr, ntr_pad, xg, m, k, var_mode, noise,
-                            compute_var, mean, var, chunk, bres, cres, pm, pm1, P, flags, skip, nullptr, 0, 0,
+                            compute_var, mean, var, chunk, bres, cres, pm, P, flags, skip, nullptr, 0, 0,
                             S(stream));
 }
 
@@ -1381,7 +1299,7 @@ size_t gp2d_predict_ozaki_planes_workspace(int64_t n, int64_t chunk) {
   if (nm <= 0 || n <= 0) return 0;
   const int64_t ncols = 2 * round_up(chunk < 1 ? 1 : chunk, IBN);
   return (size_t)nm * (size_t)n * (size_t)ncols + sizeof(double) * ozaki_partials(n) * (size_t)ncols +
-         oz_list_bytes(n, chunk) + oz_pm2_bytes(n, chunk);
+         oz_list_bytes(n, chunk);
 }
 
 int gp2d_predict_ozaki_planes(const int8_t* wres, const double* rowscale, int nmod, int64_t n, const double* alpha,
@@ -1407,11 +1325,10 @@ int gp2d_predict_ozaki_planes(const int8_t* wres, const double* rowscale, int nm
   double* pm = reinterpret_cast<double*>(cres + (size_t)nmod * n * ncols_max);
   double* P = pm + (size_t)std::max<int64_t>(n / 2 / OZ_KS_T + 1, n / OZ_CRT_ROWS + 1) * ncols_max;
   int* skip = reinterpret_cast<int*>(P + (size_t)(n / OZ_CRT_ROWS + 1) * ncols_max);
-  double* pm1 = oz_pm2_at(skip, n, chunk);
   const size_t planes = (size_t)nmod_b * (size_t)n * (size_t)ncols_max;
   const size_t stride = planes + oz_flag_bytes(n, chunk);
   return predict_ozaki_impl(wres, rowscale, nmod, n, alpha, xtr, ntr, ntr_pad, xg, m, k, var_mode, noise, 1, mean,
-                            var, chunk, nullptr, cres, pm, pm1, P, nullptr, skip, bres, stride, planes, S(stream));
+                            var, chunk, nullptr, cres, pm, P, nullptr, skip, bres, stride, planes, S(stream));
 }
 
 int gp2d_morton_codes(const double* pts, int64_t n, int dim, double* bbox, int64_t* codes, void* stream) {

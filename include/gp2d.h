@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define GP2D_ABI_VERSION 8
+#define GP2D_ABI_VERSION 7
 
 /* kernel families */
 #define GP2D_FAMILY_VECTOR2D 0   /* 2×2 matrix-valued SE kernels on (x1, x2)          */
@@ -177,13 +177,6 @@ size_t gp2d_predict_ozaki_workspace(int64_t n, int64_t chunk);
  * a 256-row grid tile — exact, such slabs add nothing.  gp2d_ozaki_set_skip(0) runs them
  * dense (A/B measurement and the bit-identity test); default on.                       */
 void   gp2d_ozaki_set_skip(int on);
-/* With more than one chunk, chunk c's CRT reconstruction and finalize run on an internal
- * stream (one per device, the caller's priority) beside chunk c+1's K* kernel, and chunk
- * c+1's GEMMs wait for chunk c's CRT; the caller's stream joins the last one before
- * gp2d_predict_ozaki / _planes return.  Same kernels, same bits.  gp2d_ozaki_set_crt_side(0)
- * (or GP2D_OZ_CRT_SIDE=0) keeps everything on the caller's stream (A/B measurement and the
- * bit-identity test); default on.  ABI 8: the workspaces hold a second mean-partials buffer. */
-void   gp2d_ozaki_set_crt_side(int on);
 /* Z-order (Morton) codes of n points (dim 2 or 3) in their bounding box, 21 bits per
  * coordinate (bbox: 6 doubles of device scratch).  The ozaki engine sorts training and grid
  * points by these codes so that all-zero K* tiles cluster into skippable slabs.          */

@@ -232,37 +232,6 @@ def test_zero_slab_skip_is_exact(kind, l):
     assert rel(vs[idx], vo) < 1e-10 and rel(ms[idx], mo) < 1e-10
 
 
-@pytest.mark.parametrize("ntr,m,chunk", [(300, 2300, 512), (700, 5000, 1024), (128, 300, 512)])
-def test_crt_stream_bit_identical(ntr, m, chunk):
-    """Chunk c's CRT + finalize on the internal CRT stream beside chunk c+1's K* kernel
-    (gp2d_ozaki_set_crt_side, default on) return the bits of the one-stream order, for the
-    inline-planes and the planes-ahead predicts, with a ragged last chunk and with one chunk;
-    two predicts back to back on one workspace (the second chunk-0 GEMMs after the first's
-    last CRT) agree as well."""
-    x, y = tracks(ntr, ntr + 7)
-    rng = np.random.default_rng(m)
-    xg = np.stack([rng.uniform(-5, 65, m), rng.uniform(-5, 50, m)], 1)
-    ks = E.KernelSpec(kind="mixed", l_df=5.0, l_cf=4.0, ratio=0.5)
-    L = E.N.lib()
-    try:
-        L.gp2d_ozaki_set_crt_side(0)
-        gp, planes, ma0, va0 = _ahead(ks, x, y, xg, 0.0025, chunk)
-        m0, v0 = (t.cpu().numpy() for t in E.Predictor(gp, chunk)(xg))
-    finally:
-        L.gp2d_ozaki_set_crt_side(1)
-    pr = E.Predictor(gp, chunk)
-    m1, v1 = (t.cpu().numpy() for t in pr(xg))
-    m2, v2 = (t.cpu().numpy() for t in pr(xg))
-    ma1, va1 = (t.cpu().numpy() for t in pr(xg, planes=planes))
-    assert np.array_equal(m0, m1) and np.array_equal(v0, v1)
-    assert np.array_equal(m1, m2) and np.array_equal(v1, v2)
-    assert np.array_equal(ma0, ma1) and np.array_equal(va0, va1) and np.array_equal(va1, v1)
-    sub = np.arange(0, m, max(1, m // 150))
-    mo, vo = O.fit_predict(x, y, xg[sub], kind="mixed", l_df=5.0, l_cf=4.0, ratio=0.5, noise=0.0025)
-    idx = np.concatenate([sub, m + sub])
-    assert rel(v1[idx], vo) < 1e-10 and rel(m1[idx], mo) < 1e-10
-
-
 def test_zero_slab_skip_far_grid_and_planes():
     """A grid block far from every observation: every K slab is skipped (empty list), so the
     variance is exactly the prior kss and the mean exactly 0; the K*-planes-ahead path (block
