@@ -155,6 +155,7 @@ static int make_ozaki_consts(int nmod, const gp2d_kernel_t* k, OzakiConsts& oc) 
   oc.M = M;
   for (int l = 0; l < OZ_MAXMOD; ++l) {
     oc.m[l] = kModuli[l];
+    oc.md[l] = (double)kModuli[l];
     oc.inv_m[l] = 1.0 / (double)kModuli[l];
     oc.h[l] = oc.t[l] = 0.0;
   }
@@ -1126,6 +1127,16 @@ size_t gp2d_predict_ozaki_workspace(int64_t n, int64_t chunk) {
 
 void gp2d_ozaki_set_skip(int on) { g_oz_skip = on ? 1 : 0; }
 
+// ozaki_kstar_kernel with buffer stores whenever a plane (n × 2·cp bytes) is below 2 GiB
+static void launch_kstar(dim3 grid, hipStream_t s, const double* xtr, int64_t ntr, int64_t npad, const double* xg,
+                         int64_t cv, int64_t cp, const VecParams& vp, const double* alpha, const OzakiConsts& oc,
+                         int8_t* bres, double* pm, uint8_t* flags) {
+  if ((uint64_t)(2 * npad) * (uint64_t)(2 * cp) < (1ull << 31))
+    ozaki_kstar_kernel<true><<<grid, 256, 0, s>>>(xtr, ntr, npad, xg, cv, cp, vp, alpha, oc, bres, pm, flags);
+  else
+    ozaki_kstar_kernel<false><<<grid, 256, 0, s>>>(xtr, ntr, npad, xg, cv, cp, vp, alpha, oc, bres, pm, flags);
+}
+
 // One chunked predict over the m grid points.  K* residue planes come either from the
 // inline ozaki_kstar_kernel (pre == nullptr: planes in the workspace, mean partials Σ α·K*)
 // or from gp2d_ozaki_kstar run earlier (pre: planes per chunk at pre + c·pre_stride, their
@@ -1160,9 +1171,8 @@ static int predict_ozaki_impl(const int8_t* wres, const double* rowscale, int nm
     const uint8_t* F = pre ? reinterpret_cast<const uint8_t*>(B) + pre_flags : flags;
     const size_t bplane = (size_t)ncols * n;
     const bool inline_planes = compute_var && !pre;
-    ozaki_kstar_kernel<<<dim3((unsigned)nmseg, (unsigned)(cp / OZ_KS_P)), 256, 0, s>>>(
-        xtr, ntr, ntr_pad, xg + point_dim(k) * c0, cv, cp, vp, alpha, inline_planes ? oc : oc_mean_only, bres, pm,
-        inline_planes ? flags : nullptr);
+    launch_kstar(dim3((unsigned)nmseg, (unsigned)(cp / OZ_KS_P)), s, xtr, ntr, ntr_pad, xg + point_dim(k) * c0, cv,
+                 cp, vp, alpha, inline_planes ? oc : oc_mean_only, bres, pm, inline_planes ? flags : nullptr);
     GP2D_CHECK(check_launch("ozaki_kstar_kernel"));
     const int nbj = (int)(ncols / IBN), kslabs = (int)(n / IBK);
     const bool use_skip = compute_var && g_oz_skip && kslabs <= (1 << 20);
@@ -1286,9 +1296,8 @@ int gp2d_ozaki_kstar(const double* xtr, int64_t ntr, int64_t ntr_pad, const doub
     const int64_t cv = std::min<int64_t>(chunk, m - c0);
     const int64_t cp = round_up(cv, IBN);
     int8_t* bc = bres + ci * stride;
-    ozaki_kstar_kernel<<<dim3((unsigned)nmseg, (unsigned)(cp / OZ_KS_P)), 256, 0, s>>>(
-        xtr, ntr, ntr_pad, xg + point_dim(k) * c0, cv, cp, vp, nullptr, oc, bc, nullptr,
-        reinterpret_cast<uint8_t*>(bc + planes));
+    launch_kstar(dim3((unsigned)nmseg, (unsigned)(cp / OZ_KS_P)), s, xtr, ntr, ntr_pad, xg + point_dim(k) * c0, cv,
+                 cp, vp, nullptr, oc, bc, nullptr, reinterpret_cast<uint8_t*>(bc + planes));
     GP2D_CHECK(check_launch("ozaki_kstar_kernel"));
   }
   return 0;

@@ -46,6 +46,7 @@ constexpr int OZ_HBITS = 33;       // exact high part of inv_l / m_l
 struct OzakiConsts {
   int nmod;
   int m[OZ_MAXMOD];
+  double md[OZ_MAXMOD];            // m_l as a double (the residue kernels' fma operand)
   double inv_m[OZ_MAXMOD];         // 1 / m_l
   double h[OZ_MAXMOD];             // inv_l / m_l rounded to a multiple of 2^-33
   double t[OZ_MAXMOD];             // inv_l / m_l − h_l
@@ -58,10 +59,18 @@ struct OzakiConsts {
 // (for odd m the fraction x/m is ≥ 1/(2m) away from ½, far above the product's rounding
 // error; m = 256 divides exactly), so r = x − m·q ∈ [−m/2, m/2] and its low byte is the
 // centred residue in [−128, 127] (r = ±128 only for m = 256, where 0x80 ≡ 128 ≡ −128).  No
-// range fix-ups: 4 VALU operations per residue (they were 8 with the fix-ups).
-__device__ __forceinline__ uint32_t residue_byte(double x, double m, double inv_m) {
-  return (uint32_t)(int)fma(-m, rint(x * inv_m), x) & 0xffu;
+// range fix-ups and no conversion: with xm = x + 1.5·2^52 (exact for |x| < 2^51; one add per
+// x, shared by every modulus) fma(−m, q, xm) = 1.5·2^52 + r exactly (in [2^52, 2^53), ulp 1),
+// whose mantissa is 2^51 + r, so the low 32 bits of the double are r in two's complement.
+// 3 VALU operations per residue (4 with a cvt_i32_f64, 8 with the fix-ups).
+constexpr double OZ_MAGIC52 = 6755399441055744.0;   // 1.5·2^52
+__device__ __forceinline__ uint32_t residue_low_m(double x, double xm, double m, double inv_m) {
+  return (uint32_t)__double_as_longlong(fma(-m, rint(x * inv_m), xm));   // low byte: the residue
 }
+// low bytes of a (byte 0) and b (byte 1); bytes 2, 3 zero — one v_perm_b32
+__device__ __forceinline__ uint32_t pack2_lo(uint32_t a, uint32_t b) { return __builtin_amdgcn_perm(b, a, 0x0c0c0400u); }
+// bytes 0-1 of a, then bytes 0-1 of b
+__device__ __forceinline__ uint32_t pack22(uint32_t a, uint32_t b) { return __builtin_amdgcn_perm(b, a, 0x05040100u); }
 
 // Slab-blocked residue planes (see the INT8 GEMM below): element (row, k) of a plane with K
 // columns; a 256-row × 64-byte tile is one contiguous 16 KB.
@@ -145,16 +154,19 @@ __global__ __launch_bounds__(256) void ozaki_w_res_kernel(const double* __restri
     const double* w = W + i * ldw + k0;
     const d2 p0 = *reinterpret_cast<const d2*>(w), p1 = *reinterpret_cast<const d2*>(w + 2);
     const double v[4] = {p0.x, p0.y, p1.x, p1.y};
-    double x[4];
+    double x[4], xm[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) x[u] = (k0 + u <= i) ? rint(ldexp(v[u], si)) : 0.0;
+    for (int u = 0; u < 4; ++u) {
+      x[u] = (k0 + u <= i) ? rint(ldexp(v[u], si)) : 0.0;
+      xm[u] = x[u] + OZ_MAGIC52;
+    }
     int8_t* dst = wres + slab_offset(i, k0, n);
     for (int l = 0; l < oc.nmod; ++l) {
-      const double m = (double)oc.m[l];
-      uint32_t packed = 0;
+      const double m = oc.md[l], im = oc.inv_m[l];
+      uint32_t r[4];   // |x| < 2^pW
 #pragma unroll
-      for (int u = 0; u < 4; ++u) packed |= residue_byte(x[u], m, oc.inv_m[l]) << (8 * u);   // |x| < 2^pW
-      *reinterpret_cast<uint32_t*>(dst + (int64_t)l * plane) = packed;
+      for (int u = 0; u < 4; ++u) r[u] = residue_low_m(x[u], xm[u], m, im);
+      *reinterpret_cast<uint32_t*>(dst + (int64_t)l * plane) = pack22(pack2_lo(r[0], r[1]), pack2_lo(r[2], r[3]));
     }
   }
 }
@@ -185,6 +197,10 @@ template <int PPL> struct packed_bytes;   // PPL residue bytes of one lane, stor
 template <> struct packed_bytes<2> { typedef uint16_t type; };
 template <> struct packed_bytes<4> { typedef uint32_t type; };
 
+// OFF32: a plane (n·2·cp bytes) is below 2^31 (the launcher checks), so the stores are buffer
+// stores — the plane in a scalar buffer resource, the 32-bit offsets computed once per grid
+// point — instead of three 64-bit address additions per modulus.
+template <bool OFF32>
 __global__ __launch_bounds__(256, GP2D_KS_OCC) void ozaki_kstar_kernel(
     const double* __restrict__ xtr, int64_t ntr, int64_t npad, const double* __restrict__ xg, int64_t cv,
     int64_t cp, VecParams vp, const double* __restrict__ alpha, OzakiConsts oc, int8_t* __restrict__ bres,
@@ -241,32 +257,49 @@ __global__ __launch_bounds__(256, GP2D_KS_OCC) void ozaki_kstar_kernel(
     if (p >= cp || t0 >= npad) continue;   // npad is a multiple of 64: whole point groups
     // The (v,u) block equals the (u,v) block (k12 is symmetric in the 2×2 kernel block), so
     // only (u,u), (u,v) and (v,v) are stored: the GEMM reads (v,u) tiles from (u,v).
-    double xi[3][PPL];  // [entry: (u,u) (u,v) (v,v)][u]
+    double xi[3][PPL], xm[3][PPL];  // [entry: (u,u) (u,v) (v,v)][u]; xm = xi + 1.5·2^52
 #pragma unroll
     for (int u = 0; u < PPL; ++u) {
       xi[0][u] = rint(k11[u] * scale);
       xi[1][u] = rint(k12[u] * scale);
       xi[2][u] = rint(k22[u] * scale);
       nz = nz || xi[0][u] != 0.0 || xi[1][u] != 0.0 || xi[2][u] != 0.0;
+#pragma unroll
+      for (int e = 0; e < 3; ++e) xm[e][u] = xi[e][u] + OZ_MAGIC52;
     }
     // (grid comp, train comp): (u,u) → row p, col t ; (u,v) → row p, col npad+t ;
     //                          (v,v) → row cp+p, col npad+t ; (v,u) not stored
     const int64_t o_uu = slab_offset(p, t0, n), o_uv = slab_offset(p, npad + t0, n),
                   o_vv = slab_offset(cp + p, npad + t0, n);
+    const int64_t pstride = ncols * n;
     for (int l = 0; l < oc.nmod; ++l) {
-      const double m = (double)oc.m[l], im = oc.inv_m[l];
+      const double m = oc.md[l], im = oc.inv_m[l];
       pk_t pk[3];
 #pragma unroll
       for (int e = 0; e < 3; ++e) {
-        uint32_t w = 0;
+        uint32_t r[PPL];   // |xi| < 2^pB
 #pragma unroll
-        for (int u = 0; u < PPL; ++u) w |= residue_byte(xi[e][u], m, im) << (8 * u);   // |xi| < 2^pB
-        pk[e] = (pk_t)w;
+        for (int u = 0; u < PPL; ++u) r[u] = residue_low_m(xi[e][u], xm[e][u], m, im);
+        if constexpr (PPL == 2) pk[e] = (pk_t)pack2_lo(r[0], r[1]);
+        else pk[e] = (pk_t)pack22(pack2_lo(r[0], r[1]), pack2_lo(r[2], r[3]));
       }
-      int8_t* plane = bres + (int64_t)l * ncols * n;
-      *reinterpret_cast<pk_t*>(plane + o_uu) = pk[0];
-      *reinterpret_cast<pk_t*>(plane + o_uv) = pk[1];
-      *reinterpret_cast<pk_t*>(plane + o_vv) = pk[2];
+      int8_t* plane = bres + (int64_t)l * pstride;
+      if constexpr (OFF32) {   // buffer stores: the plane in a scalar resource, 32-bit offsets
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(plane, (short)0, (int)pstride, 0x00020000);
+        if constexpr (PPL == 2) {
+          __builtin_amdgcn_raw_buffer_store_b16(pk[0], rs, (int)o_uu, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b16(pk[1], rs, (int)o_uv, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b16(pk[2], rs, (int)o_vv, 0, 0);
+        } else {
+          __builtin_amdgcn_raw_buffer_store_b32(pk[0], rs, (int)o_uu, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(pk[1], rs, (int)o_uv, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(pk[2], rs, (int)o_vv, 0, 0);
+        }
+      } else {
+        *reinterpret_cast<pk_t*>(plane + o_uu) = pk[0];
+        *reinterpret_cast<pk_t*>(plane + o_uv) = pk[1];
+        *reinterpret_cast<pk_t*>(plane + o_vv) = pk[2];
+      }
     }
   }
   // block flag (grid block by, training block bx): 0 iff every stored residue is zero, so the
@@ -675,26 +708,41 @@ __global__ __launch_bounds__(256) void morton_code_kernel(const double* __restri
 
 // ------------------------------------------------------------------ CRT + column Σ V²
 // Residue planes are column-major ([j][i], ld = n).  One wave per OZ_CRT_COLS consecutive
-// columns and a 1024-row segment: lane l reconstructs rows 16l..16l+15 (one 16-B load per
-// plane and column), squares, and the wave reduces each column in a fixed shuffle order →
-// partial[seg][j].  The lane's 16 row scales stay in registers across the wave's columns.
-constexpr int OZ_CRT_ROWS = 1024;
+// columns and a 64·RPL-row segment: lane l reconstructs rows RPL·l .. RPL·l + RPL − 1 (one
+// RPL-byte load per plane and column), squares, and the wave reduces each column in a fixed
+// shuffle order → partial[seg][j].  The lane's RPL row scales stay in registers across the
+// wave's columns.
+#ifndef GP2D_CRT_RPL
+#define GP2D_CRT_RPL 16   // rows per lane: 16 (124 VGPRs, 4 waves per SIMD) or 8
+#endif
+constexpr int OZ_CRT_RPL = GP2D_CRT_RPL;
+static_assert(OZ_CRT_RPL == 16 || OZ_CRT_RPL == 8, "CRT rows per lane: 16 or 8");
+constexpr int OZ_CRT_ROWS = 64 * OZ_CRT_RPL;
 constexpr int OZ_CRT_COLS = 4;    // columns per wave
 constexpr int OZ_CRT_BCOLS = 4 * OZ_CRT_COLS;   // columns per 256-thread block
 
-__global__ __launch_bounds__(256) void ozaki_crt_colsq_kernel(const uint8_t* __restrict__ cres, int64_t n,
+template <int RPL> struct crt_load;
+template <> struct crt_load<16> { typedef uint4 type; };
+template <> struct crt_load<8> { typedef uint2 type; };
+
+#ifndef GP2D_CRT_OCC
+#define GP2D_CRT_OCC 1   // min workgroups (= waves per SIMD) per CU the register budget must allow
+#endif
+__global__ __launch_bounds__(256, GP2D_CRT_OCC) void ozaki_crt_colsq_kernel(const uint8_t* __restrict__ cres, int64_t n,
                                                               int64_t ncols, OzakiConsts oc,
                                                               const double* __restrict__ rowscale,
                                                               double* __restrict__ P) {
+  constexpr int RPL = OZ_CRT_RPL;
+  typedef typename crt_load<RPL>::type ld_t;
   const int lane = threadIdx.x & 63;
   const int64_t jw = (int64_t)blockIdx.x * OZ_CRT_BCOLS + (threadIdx.x >> 6) * OZ_CRT_COLS;
   const int64_t seg = blockIdx.y;
-  const int64_t i0 = seg * OZ_CRT_ROWS + 16 * lane;
+  const int64_t i0 = seg * OZ_CRT_ROWS + RPL * lane;
   if (jw >= ncols) return;
   const bool rows_ok = i0 < n;
-  double rs[16];
+  double rs[RPL];
 #pragma unroll
-  for (int c = 0; c < 16; ++c) rs[c] = rows_ok ? rowscale[i0 + c] : 0.0;
+  for (int c = 0; c < RPL; ++c) rs[c] = rows_ok ? rowscale[i0 + c] : 0.0;
   const int64_t plane = n * ncols;
 #pragma unroll 1
   for (int jc = 0; jc < OZ_CRT_COLS; ++jc) {
@@ -702,23 +750,23 @@ __global__ __launch_bounds__(256) void ozaki_crt_colsq_kernel(const uint8_t* __r
     if (j >= ncols) break;
     double acc = 0.0;
     if (rows_ok) {
-      double H[16], T[16];
+      double H[RPL], T[RPL];
 #pragma unroll
-      for (int c = 0; c < 16; ++c) { H[c] = 0.0; T[c] = 0.0; }
+      for (int c = 0; c < RPL; ++c) { H[c] = 0.0; T[c] = 0.0; }
       // planes in groups of 4 with the group's loads issued together; a group's planes past
       // nmod re-read plane nmod−1 (cached) and add nothing (h = t = 0 beyond nmod)
       const int nm1 = oc.nmod - 1;
       for (int l0 = 0; l0 < oc.nmod; l0 += 4) {
-        uint4 v[4];
+        ld_t v[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-          v[u] = *reinterpret_cast<const uint4*>(cres + (int64_t)min(l0 + u, nm1) * plane + j * n + i0);
+          v[u] = *reinterpret_cast<const ld_t*>(cres + (int64_t)min(l0 + u, nm1) * plane + j * n + i0);
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+          const uint32_t* w = reinterpret_cast<const uint32_t*>(&v[u]);
           const double h = oc.h[l0 + u], t = oc.t[l0 + u];
 #pragma unroll
-          for (int c = 0; c < 16; ++c) {
+          for (int c = 0; c < RPL; ++c) {
             const double cl = (double)((w[c >> 2] >> (8 * (c & 3))) & 0xffu);
             H[c] = fma(cl, h, H[c]);   // exact: multiples of 2^-33 below 2^12
             T[c] = fma(cl, t, T[c]);
@@ -726,7 +774,7 @@ __global__ __launch_bounds__(256) void ozaki_crt_colsq_kernel(const uint8_t* __r
         }
       }
 #pragma unroll
-      for (int c = 0; c < 16; ++c) {
+      for (int c = 0; c < RPL; ++c) {
         const double f = (H[c] - rint(H[c])) + T[c];   // Pint / M, centred
         const double vij = f * rs[c];
         acc = fma(vij, vij, acc);

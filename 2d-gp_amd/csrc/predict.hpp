@@ -32,11 +32,14 @@ __global__ __launch_bounds__(256) void predict_finalize_kernel(
   const int64_t comp = c / cpad, loc = c - comp * cpad;
   if (loc >= cvalid) return;
   double mu = 0.0;
+  // the same left-to-right sums; unrolled so that eight partials are in flight per thread
+#pragma unroll 8
   for (int64_t g = 0; g < nmseg; ++g) mu += pm[g * ncols + c];
   const int64_t o = comp * m + c0 + loc;
   mean[o] = mu;
   if (compute_var) {
     double q = 0.0;
+#pragma unroll 8
     for (int64_t g = 0; g < npseg; ++g) q += P[g * ncols + c];
     double v = kss - q + add;
     if (clip && v < 0.0) v = 0.0;
