@@ -250,6 +250,35 @@ def test_ozaki_epilogue_reduction_exact():
         assert bias % m == 0 and bias - (K << 14) >= 0 and bias + (K << 14) < (1 << 32)
 
 
+def test_ozaki_residue_low_bytes_exact():
+    """The residue kernels' conversion-free byte (csrc/ozaki.hpp residue_low_m), emulated in
+    fp64: for integers |x| < 2^51 and every modulus, q = rint(x·(1/m)) and
+    (x + 1.5·2^52) − m·q is exact, lies in [2^52, 2^53), and the low byte of its bit pattern is
+    the centred residue's two's-complement byte — the byte the int conversion gave
+    (csrc/ozaki.hpp's former residue_byte: (int)(x − m·q) & 0xff)."""
+    moduli = [256, 255, 253, 251, 247, 241, 239, 233, 229, 227, 223, 217, 211, 199, 197, 193]
+    rng = np.random.default_rng(7)
+    lim = 2.0 ** 51 - 1
+    edges = np.array([0.0, 1.0, -1.0, 127.0, -128.0, 128.0, 2.0 ** 45, -2.0 ** 45, 2.0 ** 49 - 1, -(2.0 ** 49),
+                      lim, -lim])
+    x = np.concatenate([edges, np.rint(rng.uniform(-2.0 ** 49, 2.0 ** 49, 200_000)),
+                        np.rint(rng.uniform(-2.0 ** 12, 2.0 ** 12, 50_000))])
+    xm = x + 6755399441055744.0   # 1.5·2^52: exact for |x| < 2^51
+    assert np.array_equal(xm - 6755399441055744.0, x)
+    for m in moduli:
+        q = np.rint(x * (1.0 / m))
+        r = x - m * q              # the old path: |r| ≤ m/2, exact
+        assert np.abs(r).max() <= m / 2, m
+        rm = xm - m * q            # the new path (fma in the kernel; exact here as well)
+        assert rm.min() >= 2.0 ** 52 and rm.max() < 2.0 ** 53, m
+        assert np.array_equal(rm - 6755399441055744.0, r), m
+        lo = rm.view(np.int64) & 0xFF
+        assert np.array_equal(lo, r.astype(np.int64) & 0xFF), m
+        c = np.mod(x.astype(np.int64), m)             # the residue in [0, m), integer arithmetic
+        centred = np.where(c > m // 2, c - m, c)      # m = 256: ±128 share the byte 0x80
+        assert np.array_equal(lo, centred & 0xFF), m
+
+
 def test_factor_workspaces_cover_the_split_trtri():
     """gp2d_trtri / gp2d_potrf_inv workspaces (host functions, no device needed) include room
     for the high halves of the K-split TRTRI products (the lower levels' products with at most
