@@ -79,5 +79,24 @@ int main() {
     bad += C[(size_t)j * n + i] != want;
   }
   printf("%s: %d of 4096 sampled outputs differ from the CPU dot product\n", VARIANT, bad);
+#ifdef IG_STAMPS
+  // igemm_stamps.hpp: per-wave segment sums of the last launch → shares and per-step cycles
+  std::vector<unsigned long long> st(2048 * 8 * 8);
+  (void)hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(ig_stamp), st.size() * 8);
+  double seg[6] = {0}, steps = 0, waves = 0;
+  for (size_t w = 0; w < st.size() / 8; ++w) {
+    for (int q = 0; q < 6; ++q) seg[q] += (double)st[w * 8 + q];
+    steps += (double)st[w * 8 + 6];
+    waves += 1;
+  }
+  const char* nm[6] = {"work (reads, h1+h0 MFMAs, DMA issue)", "vmcnt wait (own DMA of next slab)", "s_barrier wait",
+                       "ring tail", "epilogue", "prologue"};
+  double tot = 0;
+  for (int q = 0; q < 6; ++q) tot += seg[q];
+  printf("stamps: %.0f waves, %.1f stamped steps per wave, %.0f wave-cycles per wave\n", waves, steps / waves, tot / waves);
+  for (int q = 0; q < 6; ++q)
+    printf("  seg %d %-40s share %.3f  per wave %.0f  per step %.1f\n", q, nm[q], seg[q] / tot, seg[q] / waves,
+           q < 3 ? seg[q] / steps : 0.0);
+#endif
   return 0;
 }

@@ -5,7 +5,8 @@ set -o pipefail
 R=gpurun_out/r04_kstar
 mkdir -p $R
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 600 python -u -m pytest tests/test_gpu_ozaki.py tests/test_gpu_configs.py tests/test_gpu_parity.py tests/test_gpu_jobs.py -x -q --timeout 300 --timeout-method thread > $R/tests.log 2>&1 || exit 1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $R/tests.log 2>&1 || exit 1
+timeout -k 10 120 python -u __graft_entry__.py smoke > $R/smoke.txt 2>&1 || exit 1
 GP2D_LIB=$PWD/build/libgp2d_crt8.so timeout -k 10 400 python -u -m pytest tests/test_gpu_ozaki.py tests/test_gpu_configs.py -x -q --timeout 300 --timeout-method thread > $R/tests_crt8.log 2>&1 || exit 1
 for i in 1 2; do
   timeout -k 10 200 python -u bench.py --steps 100 --warmup 3 --cpu-baseline 0 > $R/bench_$i.json 2> $R/bench_$i.err || exit 1
