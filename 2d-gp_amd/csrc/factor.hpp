@@ -290,11 +290,17 @@ __device__ __forceinline__ void tile4x4_store(double* __restrict__ S, int r, int
 // inv_in_place (the fused factor + inverse, gp2d_potrf_inv): A's diagonal block receives
 // W_kk = L_kk⁻¹ instead of L_kk (nothing reads L_kk from A after this kernel: the panel TRSM
 // uses dinv), which is TRTRI's level 0.
+// Problem batch (gp2d_potrf_batched): workgroup b factors problem b — A + b·sA, dinv + b·sD,
+// info + b (one workgroup and sA = sD = 0 for a lone factorisation).
 __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A, int64_t lda, int k0,
-                                                         double* __restrict__ dinv, int* info, int inv_in_place) {
+                                                         double* __restrict__ dinv, int* info, int inv_in_place,
+                                                         int64_t sA = 0, int64_t sD = 0) {
   __shared__ __attribute__((aligned(16))) double S[DS_DOUBLES];
   __shared__ __attribute__((aligned(16))) double colbuf[32];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  A += blockIdx.x * sA;
+  if (dinv) dinv += blockIdx.x * sD;
+  if (info) info += blockIdx.x;
   double* Ab = A + (int64_t)k0 * lda + k0;
   GP2D_STAMP(0);
   // load the stored (block-lower) part: block row rb is 32 rows × 16(rb+1) 16-B vectors, rows
@@ -497,7 +503,9 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
 }
 
 // Zero the strict upper triangle outside the diagonal blocks.
-__global__ __launch_bounds__(256) void zero_upper_kernel(double* __restrict__ A, int64_t n, int64_t lda) {
+__global__ __launch_bounds__(256) void zero_upper_kernel(double* __restrict__ A, int64_t n, int64_t lda,
+                                                         int64_t sA = 0) {   // problem blockIdx.z at A + z·sA
+  A += blockIdx.z * sA;
   const int64_t i = blockIdx.y;
   const int64_t j = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 2;
   const int64_t jstart = (i / NB + 1) * NB;
@@ -506,7 +514,10 @@ __global__ __launch_bounds__(256) void zero_upper_kernel(double* __restrict__ A,
 
 // Copy the inverted diagonal blocks into A's diagonal (TRTRI level 0).
 __global__ __launch_bounds__(256) void put_diag_blocks_kernel(double* __restrict__ A, int64_t lda,
-                                                              const double* __restrict__ dinv) {
+                                                              const double* __restrict__ dinv, int64_t sA = 0,
+                                                              int64_t sD = 0) {   // problem blockIdx.z
+  A += blockIdx.z * sA;
+  dinv += blockIdx.z * sD;
   const int b = blockIdx.y;
   const int idx = blockIdx.x * 256 + threadIdx.x;  // < NB*NB
   const int i = idx >> 7, j = idx & (NB - 1);

@@ -62,6 +62,12 @@ struct GemmParams {
   // half-length ones; the caller adds C2 into C (add_into_kernel)
   int ksplit, zcnt;
   double* C2; int64_t ldc2; int64_t sC2;
+  // Problem batch (batched factorisations, factor.hpp): launch_gemm(p, count, s, nprob) runs the
+  // same product on nprob independent problems, problem q at A + q·pA, B + q·pB, C + q·pC,
+  // C2 + q·pC2; grid.z = nprob × (entries per problem), zper = entries per problem (set by
+  // launch_gemm; 0 = one problem).  Every problem's tiles sum in the same order as a lone launch.
+  int zper;
+  int64_t pA, pB, pC, pC2;
 };
 
 __host__ __device__ inline int cyc_tile(const GemmParams& p, int bj) {
@@ -102,14 +108,18 @@ __global__ __launch_bounds__(256, 2) void gemm_f64_kernel(GemmParams p) {
     bj = blockIdx.x;
     bi = p.rev_rows ? (int)(gridDim.y - 1 - blockIdx.y) : (int)blockIdx.y;
   }
-  int z = blockIdx.z;
+  int z = blockIdx.z, zq = 0;
+  if (p.zper > 0) {   // problem zq of a problem batch
+    zq = z / p.zper;
+    z -= zq * p.zper;
+  }
   const bool khigh = p.ksplit > 0 && z >= p.zcnt;   // the k ≥ ksplit half of a split product
   if (khigh) z -= p.zcnt;
   const int jt = cyc_tile(p, bj);
   if (p.cyc_lower && bi + p.mask_off < jt) return;   // strictly above the global diagonal
   const int i0 = bi * GBM, j0 = jt * GBN;
-  const double* __restrict__ A = p.A + z * p.sA;
-  const double* __restrict__ B = p.B + z * p.sB;
+  const double* __restrict__ A = p.A + z * p.sA + zq * p.pA;
+  const double* __restrict__ B = p.B + z * p.sB + zq * p.pB;
 
   int kb = max(p.b_lower ? j0 : 0, p.a_upper ? i0 : 0);
   int ke = p.a_lower ? min(p.K, i0 + GBM) : p.K;
@@ -195,7 +205,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f64_kernel(GemmParams p) {
   }
 
   if (EPI == EPI_STORE) {
-    double* __restrict__ C = khigh ? p.C2 + z * p.sC2 : p.C + z * p.sC;
+    double* __restrict__ C = khigh ? p.C2 + z * p.sC2 + zq * p.pC2 : p.C + z * p.sC + zq * p.pC;
     const int64_t ldc = khigh ? p.ldc2 : p.ldc;
     const bool diag_tile = (p.c_lower && bi == bj) || (p.cyc_lower && bi + p.mask_off == jt);
     const bool has_beta = p.beta != 0.0;
@@ -268,7 +278,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f64_kernel(GemmParams p) {
     }
     __syncthreads();
     if (tid < 128) {
-      double* __restrict__ P = p.P + z * p.sP + (int64_t)bi * p.ldp + j0;
+      double* __restrict__ P = p.P + z * p.sP + (int64_t)bi * p.ldp + j0;   // (no problem batch with COLSQ)
       P[tid] = red[tid] + red[128 + tid];
     }
   }
@@ -276,8 +286,13 @@ __global__ __launch_bounds__(256, 2) void gemm_f64_kernel(GemmParams p) {
 
 // Host-side launcher.  Returns 0 / negative error.
 template <bool BT, int EPI>
-inline int launch_gemm(const GemmParams& p, int batch, hipStream_t s) {
-  if (p.M <= 0 || p.N <= 0 || batch <= 0) return 0;
+inline int launch_gemm(const GemmParams& pin, int batch, hipStream_t s, int nprob = 1) {
+  if (pin.M <= 0 || pin.N <= 0 || batch <= 0 || nprob <= 0) return 0;
+  GemmParams p = pin;
+  if (nprob > 1 && EPI != EPI_STORE) {
+    set_error("gemm: a problem batch needs EPI_STORE");
+    return -2;
+  }
   if ((p.M % GBM) || (p.N % GBN) || (p.K % GBK)) {
     set_error("gemm: sizes must be multiples of 128/128/16");
     return -2;
@@ -304,19 +319,26 @@ inline int launch_gemm(const GemmParams& p, int batch, hipStream_t s) {
     }
     grid.z = 2 * batch;
   }
+  p.zper = nprob > 1 ? (int)grid.z : 0;
+  grid.z *= (unsigned)nprob;
+  if (grid.z > 65535u) {
+    set_error("gemm: too many batch entries");
+    return -2;
+  }
   gemm_f64_kernel<BT, EPI><<<grid, 256, 0, s>>>(p);
   return check_launch("gemm_f64_kernel");
 }
 
 // C[z] += D[z] over an M×N block per batch entry (row strides ldc / ldd, batch strides sC / sD):
 // the two halves of a K-split product (GemmParams::ksplit), summed in a fixed order.
+// Problem batch: grid.z = nprob × count, problem q at C + q·pC, D + q·pD.
 __global__ __launch_bounds__(256) void add_into_kernel(double* __restrict__ C, int64_t ldc, int64_t sC,
                                                        const double* __restrict__ D, int64_t ldd, int64_t sD,
-                                                       int M, int N) {
-  const int z = blockIdx.z;
+                                                       int M, int N, int count, int64_t pC, int64_t pD) {
+  const int zq = (int)blockIdx.z / count, z = (int)blockIdx.z - zq * count;
   const int row = blockIdx.y;
-  double* c = C + z * sC + (int64_t)row * ldc;
-  const double* d = D + z * sD + (int64_t)row * ldd;
+  double* c = C + z * sC + zq * pC + (int64_t)row * ldc;
+  const double* d = D + z * sD + zq * pD + (int64_t)row * ldd;
   for (int j = (blockIdx.x * 256 + threadIdx.x) * 2; j < N; j += gridDim.x * 512) {
     const d2 a = *reinterpret_cast<const d2*>(c + j), b = *reinterpret_cast<const d2*>(d + j);
     *reinterpret_cast<d2*>(c + j) = d2{a.x + b.x, a.y + b.y};
@@ -347,12 +369,16 @@ inline GemmParams gemm_params() {
 constexpr int PNL_R = 32;
 __device__ __forceinline__ int pnl_idx(int r, int k) { return r * 64 + (k ^ ((r & 15) << 1)); }
 
+// Problem batch: problem blockIdx.y at A + y·pA, B + y·pB, C + y·pC (0 for a lone launch).
 __global__ __launch_bounds__(256) void gemm_f64_panel_kernel(const double* A, int64_t lda, const double* __restrict__ B,
                                                              int64_t ldb, double* C, int64_t ldc, double alpha,
-                                                             double beta) {
+                                                             double beta, int64_t pA, int64_t pB, int64_t pC) {
   __shared__ __attribute__((aligned(16))) double As[PNL_R * 64];   // 16 KB
   __shared__ __attribute__((aligned(16))) double Bs[128 * 64];     // 64 KB
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  A += blockIdx.y * pA;
+  B += blockIdx.y * pB;
+  C += blockIdx.y * pC;
   const int64_t r0 = (int64_t)blockIdx.x * PNL_R;
   // per K-half: 1024 A pairs + 4096 B pairs = 20 16-B loads per thread
   auto load = [&](int h, d2 (&v)[20]) {

@@ -324,14 +324,16 @@ int factor_streams(FactorCtx& c, int nblk, hipStream_t caller) {
   return 0;
 }
 
-int launch_panel(double* A, int64_t lda, int k, int64_t n, const double* dinv, hipStream_t s) {
+// nprob problems at A + q·sA with their diagonal inverses at dinv + q·sD (problem batch)
+int launch_panel(double* A, int64_t lda, int k, int64_t n, const double* dinv, hipStream_t s, int nprob = 1,
+                 int64_t sA = 0, int64_t sD = 0) {
   const int k0 = k * NB;
   const int rows = (int)(n - k0 - NB);
   if (rows <= 0) return 0;
   // in-place panel TRSM  L21 = A21 · inv(L11)ᵀ
   double* P = A + (int64_t)(k0 + NB) * lda + k0;
-  gemm_f64_panel_kernel<<<(unsigned)(rows / PNL_R), 256, 0, s>>>(P, lda, dinv + (int64_t)k * NB * NB, NB, P, lda,
-                                                                1.0, 0.0);
+  gemm_f64_panel_kernel<<<dim3((unsigned)(rows / PNL_R), (unsigned)nprob), 256, 0, s>>>(
+      P, lda, dinv + (int64_t)k * NB * NB, NB, P, lda, 1.0, 0.0, sA, sD, sA);
   return check_launch("gemm_f64_panel_kernel");
 }
 
@@ -372,13 +374,16 @@ size_t trtri_split_doubles(int nbk) {   // T2: the largest high half of any spli
 }
 
 int add_into(double* C, int64_t ldc, int64_t sC, const double* D, int64_t ldd, int64_t sD, int M, int N, int count,
-             hipStream_t s) {
-  add_into_kernel<<<dim3((unsigned)((N + 511) / 512), (unsigned)M, (unsigned)count), 256, 0, s>>>(C, ldc, sC, D, ldd,
-                                                                                                  sD, M, N);
+             hipStream_t s, int nprob = 1, int64_t pC = 0, int64_t pD = 0) {
+  add_into_kernel<<<dim3((unsigned)((N + 511) / 512), (unsigned)M, (unsigned)(count * nprob)), 256, 0, s>>>(
+      C, ldc, sC, D, ldd, sD, M, N, count, pC, pD);
   return check_launch("add_into_kernel");
 }
 
-int trtri_levels(double* A, int64_t lda, int nbk, double* T, double* T2, hipStream_t s) {
+// Problem batch: nprob problems at A + q·sA, each with its own T (+ q·pT) and T2 (+ q·pT2);
+// every problem's products are the lone launch's (the same tiles, K ranges and split sums).
+int trtri_levels(double* A, int64_t lda, int nbk, double* T, double* T2, hipStream_t s, int nprob = 1,
+                 int64_t sA = 0, int64_t pT = 0, int64_t pT2 = 0) {
   for (int g = 1; g < nbk; g *= 2) {
     for (const TrtriPair& pr : trtri_level_pairs(nbk, g)) {
       const int64_t Lo = (int64_t)pr.Ls * NB, Ro = (int64_t)pr.Rs * NB;
@@ -393,8 +398,10 @@ int trtri_levels(double* A, int64_t lda, int nbk, double* T, double* T2, hipStre
       p.cols_first = 1;   // column block j needs k ≥ j: long-K tiles first
       p.ksplit = trtri_ksplit(g, pr.Rn);
       if (p.ksplit) { p.zcnt = pr.count; p.C2 = T2; p.ldc2 = bw; p.sC2 = (int64_t)rh * bw; }
-      GP2D_CHECK((launch_gemm<false, EPI_STORE>(p, pr.count, s)));
-      if (p.ksplit) GP2D_CHECK(add_into(T, bw, (int64_t)rh * bw, T2, bw, (int64_t)rh * bw, rh, bw, pr.count, s));
+      p.pA = sA; p.pB = sA; p.pC = pT; p.pC2 = pT2;
+      GP2D_CHECK((launch_gemm<false, EPI_STORE>(p, pr.count, s, nprob)));
+      if (p.ksplit)
+        GP2D_CHECK(add_into(T, bw, (int64_t)rh * bw, T2, bw, (int64_t)rh * bw, rh, bw, pr.count, s, nprob, pT, pT2));
       // A[R, L] = −WD · T     WD = A[R, R] (rh × rh lower)
       GemmParams q = gemm_params();
       q.A = A + Ro * lda + Ro; q.lda = lda; q.sA = stride;
@@ -404,9 +411,11 @@ int trtri_levels(double* A, int64_t lda, int nbk, double* T, double* T2, hipStre
       q.rev_rows = 1;     // row block i needs k ≤ i: long-K tiles first
       q.ksplit = trtri_ksplit(pr.Rn, g);
       if (q.ksplit) { q.zcnt = pr.count; q.C2 = T2; q.ldc2 = bw; q.sC2 = (int64_t)rh * bw; }
-      GP2D_CHECK((launch_gemm<false, EPI_STORE>(q, pr.count, s)));
+      q.pA = sA; q.pB = pT; q.pC = sA; q.pC2 = pT2;
+      GP2D_CHECK((launch_gemm<false, EPI_STORE>(q, pr.count, s, nprob)));
       if (q.ksplit)
-        GP2D_CHECK(add_into(A + Ro * lda + Lo, lda, stride, T2, bw, (int64_t)rh * bw, rh, bw, pr.count, s));
+        GP2D_CHECK(add_into(A + Ro * lda + Lo, lda, stride, T2, bw, (int64_t)rh * bw, rh, bw, pr.count, s, nprob, sA,
+                            pT2));
     }
   }
   return 0;
@@ -482,10 +491,18 @@ PotrfSchedule potrf_schedule(int nb) {
 // With Tws != NULL the factor is inverted in place on the way (gp2d_potrf_inv, inv_top_split):
 // the diagonal kernels store W_kk, the left half of the inverse and the top-level product
 // T = L21·W11 run on `inv` under the second half of the factorisation, W22 and W21 after it.
-static int potrf_impl(double* A, int64_t n, int64_t lda, double* dinv, int* info_dev, hipStream_t s, double* Tws) {
+// Problem batch (nprob > 1, gp2d_potrf_batched): nprob SPD matrices at A + q·sA, their
+// diagonal inverses at dinv + q·n·128, info_dev[q]; every launch below carries all problems
+// (workgroups per problem: the diagonal kernel's one, the panel GEMMs' grid.y, the SYRK's and
+// zeroing's grid.z), so the chain's latency is paid once for the batch and each problem's
+// arithmetic is that of a lone factorisation, bit for bit.
+static int potrf_impl(double* A, int64_t n, int64_t lda, double* dinv, int* info_dev, hipStream_t s, double* Tws,
+                      int nprob = 1, int64_t sA = 0) {
   GP2D_REQUIRE(n % NB == 0 && n > 0, "potrf: n must be a positive multiple of 128");
   GP2D_REQUIRE(lda >= n && lda % 2 == 0, "potrf: lda must be >= n and even");
   GP2D_REQUIRE(dinv != nullptr, "potrf: dinv buffer is required");
+  GP2D_REQUIRE(nprob >= 1 && (nprob == 1 || (Tws == nullptr && sA >= n * lda)), "potrf: bad problem batch");
+  const int64_t sD = n * NB;   // one problem's diagonal inverses
   const int nb = (int)(n / NB);
   const bool fused = Tws != nullptr;
   FactorCtx fc;
@@ -510,16 +527,16 @@ static int potrf_impl(double* A, int64_t n, int64_t lda, double* dinv, int* info
   auto colupdate = [&](int j, int p, hipStream_t st) -> int {
     const int64_t j0 = (int64_t)j * NB;
     const double* Lp = A + j0 * lda + (int64_t)p * NB;
-    gemm_f64_panel_kernel<<<(unsigned)((n - j0) / PNL_R), 256, 0, st>>>(Lp, lda, Lp, lda, A + j0 * lda + j0, lda,
-                                                                         -1.0, 1.0);
+    gemm_f64_panel_kernel<<<dim3((unsigned)((n - j0) / PNL_R), (unsigned)nprob), 256, 0, st>>>(
+        Lp, lda, Lp, lda, A + j0 * lda + j0, lda, -1.0, 1.0, sA, sA, sA);
     return check_launch("gemm_f64_panel_kernel");
   };
   // diagonal block j (Cholesky + inverse) and its panel TRSM; then (fused) the inverse's
   // GEMMs whose inputs block column j completes
   auto factor = [&](int j) -> int {
-    potrf_diag_kernel<<<1, 256, 0, sc>>>(A, lda, j * NB, dinv, info_dev, fused ? 1 : 0);
+    potrf_diag_kernel<<<nprob, 256, 0, sc>>>(A, lda, j * NB, dinv, info_dev, fused ? 1 : 0, sA, sD);
     GP2D_CHECK(check_launch("potrf_diag_kernel"));
-    GP2D_CHECK(launch_panel(A, lda, j, n, dinv, sc));
+    GP2D_CHECK(launch_panel(A, lda, j, n, dinv, sc, nprob, sA, sD));
     if (fused && nb > 1 && j == h - 1) {   // left half final: W11 and T = L21·W11 under the rest
       GP2D_EV(hipEventRecord((*fc.blk)[0], sc));
       GP2D_EV(hipStreamWaitEvent(si, (*fc.blk)[0], 0));
@@ -573,13 +590,14 @@ static int potrf_impl(double* A, int64_t n, int64_t lda, double* dinv, int* info
           GemmParams q = gemm_params();
           q.lda = lda; q.ldb = lda; q.ldc = lda;
           q.K = g * NB; q.alpha = -1.0; q.beta = 1.0;
+          q.pA = q.pB = q.pC = sA;
           if (hw > 0) {   // head: block columns [P+g+1, P+g+1+hw), every row below, lower tiles
             q.A = A + f0 * lda + (int64_t)P * NB;
             q.B = q.A;
             q.C = A + f0 * lda + f0;
             q.M = (int)(n - f0); q.N = hw * NB;
             q.cyc_lower = 1; q.mask_off = 0;
-            GP2D_CHECK((launch_gemm<true, EPI_STORE>(q, 1, sb)));
+            GP2D_CHECK((launch_gemm<true, EPI_STORE>(q, 1, sb, nprob)));
             GP2D_EV(hipEventRecord(e_head, sb));
             q.cyc_lower = 0;
           }
@@ -589,7 +607,7 @@ static int potrf_impl(double* A, int64_t n, int64_t lda, double* dinv, int* info
             q.B = q.A;
             q.C = A + f1 * lda + f1;
             q.M = (int)(n - f1); q.N = q.M; q.c_lower = 1;
-            GP2D_CHECK((launch_gemm<true, EPI_STORE>(q, 1, sb)));
+            GP2D_CHECK((launch_gemm<true, EPI_STORE>(q, 1, sb, nprob)));
           }
           if (hw == 0) GP2D_EV(hipEventRecord(e_head, sb));
         } else {
@@ -626,8 +644,8 @@ static int potrf_impl(double* A, int64_t n, int64_t lda, double* dinv, int* info
   // gp2d_factor_join(1) the host waits for the chain first, so the wait is enqueued complete.
   if (t_factor_join) GP2D_EV(hipEventSynchronize(e_join));
   GP2D_EV(hipStreamWaitEvent(s, e_join, 0));
-  dim3 zg((unsigned)((n / 2 + 255) / 256), (unsigned)n);
-  zero_upper_kernel<<<zg, 256, 0, s>>>(A, n, lda);
+  dim3 zg((unsigned)((n / 2 + 255) / 256), (unsigned)n, (unsigned)nprob);
+  zero_upper_kernel<<<zg, 256, 0, s>>>(A, n, lda, sA);
   return check_launch("zero_upper_kernel");
 }
 
@@ -712,6 +730,42 @@ int gp2d_trtri(double* A, int64_t n, int64_t lda, const double* dinv, void* work
   return trtri_levels(A, lda, nb, T, dwork + (size_t)nb * NB * NB, s);
 }
 
+// ------------------------------------------------------------------------ batched factor
+// nprob independent fits of one size in one chain (a hyperparameter sweep's settings, a job
+// stream's next jobs): problem q's matrix at A + q·sA, its diagonal inverses at dinv + q·n·128,
+// its info word at info_dev[q].  Each problem's results are those of gp2d_potrf / gp2d_trtri
+// alone, bit for bit (tests/test_gpu_batched.py).
+int gp2d_potrf_batched(double* A, int64_t n, int64_t lda, int64_t sA, int nprob, double* dinv, int* info_dev,
+                       void* stream) {
+  GP2D_REQUIRE(nprob >= 1 && nprob <= 64, "potrf_batched: nprob must be 1..64");
+  GP2D_REQUIRE(nprob == 1 || sA >= n * lda, "potrf_batched: problem stride below n·lda");
+  return potrf_impl(A, n, lda, dinv, info_dev, S(stream), nullptr, nprob, nprob > 1 ? sA : 0);
+}
+
+size_t gp2d_trtri_batched_workspace(int64_t n, int nprob) {
+  if (nprob < 1) return 0;
+  const int64_t nb = n / NB;
+  return (size_t)nprob * ((size_t)(n / 2 + NB) * (size_t)(n / 2 + NB) + trtri_split_doubles((int)nb)) * sizeof(double);
+}
+
+int gp2d_trtri_batched(double* A, int64_t n, int64_t lda, int64_t sA, int nprob, const double* dinv, void* work,
+                       size_t work_bytes, void* stream) {
+  GP2D_REQUIRE(n % NB == 0 && n > 0, "trtri_batched: n must be a positive multiple of 128");
+  GP2D_REQUIRE(nprob >= 1 && nprob <= 64, "trtri_batched: nprob must be 1..64");
+  GP2D_REQUIRE(nprob == 1 || sA >= n * lda, "trtri_batched: problem stride below n·lda");
+  GP2D_REQUIRE(dinv != nullptr, "trtri_batched: dinv (from gp2d_potrf_batched) is required");
+  GP2D_REQUIRE(work != nullptr && work_bytes >= gp2d_trtri_batched_workspace(n, nprob),
+               "trtri_batched: workspace too small");
+  hipStream_t s = S(stream);
+  const int nb = (int)(n / NB);
+  const int64_t pT = (int64_t)(n / 2 + NB) * (n / 2 + NB), pT2 = (int64_t)trtri_split_doubles(nb);
+  double* T = reinterpret_cast<double*>(work);
+  double* T2 = T + (size_t)nprob * pT;
+  put_diag_blocks_kernel<<<dim3(NB * NB / 256, nb, nprob), 256, 0, s>>>(A, lda, dinv, nprob > 1 ? sA : 0, n * NB);
+  GP2D_CHECK(check_launch("put_diag_blocks_kernel"));
+  return trtri_levels(A, lda, nb, T, T2, s, nprob, nprob > 1 ? sA : 0, pT, pT2);
+}
+
 // ------------------------------------------------------------------------ distributed factor
 // One job's POTRF + TRTRI over P ranks (dfact.hpp): 512-column super-blocks dealt block-
 // cyclically, a panel broadcast per step by the caller.  Every GEMM below is gemm_f64_kernel;
@@ -766,13 +820,13 @@ int gp2d_dfact_panel(double* A, int64_t n, int64_t lda, int s, double* panel, in
     if (below <= 0) continue;
     double* Pj = As + (c0 + NB) * lda + c0;        // sub-column j below its diagonal block
     gemm_f64_panel_kernel<<<(unsigned)(below / PNL_R), 256, 0, st>>>(Pj, lda, dinv + j * NB * NB, NB, Pj, lda,
-                                                                    1.0, 0.0);
+                                                                    1.0, 0.0, 0, 0, 0);
     GP2D_CHECK(check_launch("gemm_f64_panel_kernel"));
     for (int j2 = j + 1; j2 < DF_SBT; ++j2) {      // sub-column j2 (rows ≥ its diagonal) −= L_j · L_j[j2 rows]ᵀ
       const int64_t r2 = (int64_t)j2 * NB;
       const double* Lp = As + r2 * lda + c0;
       gemm_f64_panel_kernel<<<(unsigned)((rows - r2) / PNL_R), 256, 0, st>>>(Lp, lda, Lp, lda, As + r2 * lda + r2,
-                                                                            lda, -1.0, 1.0);
+                                                                            lda, -1.0, 1.0, 0, 0, 0);
       GP2D_CHECK(check_launch("gemm_f64_panel_kernel"));
     }
   }

@@ -12,7 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GP2D_LIB", os.path.join(_HERE, "libgp2d.so"))
-ABI_VERSION = 7          # GP2D_ABI_VERSION in include/gp2d.h
+ABI_VERSION = 8          # GP2D_ABI_VERSION in include/gp2d.h
 
 FAMILY_VECTOR2D, FAMILY_ARD_RBF, FAMILY_VECTOR_ST = 0, 1, 2
 KIND_SCALAR, KIND_DIVFREE, KIND_CURLFREE, KIND_MIXED = 0, 1, 2, 3
@@ -22,7 +22,8 @@ VAR_LATENT, VAR_NOISY, VAR_CLIPPED = 0, 1, 2
 EXPORTS = (
     "gp2d_abi_version", "gp2d_padded_points", "gp2d_block_dim", "gp2d_kernel_diag",
     "gp2d_assemble", "gp2d_factor_sets", "gp2d_factor_set_of", "gp2d_factor_join", "gp2d_potrf_workspace", "gp2d_potrf", "gp2d_trtri_workspace", "gp2d_trtri",
-    "gp2d_potrf_inv_workspace", "gp2d_potrf_inv",
+    "gp2d_potrf_inv_workspace", "gp2d_potrf_inv", "gp2d_potrf_batched", "gp2d_trtri_batched_workspace",
+    "gp2d_trtri_batched",
     "gp2d_potrs_workspace", "gp2d_potrs_inv", "gp2d_predict_workspace", "gp2d_predict",
     "gp2d_ozaki_nmod", "gp2d_ozaki_wres_bytes", "gp2d_ozaki_prepare", "gp2d_ozaki_prepare_async",
     "gp2d_predict_ozaki_workspace",
@@ -85,6 +86,9 @@ _SIGS = {
     "gp2d_trtri": (_I, [_P, _I64, _I64, _P, _P, _SZ, _P]),
     "gp2d_potrf_inv_workspace": (_SZ, [_I64]),
     "gp2d_potrf_inv": (_I, [_P, _I64, _I64, _P, _P, _P, _SZ, _P]),
+    "gp2d_potrf_batched": (_I, [_P, _I64, _I64, _I64, _I, _P, _P, _P]),
+    "gp2d_trtri_batched_workspace": (_SZ, [_I64, _I]),
+    "gp2d_trtri_batched": (_I, [_P, _I64, _I64, _I64, _I, _P, _P, _SZ, _P]),
     "gp2d_potrs_workspace": (_SZ, [_I64]),
     "gp2d_potrs_inv": (_I, [_P, _I64, _I64, _P, _P, _P, _SZ, _P]),
     "gp2d_predict_workspace": (_SZ, [_I64, _I64, _I]),

@@ -391,6 +391,98 @@ def fit(kernel: KernelSpec, x, y, noise: float, jitter: float = 0.0, device=None
     return gp
 
 
+def fit_batch(problems, variance: str = "f64", jitter: float = 0.0, device=None, check: bool = True,
+              join: bool | None = None) -> list:
+    """Fit several GPs of one size together: `problems` is a sequence of (kernel, x, y, noise)
+    whose matrices K_y share the order n (a hyperparameter sweep's settings over one training
+    set, or a job stream's next jobs with equal point counts).  Their K_y are factored and
+    inverted in ONE chain (gp2d_potrf_batched + gp2d_trtri_batched: every launch carries every
+    problem), so the latency-bound diagonal chain of a fit is paid once per
+    batch instead of once per fit; each problem's W, α (and INT8 residue planes) are those of
+    engine.fit on it alone, bit for bit.  Returns one GPFit per problem (W views into one
+    (B, n, n) tensor).  check=True raises LinAlgError for the first non-PD problem (the index
+    is in the message); check=False defers it to each GPFit.check().  join as in fit()."""
+    if variance not in VARIANCE_ENGINES:
+        raise ValueError(f"variance must be one of {VARIANCE_ENGINES}")
+    probs = list(problems)
+    if not probs:
+        return []
+    if len(probs) > 64:
+        raise ValueError("fit_batch: at most 64 problems per batch")
+    dev = _require_device(device)
+    L = N.lib()
+    s = _stream_handle(dev)
+    prep = []
+    for kernel, x, y, noise in probs:
+        if variance == "ozaki" and not kernel.is_vector:
+            raise ValueError("the ozaki variance engine supports the vector families only")
+        X = _as_points(x, kernel.input_dim, dev)
+        ntr = X.shape[0]
+        if ntr < 1:
+            raise ValueError("need at least one training point")
+        npad, n = fit_layout(kernel, ntr, variance)
+        perm = None
+        if variance == "ozaki" and ntr > 1:
+            perm = morton_order(X)
+            X = X[perm].contiguous()
+        prep.append((kernel, X, y, float(noise), ntr, npad, n, perm))
+    n = prep[0][6]
+    if any(p[6] != n for p in prep):
+        raise ValueError("fit_batch: every problem must have the same matrix order n")
+    if variance == "ozaki" and n >= 131072:
+        raise ValueError("the ozaki variance engine supports n < 131072")
+    B = len(prep)
+    A = torch.empty((B, n, n), dtype=torch.float64, device=dev)
+    for b, (kernel, X, _, noise, ntr, npad, _, _) in enumerate(prep):
+        N.check(L.gp2d_assemble(_ptr(X), ntr, npad, _ptr(X), ntr, npad, ctypes.byref(kernel.desc()),
+                                float(noise + jitter), 1, _ptr(A[b]), n, s), "gp2d_assemble")
+    dinv = torch.empty((B, n // NB, NB, NB), dtype=torch.float64, device=dev)
+    info = torch.zeros(B, dtype=torch.int32, device=dev)
+    prev_join = L.gp2d_factor_join(1 if (check if join is None else join) else 0)
+    try:
+        N.check(L.gp2d_potrf_batched(_ptr(A), n, n, n * n, B, _ptr(dinv), _ptr(info), s), "gp2d_potrf_batched")
+    finally:
+        L.gp2d_factor_join(prev_join)
+    wbytes = int(L.gp2d_trtri_batched_workspace(n, B))
+    work = torch.empty(wbytes // 8 + 1, dtype=torch.float64, device=dev)
+    N.check(L.gp2d_trtri_batched(_ptr(A), n, n, n * n, B, _ptr(dinv), _ptr(work), wbytes, s), "gp2d_trtri_batched")
+    del work, dinv
+    pbytes = int(L.gp2d_potrs_workspace(n))
+    pwork = torch.empty(pbytes // 8 + 1, dtype=torch.float64, device=dev)
+    fits, errs = [], []
+    for b, (kernel, X, y, noise, ntr, npad, _, perm) in enumerate(prep):
+        bd = kernel.block_dim
+        Y = _pad_obs(y, ntr, npad, bd, dev)
+        if perm is not None:
+            for c in range(bd):
+                Y[c * npad:c * npad + ntr] = Y[c * npad:c * npad + ntr][perm]
+        alpha = torch.empty(n, dtype=torch.float64, device=dev)
+        W = A[b]
+        N.check(L.gp2d_potrs_inv(_ptr(W), n, n, _ptr(Y), _ptr(alpha), _ptr(pwork), pbytes, s), "gp2d_potrs_inv")
+        gp = GPFit(kernel=kernel, noise=noise, x=X, n_train=ntr, n_pad=npad, W=W, alpha=alpha, device=dev, y=Y,
+                   perm=perm)
+        gp.extra["info_dev"] = info[b:b + 1]
+        err = None
+        if variance == "ozaki":
+            try:
+                ozaki_prepare(gp, diag_add=float(noise + jitter))
+            except N.GP2DError as e:
+                err = e
+        if not check:
+            gp.pending = pending_status(info[b:b + 1], err)
+        fits.append(gp)
+        errs.append(err)
+    del pwork
+    if check:
+        infos = info.cpu().tolist()
+        for b, (inf, err) in enumerate(zip(infos, errs)):
+            try:
+                _raise_fit_errors(int(inf), err)
+            except np.linalg.LinAlgError as e:
+                raise np.linalg.LinAlgError(f"problem {b}: {e}") from None
+    return fits
+
+
 def ozaki_prepare(gp: GPFit, diag_add: float | None = None) -> GPFit:
     """Residue planes of W for the INT8 variance engine (once per fit).  With `diag_add`
     (the noise + jitter of K_y's diagonal) the moduli count is the a-priori bound and nothing

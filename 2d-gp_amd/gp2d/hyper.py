@@ -196,7 +196,7 @@ def optimize_restarts(kernel: E.KernelSpec, x, y, noise: float, num_restarts: in
 
 
 def sweep(kernel: E.KernelSpec, x, y, settings, noise: float = None, jitter: float = 0.0, device=None,
-          eval_gradient: bool = False, concurrent: int | None = None):
+          eval_gradient: bool = False, concurrent: int | None = None, batch: int | None = None):
     """LML (and gradient) for each hyperparameter setting (a list of get_params-style dicts,
     missing keys taken from kernel/noise) — BASELINE config E.  Under torch.distributed the
     settings are dealt round-robin over ranks and the results all-reduced (bit-identical to
@@ -208,7 +208,11 @@ def sweep(kernel: E.KernelSpec, x, y, settings, noise: float = None, jitter: flo
     and gradient run under setting i+1's factorisation (config E: 60.8–61.2 vs 58.3–59.2
     settings/s at c = 1; without the join, 41.9).  Same kernels, same bits as c = 1.
     concurrent = None (default): auto_concurrent() — 2 when there is a gradient to overlap and
-    this rank holds at least two settings, else 1."""
+    this rank holds at least two settings, else 1.
+    batch = b > 1: the settings are fitted b at a time in one batched factorisation
+    (engine.fit_batch: the fit's latency-bound diagonal chain paid once per b settings), then
+    each setting's LML (+ gradient) runs on the filled chip; same bits as b = 1.  batch = None
+    (default): auto_batch() — used instead of `concurrent` when it applies."""
     ws, rank = (dist.get_world_size(), dist.get_rank()) if dist.is_available() and dist.is_initialized() else (1, 0)
     base = get_params(kernel, noise if noise is not None else 0.0)
     S = len(settings)
@@ -216,8 +220,11 @@ def sweep(kernel: E.KernelSpec, x, y, settings, noise: float = None, jitter: flo
     vals = np.zeros(S)
     grads = np.zeros((S, P))
     mine = list(range(rank, S, ws))
+    bsz = auto_batch(kernel, x, len(mine), concurrent) if batch is None else max(1, int(batch))
     c = auto_concurrent(len(mine), eval_gradient) if concurrent is None else max(1, int(concurrent))
-    if c == 1:
+    if bsz > 1:
+        _sweep_batched(kernel, x, y, settings, base, mine, jitter, device, eval_gradient, bsz, vals, grads)
+    elif c == 1:
         for i in mine:
             p = dict(base)
             p.update(settings[i])
@@ -261,6 +268,46 @@ def sweep(kernel: E.KernelSpec, x, y, settings, noise: float = None, jitter: flo
     if ws > 1:
         vals, grads = allreduce_disjoint(vals, grads, device)
     return vals, (grads if eval_gradient else None)
+
+
+BATCH_MAX = 8
+BATCH_MAX_BYTES = 32 << 30   # factor + TRTRI workspace of one batch
+
+
+def auto_batch(kernel: E.KernelSpec, x, n_settings: int, concurrent=None) -> int:
+    """hyper.sweep's default batch: up to BATCH_MAX settings per batched factorisation when the
+    caller did not ask for concurrent streams, there are at least two settings and the batch's
+    matrices (n² doubles each, plus the TRTRI's quarter-size workspace) fit BATCH_MAX_BYTES."""
+    if concurrent is not None or n_settings < 2:
+        return 1
+    npad, n = E.fit_layout(kernel, E._point_count(x, kernel.input_dim))
+    per = 8 * (n * n + (n // 2 + 128) ** 2)
+    return max(1, min(BATCH_MAX, n_settings, BATCH_MAX_BYTES // max(per, 1)))
+
+
+def _sweep_batched(kernel, x, y, settings, base, mine, jitter, device, eval_gradient, bsz, vals, grads):
+    dev = E._require_device(device)
+    for g0 in range(0, len(mine), bsz):
+        group = mine[g0:g0 + bsz]
+        problems = []
+        for i in group:
+            p = dict(base)
+            p.update(settings[i])
+            k, nz = set_params(kernel, p)
+            problems.append((k, x, y, nz))
+        # joined on the host (the chain runs with no wait pending on this stream, cf. fit(join))
+        fits = E.fit_batch(problems, jitter=jitter, device=dev, check=False, join=True)
+        outs = [E.lml_device(gp, eval_gradient) for gp in fits]
+        for i, gp, (out, g) in zip(group, fits, outs):
+            try:
+                gp.check()
+            except np.linalg.LinAlgError:
+                vals[i] = -np.inf
+                continue
+            vals[i] = float(out.item())
+            if g is not None:
+                grads[i] = g.cpu().numpy()
+        del fits, outs
 
 
 def auto_concurrent(n_settings: int, eval_gradient: bool) -> int:

@@ -100,6 +100,9 @@ def parse():
     ap.add_argument("--sweep-concurrent", type=int, default=None,
                     help="config E: streams the settings' fit + LML are queued on (hyper.sweep concurrent; "
                          "default: the library's hyper.auto_concurrent)")
+    ap.add_argument("--sweep-batch", type=int, default=None,
+                    help="config E: settings per batched factorisation (hyper.sweep batch; default: the "
+                         "library's hyper.auto_batch)")
     ap.add_argument("--single-job-dist", type=int, default=0,
                     help="also time one job with distributed.fit_distributed at N = 1 (always at N > 1)")
     a = ap.parse_args()
@@ -240,8 +243,11 @@ def run_sweep(args, ws, rank, dev):
     # None: the library's default (hyper.auto_concurrent)
     conc = args.sweep_concurrent
 
+    bsz = args.sweep_batch
+
     def sweep():
-        return H.sweep(ks, xt, yt, settings, noise=0.0025, eval_gradient=True, device=dev, concurrent=conc)
+        return H.sweep(ks, xt, yt, settings, noise=0.0025, eval_gradient=True, device=dev, concurrent=conc,
+                       batch=bsz)
 
     for _ in range(args.warmup):
         sweep()
@@ -268,6 +274,8 @@ def run_sweep(args, ws, rank, dev):
             "config": {"workload": f"BASELINE config E: 64 (l_df, noise) settings x N_train={args.ntrain}, "
                                    f"div-free, LML + exact gradient per setting, settings dealt over {ws} GPU(s)",
                        "n_train": args.ntrain, "settings": len(settings), "parallelism": f"settings round robin x{ws}",
+                       "sweep_batch": bsz if bsz is not None else
+                       H.auto_batch(ks, xt, len(range(rank, len(settings), ws)), conc),
                        "sweep_concurrent": conc if conc is not None else
                        H.auto_concurrent(len(range(rank, len(settings), ws)), True)},
             "roofline": {"bound": "mfma", "achieved": per_gpu, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define GP2D_ABI_VERSION 7
+#define GP2D_ABI_VERSION 8
 
 /* kernel families */
 #define GP2D_FAMILY_VECTOR2D 0   /* 2×2 matrix-valued SE kernels on (x1, x2)          */
@@ -128,6 +128,18 @@ int gp2d_trtri(double* A, int64_t n, int64_t lda, const double* dinv,
 size_t gp2d_potrf_inv_workspace(int64_t n);
 int gp2d_potrf_inv(double* A, int64_t n, int64_t lda, double* dinv, int* info_dev,
                    void* work, size_t work_bytes, void* stream);
+
+/* gp2d_potrf_batched / gp2d_trtri_batched: nprob independent fits of one size in one
+ * chain — problem q's SPD matrix at A + q·sA (sA ≥ n·lda elements), its diagonal-block
+ * inverses at dinv + q·n·128, its info word at info_dev[q].  Each launch carries every
+ * problem, so a sweep's settings (runKrig.py:14-17's hyperparameter table) or a job
+ * stream's next fits pay the latency-bound diagonal chain once.  Problem q's results are
+ * bit for bit those of gp2d_potrf / gp2d_trtri on it alone.  nprob ≤ 64.             */
+int gp2d_potrf_batched(double* A, int64_t n, int64_t lda, int64_t sA, int nprob, double* dinv,
+                       int* info_dev, void* stream);
+size_t gp2d_trtri_batched_workspace(int64_t n, int nprob);
+int gp2d_trtri_batched(double* A, int64_t n, int64_t lda, int64_t sA, int nprob, const double* dinv,
+                       void* work, size_t work_bytes, void* stream);
 
 /* gp2d_potrs_inv: alpha = Wᵀ (W y) = K_y⁻¹ y given W = L⁻¹.  Replaces
  * np.dot(Ki, y) (GP_scripts.py:45) / cho_solve (_gpr.py:360).                    */

@@ -143,14 +143,14 @@ int main() {
   timeit("potrf_diag_reg (chol+inv)", [&] { hipMemcpyAsync(A, A0, n * n * 8, hipMemcpyDeviceToDevice); potrf_diag_reg_kernel<<<1, 256>>>(A, n, 0, D, info); });
   std::vector<double> Lr(n * n), Dr(n * n), Lb(n * n), Db(n * n);
   hipMemcpy(Lr.data(), A, n * n * 8, hipMemcpyDeviceToHost); hipMemcpy(Dr.data(), D, n * n * 8, hipMemcpyDeviceToHost);
-  timeit("potrf_diag blocked (chol+inv)", [&] { hipMemcpyAsync(A, A0, n * n * 8, hipMemcpyDeviceToDevice); potrf_diag_kernel<<<1, 256>>>(A, n, 0, D, info, 0); });
+  timeit("potrf_diag blocked (chol+inv)", [&] { hipMemcpyAsync(A, A0, n * n * 8, hipMemcpyDeviceToDevice); potrf_diag_kernel<<<1, 256>>>(A, n, 0, D, info, 0, 0, 0); });
   hipMemcpy(Lb.data(), A, n * n * 8, hipMemcpyDeviceToHost); hipMemcpy(Db.data(), D, n * n * 8, hipMemcpyDeviceToHost);
   double eL = 0, eD = 0, mL = 0, mD = 0;
   for (int i = 0; i < n * n; ++i) { eL = std::max(eL, std::abs(Lr[i] - Lb[i])); eD = std::max(eD, std::abs(Dr[i] - Db[i])); mL = std::max(mL, std::abs(Lr[i])); mD = std::max(mD, std::abs(Dr[i])); }
   printf("blocked vs reg: L max rel diff %.2e, inv max rel diff %.2e\n", eL / mL, eD / mD);
   timeit("memcpy only", [&] { hipMemcpyAsync(A, A0, n * n * 8, hipMemcpyDeviceToDevice); });
   timeit("trti2_diag (inv only)", [&] { trti2_diag_kernel<<<1, 256>>>(A, n, D); });
-  potrf_diag_kernel<<<1, 256>>>(A, n, 0, D, info, 0); (void)hipDeviceSynchronize();
+  potrf_diag_kernel<<<1, 256>>>(A, n, 0, D, info, 0, 0, 0); (void)hipDeviceSynchronize();
   unsigned long long st[16]; (void)hipMemcpyFromSymbol(st, HIP_SYMBOL(g_stamps), sizeof(st));
   const char* ph[12] = {"load", "P0", "U0", "P1", "U1", "P2", "U2", "P3", "B", "C", "E", "dinv"};
   printf("phases (cycles):");
