@@ -97,6 +97,9 @@ def parse():
     ap.add_argument("--fits-ahead", type=int, default=None,
                     help="N=1 job stream: fits in flight (engine.krige_jobs fits_ahead; default: the library's "
                          "engine.auto_fits_ahead for the job shape — 0 = each job's fit and predict back to back)")
+    ap.add_argument("--batch-fits", type=int, default=None,
+                    help="N=1 back-to-back job stream: fits per batched factorisation (engine.krige_jobs "
+                         "batch_fits; default: the library's engine.auto_fit_batch)")
     ap.add_argument("--sweep-concurrent", type=int, default=None,
                     help="config E: streams the settings' fit + LML are queued on (hyper.sweep concurrent; "
                          "default: the library's hyper.auto_concurrent)")
@@ -472,7 +475,7 @@ def main():
 
         def stream(k):   # the shipped API for a sweep of jobs
             return E.krige_jobs(itertools.repeat(job, k), variance=args.variance, chunk=args.chunk, stats=stats,
-                                fits_ahead=args.fits_ahead)
+                                fits_ahead=args.fits_ahead, batch_fits=args.batch_fits)
         api = "engine.krige_jobs"
     trace = os.environ.get("GP2D_BENCH_TRACE") == "1"   # per-step wall times on stderr (diagnostics)
 
@@ -631,6 +634,10 @@ def main():
         "api": api,
         "fits_ahead": (E.auto_fits_ahead(spec, args.ntrain, m, args.variance) if args.fits_ahead is None
                        else args.fits_ahead) if api == "engine.krige_jobs" else None,
+        "batch_fits": ((E.auto_fit_batch(spec, args.ntrain, args.variance) if args.batch_fits is None
+                        else args.batch_fits) if (args.fits_ahead if args.fits_ahead is not None else
+                                                  E.auto_fits_ahead(spec, args.ntrain, m, args.variance)) <= 0
+                       else 1) if api == "engine.krige_jobs" else None,
         "unpipelined": unpiped,
         "single_job": single_job,
         "timed_fits": timed_fits,

@@ -29,14 +29,17 @@ JOBS = [(1, 700, 60, "df"), (2, 700, 64, "mixed"), (3, 1500, 50, "df"), (4, 300,
         (5, 1500, 72, "mixed"), (6, 1500, 72, "df")]
 
 
-@pytest.mark.parametrize("variance,ahead", [("ozaki", 1), ("f64", 1), ("ozaki", 2), ("ozaki", 3), ("ozaki", 0),
-                                            ("ozaki", None)])
-def test_krige_jobs_bit_identical_to_sequential(variance, ahead):
+@pytest.mark.parametrize("variance,ahead,batch", [("ozaki", 1, None), ("f64", 1, None), ("ozaki", 2, None),
+                                                  ("ozaki", 3, None), ("ozaki", 0, None), ("ozaki", None, None),
+                                                  ("ozaki", 0, 1), ("ozaki", 0, 2), ("f64", 0, 3)])
+def test_krige_jobs_bit_identical_to_sequential(variance, ahead, batch):
     """fits_ahead > 1: consecutive fits in flight together, each drawing its own internal
-    factor stream set; fits_ahead = 0: back to back on one stream — still the bits of one job
-    at a time."""
+    factor stream set; fits_ahead = 0: back to back on one stream, the fits of consecutive jobs
+    of one matrix order batched (batch_fits; None = auto, 8 here; the mixed sizes of JOBS end
+    batches early) — still the bits of one job at a time."""
     jobs = [_job(*j) for j in JOBS]
-    got = [(m.clone(), v.clone()) for m, v in E.krige_jobs(jobs, variance=variance, chunk=2048, fits_ahead=ahead)]
+    got = [(m.clone(), v.clone()) for m, v in E.krige_jobs(jobs, variance=variance, chunk=2048, fits_ahead=ahead,
+                                                             batch_fits=batch)]
     assert len(got) == len(jobs)
     for (spec, x, y, noise, xg), (m, v) in zip(jobs, got):
         gp = E.fit(spec, x, y, noise, variance=variance)

@@ -330,5 +330,11 @@ def test_job_shape_defaults_live_in_the_library():
     assert E.auto_fits_ahead(df, 4096, 256 * 256) == 1
     assert E.auto_fits_ahead(mixed, 16384, 512 * 512) == 1
     assert H.auto_concurrent(8, True) == 2 and H.auto_concurrent(8, False) == 1 and H.auto_concurrent(1, True) == 1
+    # batched factorisations: config B's back-to-back jobs and config E's sweep batch 8 fits
+    # (profiles/r04_fit_batch.jsonl); D-sized matrices (8 GB each) are not batched
+    assert E.auto_fit_batch(df, 1024) == 8 and E.auto_fit_batch(df, 4096) == 8 and E.auto_fit_batch(mixed, 16384) == 1
+    x = np.zeros((4096, 2))
+    assert H.auto_batch(df, x, 8) == 8 and H.auto_batch(df, x, 3) == 3 and H.auto_batch(df, x, 1) == 1
+    assert H.auto_batch(df, x, 8, concurrent=2) == 1
     src = open(os.path.join(ROOT, "bench.py")).read()
     assert "a.fits_ahead = 0" not in src and "sweep_concurrent or 2" not in src
