@@ -708,7 +708,8 @@ def note_fit_issued(stats: dict | None):
 
 def krige_jobs(jobs, variance: str = "ozaki", chunk: int = 8192, var_mode: str = "latent",
                compute_var: bool = True, jitter: float = 0.0, device=None, stats: dict | None = None,
-               fits_ahead: int | None = None, batch_fits: int | None = None):
+               fits_ahead: int | None = None, batch_fits: int | None = None,
+               batch_ahead: bool | None = None):
     """Independent kriging jobs (kernel, x, y, noise, xg), one after another — the reference's
     runKrig.py:1-40 sweep (one GP_laser / krig.kriging fit + grid predict per setting or
     time window) run in one process.  Yields (mean, var) per job, in order, on the current
@@ -734,7 +735,9 @@ def krige_jobs(jobs, variance: str = "ozaki", chunk: int = 8192, var_mode: str =
     batch_fits = b > 1 (with fits_ahead = 0): the next b jobs of one matrix order are fitted
     together (engine.fit_batch: one batched factorisation, the fit's latency-bound chain paid
     once per b jobs), then predicted one by one; same bits.  batch_fits = None (default):
-    auto_fit_batch() for the back-to-back form, 1 otherwise."""
+    auto_fit_batch() for the back-to-back form, 1 otherwise.  batch_ahead=True: batch g+1's fit
+    on a side stream under batch g's predicts; None (default): auto_batch_ahead() on the first
+    job's shape."""
     dev = _require_device(device)
     main = torch.cuda.current_stream(dev)
     it = iter(jobs)
@@ -747,16 +750,21 @@ def krige_jobs(jobs, variance: str = "ozaki", chunk: int = 8192, var_mode: str =
         fits_ahead = auto_fits_ahead(kernel, _point_count(x, kernel.input_dim),
                                      _point_count(xg, kernel.input_dim), variance, compute_var)
     if int(fits_ahead) <= 0:
-        if batch_fits is None:
+        if batch_fits is None or batch_ahead is None:
             first = next(it, None)
             if first is None:
                 return
             it = itertools.chain([first], it)
-            kernel, x = first[0], first[1]
-            batch_fits = auto_fit_batch(kernel, _point_count(x, kernel.input_dim), variance)
+            kernel, x, xg = first[0], first[1], first[4]
+            ntr = _point_count(x, kernel.input_dim)
+            if batch_fits is None:
+                batch_fits = auto_fit_batch(kernel, ntr, variance)
+            if batch_ahead is None:
+                batch_ahead = auto_batch_ahead(kernel, ntr, _point_count(xg, kernel.input_dim), int(batch_fits),
+                                               variance, compute_var)
         if int(batch_fits) > 1:
             yield from _krige_jobs_batched(it, int(batch_fits), variance, chunk, var_mode, compute_var, jitter, dev,
-                                           stats)
+                                           stats, ahead=bool(batch_ahead))
         else:
             yield from _krige_jobs_serial(it, variance, chunk, var_mode, compute_var, jitter, dev, stats)
         return
@@ -823,6 +831,27 @@ def _point_count(x, dim: int) -> int:
 _PRED_MS_REF, _FIT_MS_COEF, _FIT_MS_EXP, _FIT_STRETCH = 48.0, 0.061, 1.3, 2.4
 
 
+def _predict_ms_model(kernel: KernelSpec, n: int, m_grid: int, variance: str, compute_var: bool) -> float:
+    scale = (m_grid / 65536.0) * (n / (2.0 * 4096)) ** 2 * (kernel.block_dim / 2.0)
+    p = (1.0 + _PRED_MS_REF * scale) * (1.0 if variance == "ozaki" else 2.5)
+    return 1.0 + 0.1 * (p - 1.0) if not compute_var else p
+
+
+def auto_batch_ahead(kernel: KernelSpec, n_train: int, m_grid: int, b: int, variance: str = "ozaki",
+                     compute_var: bool = True) -> bool:
+    """krige_jobs' default for batched back-to-back jobs: batch g+1's fit under batch g's
+    predicts when the batch's predicts outlast its stretched fit by the model of auto_fits_ahead,
+    with the batched fit ≈ max(f·(1 + 0.15·(b − 1)), b·(2n³/3) / 46 TF/s) (chain-bound small
+    batches, FLOP-bound large ones; profiles/r04_fit_batch.jsonl).  Config B (b = 8): 8.8e6 vs
+    7.8e6 points/s back to back; with b = 4, 7.1e6 (profiles/r04_batch_ahead_ab.txt)."""
+    if b <= 1:
+        return False
+    _, n = fit_layout(kernel, max(1, int(n_train)), variance)
+    f1 = _FIT_MS_COEF * (n / NB) ** _FIT_MS_EXP
+    fb = max(f1 * (1.0 + 0.15 * (b - 1)), b * (2.0 * n ** 3 / 3.0) / 46e9)
+    return b * _predict_ms_model(kernel, n, m_grid, variance, compute_var) > (_FIT_STRETCH - 1.0) * fb
+
+
 def auto_fits_ahead(kernel: KernelSpec, n_train: int, m_grid: int, variance: str = "ozaki",
                     compute_var: bool = True) -> int:
     """krige_jobs' default fits in flight for jobs of this shape: 1 (job i+1's fit under job
@@ -832,11 +861,7 @@ def auto_fits_ahead(kernel: KernelSpec, n_train: int, m_grid: int, variance: str
     grid) 4.19e6 points/s back to back vs 2.8–3.3e6 with one fit in flight; the headline
     (N = 4096, 256²) 55.7 vs 61.3 ms per job with one."""
     _, n = fit_layout(kernel, max(1, int(n_train)), variance)
-    bd = kernel.block_dim
-    scale = (m_grid / 65536.0) * (n / (2.0 * 4096)) ** 2 * (bd / 2.0)
-    p = (1.0 + _PRED_MS_REF * scale) * (1.0 if variance == "ozaki" else 2.5)
-    if not compute_var:
-        p = 1.0 + 0.1 * (p - 1.0)
+    p = _predict_ms_model(kernel, n, m_grid, variance, compute_var)
     f = _FIT_MS_COEF * (n / NB) ** _FIT_MS_EXP
     return 1 if p > (_FIT_STRETCH - 1.0) * f else 0
 
@@ -855,39 +880,63 @@ def auto_fit_batch(kernel: KernelSpec, n_train: int, variance: str = "ozaki") ->
     return max(1, min(FIT_BATCH_MAX, FIT_BATCH_MAX_BYTES // max(per, 1)))
 
 
-def _krige_jobs_batched(jobs, b, variance, chunk, var_mode, compute_var, jitter, dev, stats):
-    """Back-to-back jobs with their fits in batches of up to b jobs of one matrix order."""
-    pred = None
-    look = None   # a job read ahead whose matrix order ended the previous batch
-    it = iter(jobs)
-    while True:
-        group = [look] if look is not None else []
-        look = None
-        n0 = fit_layout(group[0][0], _point_count(group[0][1], group[0][0].input_dim), variance)[1] if group else None
-        while len(group) < b:
-            job = next(it, None)
-            if job is None:
-                break
-            n1 = fit_layout(job[0], _point_count(job[1], job[0].input_dim), variance)[1]
-            if n0 is not None and n1 != n0:
-                look = job
-                break
-            n0 = n1
-            group.append(job)
-        if not group:
-            return
+def _job_groups(jobs, b, variance):
+    """Consecutive jobs in groups of up to b with one matrix order (a job of another order starts
+    the next group)."""
+    group, n0 = [], None
+    for job in jobs:
+        n1 = fit_layout(job[0], _point_count(job[1], job[0].input_dim), variance)[1]
+        if group and (n1 != n0 or len(group) == b):
+            yield group
+            group = []
+        group.append(job)
+        n0 = n1
+    if group:
+        yield group
+
+
+def _krige_jobs_batched(jobs, b, variance, chunk, var_mode, compute_var, jitter, dev, stats, ahead=False):
+    """Jobs with their fits in batches of up to b jobs of one matrix order (engine.fit_batch),
+    predicted one by one.  ahead=False: each batch's fit, then its predicts, on the current
+    stream.  ahead=True: batch g+1's fit on a side stream under batch g's predicts (queued after
+    batch g's first predict); the first batch, with nothing to overlap, joins on the host."""
+    main = torch.cuda.current_stream(dev)
+    side = side_stream(dev) if ahead else None
+    groups = _job_groups(jobs, b, variance)
+
+    def issue(group, first):
         for _ in group:
             note_fit_issued(stats)
-        fits = fit_batch([(k, x, y, nz) for k, x, y, nz, _ in group], variance=variance, jitter=jitter, device=dev,
-                         check=False)
-        for job, gp in zip(group, fits):
+        probs = [(k, x, y, nz) for k, x, y, nz, _ in group]
+        if side is None:
+            return fit_batch(probs, variance=variance, jitter=jitter, device=dev, check=False)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            return fit_batch(probs, variance=variance, jitter=jitter, device=dev, check=False, join=first)
+
+    pred = None
+    group = next(groups, None)
+    fits = issue(group, True) if group else None
+    while group:
+        if side is not None:
+            main.wait_stream(side)
+            for gp in fits:
+                gp.record_stream(main)
+        nxt, nfits = None, None
+        for q, (job, gp) in enumerate(zip(group, fits)):
             if pred is None or not pred.fits(gp):
                 pred = Predictor(gp, chunk)
             pred.gp = gp
             out = pred(job[4], var_mode=var_mode, compute_var=compute_var)
+            if q == 0 and side is not None:   # the next batch's fit under this batch's predicts
+                nxt = next(groups, None)
+                nfits = issue(nxt, False) if nxt else None
             gp.check()
             yield out
-        del fits
+        if side is None:
+            nxt = next(groups, None)
+            nfits = issue(nxt, False) if nxt else None
+        group, fits = nxt, nfits
 
 
 def _krige_jobs_serial(jobs, variance, chunk, var_mode, compute_var, jitter, dev, stats):

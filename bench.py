@@ -100,6 +100,9 @@ def parse():
     ap.add_argument("--batch-fits", type=int, default=None,
                     help="N=1 back-to-back job stream: fits per batched factorisation (engine.krige_jobs "
                          "batch_fits; default: the library's engine.auto_fit_batch)")
+    ap.add_argument("--batch-ahead", type=int, default=None,
+                    help="N=1 batched job stream: 1 = batch g+1's fit under batch g's predicts (engine.krige_jobs "
+                         "batch_ahead; default: the library's)")
     ap.add_argument("--sweep-concurrent", type=int, default=None,
                     help="config E: streams the settings' fit + LML are queued on (hyper.sweep concurrent; "
                          "default: the library's hyper.auto_concurrent)")
@@ -475,7 +478,8 @@ def main():
 
         def stream(k):   # the shipped API for a sweep of jobs
             return E.krige_jobs(itertools.repeat(job, k), variance=args.variance, chunk=args.chunk, stats=stats,
-                                fits_ahead=args.fits_ahead, batch_fits=args.batch_fits)
+                                fits_ahead=args.fits_ahead, batch_fits=args.batch_fits,
+                                **({} if args.batch_ahead is None else {"batch_ahead": bool(args.batch_ahead)}))
         api = "engine.krige_jobs"
     trace = os.environ.get("GP2D_BENCH_TRACE") == "1"   # per-step wall times on stderr (diagnostics)
 
@@ -638,6 +642,10 @@ def main():
                         else args.batch_fits) if (args.fits_ahead if args.fits_ahead is not None else
                                                   E.auto_fits_ahead(spec, args.ntrain, m, args.variance)) <= 0
                        else 1) if api == "engine.krige_jobs" else None,
+        "batch_ahead": (bool(args.batch_ahead) if args.batch_ahead is not None else
+                        E.auto_batch_ahead(spec, args.ntrain, m, E.auto_fit_batch(spec, args.ntrain, args.variance)
+                                           if args.batch_fits is None else args.batch_fits, args.variance))
+                       if api == "engine.krige_jobs" else None,
         "unpipelined": unpiped,
         "single_job": single_job,
         "timed_fits": timed_fits,

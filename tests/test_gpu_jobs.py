@@ -29,17 +29,18 @@ JOBS = [(1, 700, 60, "df"), (2, 700, 64, "mixed"), (3, 1500, 50, "df"), (4, 300,
         (5, 1500, 72, "mixed"), (6, 1500, 72, "df")]
 
 
-@pytest.mark.parametrize("variance,ahead,batch", [("ozaki", 1, None), ("f64", 1, None), ("ozaki", 2, None),
-                                                  ("ozaki", 3, None), ("ozaki", 0, None), ("ozaki", None, None),
-                                                  ("ozaki", 0, 1), ("ozaki", 0, 2), ("f64", 0, 3)])
-def test_krige_jobs_bit_identical_to_sequential(variance, ahead, batch):
+@pytest.mark.parametrize("variance,ahead,batch,bahead", [
+    ("ozaki", 1, None, False), ("f64", 1, None, False), ("ozaki", 2, None, False), ("ozaki", 3, None, False),
+    ("ozaki", 0, None, False), ("ozaki", None, None, False), ("ozaki", 0, 1, False), ("ozaki", 0, 2, False),
+    ("f64", 0, 3, False), ("ozaki", 0, 2, True), ("ozaki", 0, None, True)])
+def test_krige_jobs_bit_identical_to_sequential(variance, ahead, batch, bahead):
     """fits_ahead > 1: consecutive fits in flight together, each drawing its own internal
     factor stream set; fits_ahead = 0: back to back on one stream, the fits of consecutive jobs
     of one matrix order batched (batch_fits; None = auto, 8 here; the mixed sizes of JOBS end
     batches early) — still the bits of one job at a time."""
     jobs = [_job(*j) for j in JOBS]
     got = [(m.clone(), v.clone()) for m, v in E.krige_jobs(jobs, variance=variance, chunk=2048, fits_ahead=ahead,
-                                                             batch_fits=batch)]
+                                                             batch_fits=batch, batch_ahead=bahead)]
     assert len(got) == len(jobs)
     for (spec, x, y, noise, xg), (m, v) in zip(jobs, got):
         gp = E.fit(spec, x, y, noise, variance=variance)
@@ -47,10 +48,11 @@ def test_krige_jobs_bit_identical_to_sequential(variance, ahead, batch):
         assert torch.equal(m, rm) and torch.equal(v, rv)
 
 
-@pytest.mark.parametrize("ahead", [0, 1, 2])
-def test_krige_jobs_non_spd_raises_at_its_job(ahead):
+@pytest.mark.parametrize("ahead,bahead", [(0, False), (1, False), (2, False), (0, True)])
+def test_krige_jobs_non_spd_raises_at_its_job(ahead, bahead):
     jobs = [_job(1, 500, 40, "df"), _job(2, 500, 40, "df", noise=-100.0), _job(3, 500, 40, "df")]
-    gen = E.krige_jobs(jobs, variance="ozaki", chunk=1024, fits_ahead=ahead)
+    gen = E.krige_jobs(jobs, variance="ozaki", chunk=1024, fits_ahead=ahead, batch_fits=2 if bahead else None,
+                       batch_ahead=bahead)
     m, v = next(gen)
     assert torch.isfinite(v).all()
     with pytest.raises(np.linalg.LinAlgError):
