@@ -435,3 +435,49 @@ def test_round_robin_jobs_list_inputs(tmp_path):
             m, 2, [(int(r[i][f"lo{j}"]), int(r[i][f"hi{j}"]), r[i][f"mean{j}"]) for i in range(world)]), mu), j
         assert np.array_equal(GD.assemble_from_shards(
             m, 2, [(int(r[i][f"lo{j}"]), int(r[i][f"hi{j}"]), r[i][f"var{j}"]) for i in range(world)]), var), j
+
+
+def _sweep_settings():
+    return [dict(l_df=l, noise=nz) for l in (3.0, 5.0, 8.0) for nz in (0.0025, 0.01)] + [dict(noise=-50.0)]
+
+
+def _sweep_tracks():
+    rng = np.random.default_rng(31)
+    x = np.stack([rng.uniform(0, 60, 400), rng.uniform(0, 45, 400)], 1)
+    y = np.concatenate([np.sin(x[:, 1] / 7), np.cos(x[:, 0] / 9)]) + rng.normal(0, 0.05, 800)
+    return x, y
+
+
+def _sweep_worker(rank, world, port, out_dir):
+    for p in (ROOT, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from gp2d import engine as E
+    from gp2d import hyper as H
+    x, y = _sweep_tracks()
+    vals, grads = H.sweep(E.KernelSpec(kind="df", l_df=5.0), x, y, _sweep_settings(), noise=0.0025,
+                          eval_gradient=True)   # the default: each rank's settings in one batched factorisation
+    np.savez(os.path.join(out_dir, f"sweep{rank}.npz"), vals=vals, grads=grads)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sweep_two_ranks_batched_bit_identical(tmp_path):
+    """hyper.sweep over two ranks: each rank's settings (dealt round robin) fitted in one batched
+    factorisation, the results all-reduced — every rank holds one process's sweep, bit for bit,
+    the non-PD setting -inf."""
+    from gp2d import engine as E
+    from gp2d import hyper as H
+    world = 2
+    _spawn(_sweep_worker, world, str(tmp_path))
+    x, y = _sweep_tracks()
+    ref_v, ref_g = H.sweep(E.KernelSpec(kind="df", l_df=5.0), x, y, _sweep_settings(), noise=0.0025,
+                           eval_gradient=True, batch=1)
+    assert ref_v[-1] == -np.inf
+    for r in range(world):
+        got = np.load(os.path.join(tmp_path, f"sweep{r}.npz"))
+        assert np.array_equal(got["vals"], ref_v) and np.array_equal(got["grads"], ref_g)
