@@ -537,8 +537,11 @@ def main():
     single_job = {"ms": single_ms, "value": m_all / (single_ms * 1e-3), "reps": reps,
                   "fit": "rank 0, factor broadcast" if is_multi(ws) else "local"}
     if is_multi(ws) or args.single_job_dist:
-        single_job["distributed_fit"] = single_job_distributed(args, ws, spec, xt, yt, noise, xg, m_all, dev,
-                                                               pred_cache, mean, var, reps)
+        try:
+            single_job["distributed_fit"] = single_job_distributed(args, ws, spec, xt, yt, noise, xg, m_all, dev,
+                                                                   pred_cache, mean, var, reps)
+        except Exception as e:   # an informational reading: the timed value above stands without it
+            single_job["distributed_fit"] = {"error": f"{type(e).__name__}: {e}"}
 
     # mean-only throughput (secondary, same fit; at most 20 jobs)
     mo_steps = min(args.steps, 20)
