@@ -354,80 +354,91 @@ inline GemmParams gemm_params() {
 
 // ---------------------------------------------------------------------------------------
 // Skinny NT GEMM for the POTRF critical path (column update, panel TRSM):
-//   C[M×128] = alpha · A[M×128] · B[128×128]ᵀ + beta · C,   M a multiple of 32.
+//   C[M×128] = alpha · A[M×128] · B[128×128]ᵀ + beta · C,   M a multiple of R.
 // With K = 128 the 128×128-tile kernel above spends most of each tile waiting for its
-// next BK = 16 slab (≈ 45 µs per tile); here one workgroup owns a 32-row block and stages
-// its operands in two K-halves of 64 — 32 A rows and all 128 B rows each (B is identical
-// for every workgroup, so L2-resident) — with the second half's loads in flight during
-// the first half's MFMAs; 4 waves × (32 rows × 32 columns) of v_mfma_f64_16x16x4.  80 KB
-// of LDS, so a workgroup fits beside one workgroup of the 128×128 kernel (73.7 KB): these
-// launches sit on the critical path while the trailing SYRK fills the chip.  LDS rows are
-// 64 doubles with k XOR-swizzled by 2·(row & 15): the MFMA operand reads (16 rows × 2 k per
-// 32-lane half) touch 64 distinct banks and 16-B pairs (k, k+1) stay adjacent.
-// C may alias A row for row (the in-place TRSM): a workgroup reads all of its A rows before
-// it writes them, and no other workgroup touches those rows.
+// next BK = 16 slab (≈ 45 µs per tile); here one workgroup owns an R-row × CB-column block of
+// C and stages its operands in two K-halves of 64 — R A rows and the CB B rows of its columns
+// (B is identical for every workgroup, so L2-resident) — with the second half's loads in
+// flight during the first half's MFMAs; the 4 waves share the block's 16×16 tiles of
+// v_mfma_f64_16x16x4.  LDS rows are 64 doubles with k XOR-swizzled by 2·(row & 15): the MFMA
+// operand reads (16 rows × 2 k per 32-lane half) touch 64 distinct banks and 16-B pairs
+// (k, k+1) stay adjacent.  Every 16×16 tile of C sums its K = 128 in the same order (k = 4ks +
+// lane/16, ks ascending, the first half then the second) whatever R and CB, so all shapes give
+// the same bits.
+// Shapes (measured, tools/microbench/panel_bench.hip): a launch costs ≈ 11 µs even for four
+// workgroups — a workgroup's own 1 Mflop of f64 MFMAs at one wave per SIMD is ≈ 8k cycles — so
+// the column update splits its 128 columns over four workgroups (R = 32, CB = 32; one tile per
+// wave) and the in-place TRSM, whose workgroups must own whole rows, halves the rows (R = 16,
+// CB = 128).
+// C may alias A row for row only with CB = 128 (the in-place TRSM): a workgroup reads all of
+// its A rows before it writes them, and no other workgroup touches those rows.
+// Grid: (M / R, problems, 128 / CB).
 constexpr int PNL_R = 32;
 __device__ __forceinline__ int pnl_idx(int r, int k) { return r * 64 + (k ^ ((r & 15) << 1)); }
 
 // Problem batch: problem blockIdx.y at A + y·pA, B + y·pB, C + y·pC (0 for a lone launch).
+template <int R, int CB>
 __global__ __launch_bounds__(256) void gemm_f64_panel_kernel(const double* A, int64_t lda, const double* __restrict__ B,
                                                              int64_t ldb, double* C, int64_t ldc, double alpha,
                                                              double beta, int64_t pA, int64_t pB, int64_t pC) {
-  __shared__ __attribute__((aligned(16))) double As[PNL_R * 64];   // 16 KB
-  __shared__ __attribute__((aligned(16))) double Bs[128 * 64];     // 64 KB
+  static_assert((R == 16 || R == 32) && (CB == 32 || CB == 64 || CB == 128), "panel block shape");
+  constexpr int TJ = CB / 16;                  // column tiles of the block
+  constexpr int TPW = (R / 16) * TJ / 4;       // 16×16 tiles per wave: 1, 2 or 4
+  static_assert(TPW >= 1, "at least one tile per wave");
+  constexpr int NLD = (R + CB) * 32 / 256;     // 16-B loads per thread per K-half
+  __shared__ __attribute__((aligned(16))) double As[R * 64];
+  __shared__ __attribute__((aligned(16))) double Bs[CB * 64];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   A += blockIdx.y * pA;
   B += blockIdx.y * pB;
   C += blockIdx.y * pC;
-  const int64_t r0 = (int64_t)blockIdx.x * PNL_R;
-  // per K-half: 1024 A pairs + 4096 B pairs = 20 16-B loads per thread
-  auto load = [&](int h, d2 (&v)[20]) {
+  const int64_t r0 = (int64_t)blockIdx.x * R;
+  const int c0 = (int)blockIdx.z * CB;
+  auto load = [&](int h, d2 (&v)[NLD]) {
 #pragma unroll
-    for (int u = 0; u < 20; ++u) {
-      const int idx = tid + 256 * u;   // < 5120
-      if (idx < 1024) {
+    for (int u = 0; u < NLD; ++u) {
+      const int idx = tid + 256 * u;   // < (R + CB)·32
+      if (idx < R * 32) {
         const int r = idx >> 5, c = 64 * h + 2 * (idx & 31);
         v[u] = *reinterpret_cast<const d2*>(A + (r0 + r) * lda + c);
       } else {
-        const int j = idx - 1024, r = j >> 5, c = 64 * h + 2 * (j & 31);
-        v[u] = *reinterpret_cast<const d2*>(B + (int64_t)r * ldb + c);
+        const int j = idx - R * 32, r = j >> 5, c = 64 * h + 2 * (j & 31);
+        v[u] = *reinterpret_cast<const d2*>(B + (int64_t)(c0 + r) * ldb + c);
       }
     }
   };
-  auto stage = [&](const d2 (&v)[20]) {
+  auto stage = [&](const d2 (&v)[NLD]) {
 #pragma unroll
-    for (int u = 0; u < 20; ++u) {
+    for (int u = 0; u < NLD; ++u) {
       const int idx = tid + 256 * u;
-      if (idx < 1024) {
+      if (idx < R * 32) {
         const int r = idx >> 5, c = 2 * (idx & 31);
         *reinterpret_cast<d2*>(As + pnl_idx(r, c)) = v[u];
       } else {
-        const int j = idx - 1024, r = j >> 5, c = 2 * (j & 31);
+        const int j = idx - R * 32, r = j >> 5, c = 2 * (j & 31);
         *reinterpret_cast<d2*>(Bs + pnl_idx(r, c)) = v[u];
       }
     }
   };
-  d4 acc[2][2];
+  d4 acc[TPW];
 #pragma unroll
-  for (int ti = 0; ti < 2; ++ti)
-#pragma unroll
-    for (int tj = 0; tj < 2; ++tj) acc[ti][tj] = d4{0.0, 0.0, 0.0, 0.0};
+  for (int u = 0; u < TPW; ++u) acc[u] = d4{0.0, 0.0, 0.0, 0.0};
   const int l16 = lane & 15, lk = lane >> 4;
-  const int cb = 32 * wid;
+  auto tile_i = [&](int u) { return (wid * TPW + u) / TJ; };   // row tile of the wave's u-th tile
+  auto tile_j = [&](int u) { return (wid * TPW + u) % TJ; };   // column tile
   auto compute = [&]() {
 #pragma unroll 4
     for (int ks = 0; ks < 16; ++ks) {
       const int k = 4 * ks + lk;
-      const double a0 = As[pnl_idx(l16, k)], a1 = As[pnl_idx(16 + l16, k)];
-      const double b0 = Bs[pnl_idx(cb + l16, k)], b1 = Bs[pnl_idx(cb + 16 + l16, k)];
-      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+#pragma unroll
+      for (int u = 0; u < TPW; ++u) {
+        const double a = As[pnl_idx(16 * tile_i(u) + l16, k)], b = Bs[pnl_idx(16 * tile_j(u) + l16, k)];
+        acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[u], 0, 0, 0);
+      }
     }
   };
   {
-    d2 v[20];
+    d2 v[NLD];
     load(0, v);
     stage(v);
     load(1, v);   // second half in flight during the first half's MFMAs
@@ -438,20 +449,21 @@ __global__ __launch_bounds__(256) void gemm_f64_panel_kernel(const double* A, in
     __syncthreads();
     compute();
   }
-  // f64 C/D map: acc[r] of lane l is C[(l>>4) + 4r][l&15].  C may alias A: this workgroup's
-  // A rows were all read (into registers / LDS) before the barrier above.
+  // f64 C/D map: acc[r] of lane l is C[(l>>4) + 4r][l&15].  C may alias A (CB = 128 only): this
+  // workgroup's A rows were all read (into registers / LDS) before the barrier above.
 #pragma unroll
-  for (int ti = 0; ti < 2; ++ti)
+  for (int u = 0; u < TPW; ++u)
 #pragma unroll
-    for (int tj = 0; tj < 2; ++tj)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int64_t row = r0 + 16 * ti + lk + 4 * q;
-        const int col = cb + 16 * tj + l16;
-        double* cp = C + row * ldc + col;
-        const double old = (beta != 0.0) ? *cp : 0.0;
-        *cp = fma(alpha, acc[ti][tj][q], beta * old);
-      }
+    for (int q = 0; q < 4; ++q) {
+      const int64_t row = r0 + 16 * tile_i(u) + lk + 4 * q;
+      const int col = c0 + 16 * tile_j(u) + l16;
+      double* cp = C + row * ldc + col;
+      const double old = (beta != 0.0) ? *cp : 0.0;
+      *cp = fma(alpha, acc[u][q], beta * old);
+    }
 }
+
+// The two shapes of the POTRF chain: column update (C ≠ A) and in-place panel TRSM (C = A).
+constexpr int PNL_UPD_R = 32, PNL_UPD_CB = 32, PNL_TRSM_R = 16, PNL_TRSM_CB = 128;
 
 }  // namespace gp2d

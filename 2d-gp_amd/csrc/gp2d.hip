@@ -332,7 +332,7 @@ int launch_panel(double* A, int64_t lda, int k, int64_t n, const double* dinv, h
   if (rows <= 0) return 0;
   // in-place panel TRSM  L21 = A21 · inv(L11)ᵀ
   double* P = A + (int64_t)(k0 + NB) * lda + k0;
-  gemm_f64_panel_kernel<<<dim3((unsigned)(rows / PNL_R), (unsigned)nprob), 256, 0, s>>>(
+  gemm_f64_panel_kernel<PNL_TRSM_R, PNL_TRSM_CB><<<dim3((unsigned)(rows / PNL_TRSM_R), (unsigned)nprob, 1), 256, 0, s>>>(
       P, lda, dinv + (int64_t)k * NB * NB, NB, P, lda, 1.0, 0.0, sA, sD, sA);
   return check_launch("gemm_f64_panel_kernel");
 }
@@ -527,8 +527,9 @@ static int potrf_impl(double* A, int64_t n, int64_t lda, double* dinv, int* info
   auto colupdate = [&](int j, int p, hipStream_t st) -> int {
     const int64_t j0 = (int64_t)j * NB;
     const double* Lp = A + j0 * lda + (int64_t)p * NB;
-    gemm_f64_panel_kernel<<<dim3((unsigned)((n - j0) / PNL_R), (unsigned)nprob), 256, 0, st>>>(
-        Lp, lda, Lp, lda, A + j0 * lda + j0, lda, -1.0, 1.0, sA, sA, sA);
+    gemm_f64_panel_kernel<PNL_UPD_R, PNL_UPD_CB>
+        <<<dim3((unsigned)((n - j0) / PNL_UPD_R), (unsigned)nprob, NB / PNL_UPD_CB), 256, 0, st>>>(
+            Lp, lda, Lp, lda, A + j0 * lda + j0, lda, -1.0, 1.0, sA, sA, sA);
     return check_launch("gemm_f64_panel_kernel");
   };
   // diagonal block j (Cholesky + inverse) and its panel TRSM; then (fused) the inverse's
@@ -819,14 +820,15 @@ int gp2d_dfact_panel(double* A, int64_t n, int64_t lda, int s, double* panel, in
     const int64_t below = rows - c0 - NB;
     if (below <= 0) continue;
     double* Pj = As + (c0 + NB) * lda + c0;        // sub-column j below its diagonal block
-    gemm_f64_panel_kernel<<<(unsigned)(below / PNL_R), 256, 0, st>>>(Pj, lda, dinv + j * NB * NB, NB, Pj, lda,
-                                                                    1.0, 0.0, 0, 0, 0);
+    gemm_f64_panel_kernel<PNL_TRSM_R, PNL_TRSM_CB><<<(unsigned)(below / PNL_TRSM_R), 256, 0, st>>>(
+        Pj, lda, dinv + j * NB * NB, NB, Pj, lda, 1.0, 0.0, 0, 0, 0);
     GP2D_CHECK(check_launch("gemm_f64_panel_kernel"));
     for (int j2 = j + 1; j2 < DF_SBT; ++j2) {      // sub-column j2 (rows ≥ its diagonal) −= L_j · L_j[j2 rows]ᵀ
       const int64_t r2 = (int64_t)j2 * NB;
       const double* Lp = As + r2 * lda + c0;
-      gemm_f64_panel_kernel<<<(unsigned)((rows - r2) / PNL_R), 256, 0, st>>>(Lp, lda, Lp, lda, As + r2 * lda + r2,
-                                                                            lda, -1.0, 1.0, 0, 0, 0);
+      gemm_f64_panel_kernel<PNL_UPD_R, PNL_UPD_CB>
+          <<<dim3((unsigned)((rows - r2) / PNL_UPD_R), 1, NB / PNL_UPD_CB), 256, 0, st>>>(
+              Lp, lda, Lp, lda, As + r2 * lda + r2, lda, -1.0, 1.0, 0, 0, 0);
       GP2D_CHECK(check_launch("gemm_f64_panel_kernel"));
     }
   }
