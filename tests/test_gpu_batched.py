@@ -143,3 +143,18 @@ def test_sweep_batched_matches_individual_fits():
         assert v == rv and np.array_equal(g, rg)
     v2, g2 = H.sweep(ks, x, y, settings, noise=0.0025, eval_gradient=True)   # the default (auto batch)
     assert np.array_equal(v2, vals) and np.array_equal(g2, grads)
+
+
+def test_fit_batch_single_and_mixed_kinds():
+    """B = 1 is engine.fit; one batch may mix kernel families of one matrix order (df, cf,
+    mixed, different noise) — each problem keeps its own bits."""
+    x, y = tracks(640, seed=77)
+    k = E.KernelSpec(kind="mixed", l_df=4.0, l_cf=6.0, ratio=0.3)
+    (g1,) = E.fit_batch([(k, x, y, 0.004)], variance="ozaki")
+    ref = E.fit(k, x, y, 0.004, variance="ozaki")
+    assert same(g1.W, ref.W) and same(g1.alpha, ref.alpha)
+    probs = [(E.KernelSpec(kind="df", l_df=3.0), x, y, 0.0025), (E.KernelSpec(kind="cf", l_cf=7.0), x, y, 0.01),
+             (k, x, y, 0.004)]
+    for (kk, _, _, nz), gb in zip(probs, E.fit_batch(probs)):
+        g = E.fit(kk, x, y, nz)
+        assert same(gb.W, g.W) and same(gb.alpha, g.alpha)

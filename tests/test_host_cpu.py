@@ -342,3 +342,13 @@ def test_job_shape_defaults_live_in_the_library():
     assert not E.auto_batch_ahead(df, 1024, 128 * 128, 1)
     src = open(os.path.join(ROOT, "bench.py")).read()
     assert "a.fits_ahead = 0" not in src and "sweep_concurrent or 2" not in src
+
+
+def test_fit_batch_rejects_more_than_64_problems():
+    """engine.fit_batch / gp2d_potrf_batched take at most 64 problems per batch (checked on the
+    host before any device work)."""
+    from gp2d import engine as E
+    k = E.KernelSpec(kind="df")
+    with pytest.raises(ValueError, match="at most 64"):
+        E.fit_batch([(k, np.zeros((10, 2)), np.zeros(20), 0.01)] * 65)
+    assert E.fit_batch([]) == []
