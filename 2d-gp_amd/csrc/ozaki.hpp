@@ -437,11 +437,27 @@ __device__ __forceinline__ void vmwait_barrier(std::integral_constant<int, W>) {
 //              instead of idling the matrix cores (the epilogue alone is ≈ 17 % of a launch
 //              on random residues, tools/microbench ablation).  Costs: 1.5× the LDS-DMA
 //              pieces per MAC (the A slab is fetched by both column halves).
+// Moduli batch: a launch with gridDim.z > 1 runs modulus z's product on planes A + z·sA,
+// B + z·sB, C + z·sC with modulus m[z].  The dispatcher walks x, then y, then z, so one
+// modulus's tiles go out before the next one's (the L2 working set of a single-modulus launch)
+// and the next modulus's long-K tiles fill the previous one's tail instead of a launch gap.
+struct IgemmZ {
+  int64_t sA, sB, sC;
+  int m[OZ_MAXMOD];
+};
+constexpr int64_t kIgemmZBatchMaxN = 4096;   // predict_ozaki_impl batches the moduli up to this n
+
 template <int TBN, int NST>
 __global__ __launch_bounds__(TBN * 2, (TBN == 256) ? 1 : 2) void igemm_nt_mod_kernel(
     const int8_t* __restrict__ A, const int8_t* __restrict__ B, uint8_t* __restrict__ C, int64_t ldc, int M, int N,
     int K, int a_lower, int modulus, int alias_rb, int alias_ks, const int* __restrict__ slist,
-    const int* __restrict__ scnt) {
+    const int* __restrict__ scnt, const IgemmZ zb) {
+  if (gridDim.z > 1) {
+    A += blockIdx.z * zb.sA;
+    B += blockIdx.z * zb.sB;
+    C += blockIdx.z * zb.sC;
+    modulus = zb.m[blockIdx.z];
+  }
   static_assert(TBN == 256 || TBN == 128, "tile width");
   static_assert(NST >= 3 && NST <= 5, "ring depth 3..5 (the tail is written out for these)");
   constexpr int NW = TBN / 32;                 // waves: 8 or 4

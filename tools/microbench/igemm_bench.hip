@@ -18,7 +18,7 @@ using namespace gp2d;
 #endif
 #ifndef IGEMM_KERNEL
 #define IGEMM_KERNEL igemm_nt_mod_kernel<IG_TBN, IG_NST>
-#define IGEMM_EXTRA , nullptr, nullptr   // dense K loop (no slab list)
+#define IGEMM_EXTRA , nullptr, nullptr, gp2d::IgemmZ{}   // dense K loop (no slab list), one modulus
 #endif
 #ifndef IGEMM_EXTRA
 #define IGEMM_EXTRA
