@@ -867,17 +867,23 @@ def auto_fits_ahead(kernel: KernelSpec, n_train: int, m_grid: int, variance: str
 
 
 FIT_BATCH_MAX = 8
+FIT_BATCH_MAX_SMALL = 16        # matrix order ≤ FIT_BATCH_SMALL_N: the chain-bound sizes
+FIT_BATCH_SMALL_N = 2048
 FIT_BATCH_MAX_BYTES = 8 << 30
 
 
 def auto_fit_batch(kernel: KernelSpec, n_train: int, variance: str = "ozaki") -> int:
     """krige_jobs' default batch for back-to-back jobs: up to FIT_BATCH_MAX fits per batched
-    factorisation while the batch's matrices stay below FIT_BATCH_MAX_BYTES.  Measured
-    (profiles/r04_fit_batch.jsonl): N_train = 1024, 1/2/4/8 fits in 2.27 / 2.56 / 3.20 / 4.67 ms
-    (2.28 ms each alone); 4096: 8 fits in 64 ms (13.4 each)."""
+    factorisation (FIT_BATCH_MAX_SMALL for matrix orders ≤ FIT_BATCH_SMALL_N, whose fit is the
+    diagonal chain's latency) while the batch's matrices stay below FIT_BATCH_MAX_BYTES.
+    Measured (profiles/r04_fit_batch.jsonl): N_train = 1024, 1/2/4/8 fits in 2.27 / 2.56 / 3.20 /
+    4.67 ms (2.28 ms each alone); 4096: 8 fits in 64 ms (13.4 each).  Config B's job stream
+    (N_train = 1024, profiles/r04_bfit16_ab.jsonl): 8.33–8.38e6 points/s with 8 fits per batch,
+    9.39–9.46e6 with 16, 9.24–9.27e6 with 32."""
     _, n = fit_layout(kernel, max(1, int(n_train)), variance)
     per = 8 * (n * n + (n // 2 + NB) ** 2)
-    return max(1, min(FIT_BATCH_MAX, FIT_BATCH_MAX_BYTES // max(per, 1)))
+    cap = FIT_BATCH_MAX_SMALL if n <= FIT_BATCH_SMALL_N else FIT_BATCH_MAX
+    return max(1, min(cap, FIT_BATCH_MAX_BYTES // max(per, 1)))
 
 
 def _job_groups(jobs, b, variance):

@@ -270,8 +270,9 @@ def sweep(kernel: E.KernelSpec, x, y, settings, noise: float = None, jitter: flo
     return vals, (grads if eval_gradient else None)
 
 
-BATCH_MAX = 8
-BATCH_MAX_BYTES = 32 << 30   # factor + TRTRI workspace of one batch
+BATCH_MAX = 16              # config E (64 settings, N_train = 4096): 8 / 12 / 16 / 32 / 64 per batch
+BATCH_MAX_BYTES = 32 << 30   # 90.1 / 90.8 / 92.3 / 93.0 / 92.7 settings/s (profiles/r04_ebatch_ab.jsonl);
+                             # factor + TRTRI workspace of one batch
 
 
 def auto_batch(kernel: E.KernelSpec, x, n_settings: int, concurrent=None) -> int:

@@ -330,11 +330,13 @@ def test_job_shape_defaults_live_in_the_library():
     assert E.auto_fits_ahead(df, 4096, 256 * 256) == 1
     assert E.auto_fits_ahead(mixed, 16384, 512 * 512) == 1
     assert H.auto_concurrent(8, True) == 2 and H.auto_concurrent(8, False) == 1 and H.auto_concurrent(1, True) == 1
-    # batched factorisations: config B's back-to-back jobs and config E's sweep batch 8 fits
-    # (profiles/r04_fit_batch.jsonl); D-sized matrices (8 GB each) are not batched
-    assert E.auto_fit_batch(df, 1024) == 8 and E.auto_fit_batch(df, 4096) == 8 and E.auto_fit_batch(mixed, 16384) == 1
+    # batched factorisations: config B's back-to-back jobs 16 fits, N = 4096 job streams 8, config
+    # E's sweep 16 settings (profiles/r04_bfit16_ab.jsonl, r04_ebatch_ab.jsonl); D-sized matrices
+    # (8 GB each) are not batched
+    assert E.auto_fit_batch(df, 1024) == 16 and E.auto_fit_batch(df, 4096) == 8 and E.auto_fit_batch(mixed, 16384) == 1
     x = np.zeros((4096, 2))
-    assert H.auto_batch(df, x, 8) == 8 and H.auto_batch(df, x, 3) == 3 and H.auto_batch(df, x, 1) == 1
+    assert H.auto_batch(df, x, 64) == 16 and H.auto_batch(df, x, 8) == 8 and H.auto_batch(df, x, 3) == 3
+    assert H.auto_batch(df, x, 1) == 1
     assert H.auto_batch(df, x, 8, concurrent=2) == 1
     # config B's batches overlap the next batch's fit with their predicts (8.8e6 vs 7.8e6 points/s);
     # a tiny grid beside FLOP-bound N = 4096 batches does not
