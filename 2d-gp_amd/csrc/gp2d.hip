@@ -11,6 +11,7 @@
 #include "ozaki.hpp"
 #include "lml.hpp"
 #include "dfact.hpp"
+#include "order.hpp"
 #include "../../include/gp2d.h"
 
 #include <dlfcn.h>
@@ -108,6 +109,14 @@ static int assemble_impl(const double* xa, int64_t na, int64_t na_pad, const dou
 }
 
 
+// Dev knob for attribution A/Bs (tools/runs/r05_attrib.sh), never set in the product build:
+// bit 0 skips the POTRF trailing SYRKs, bit 1 the TRTRI products — the factor is then wrong, but
+// the fit's chain and its launch pattern stay, so a job stream shows what its predict pays for the
+// fit's FP64 GEMM arithmetic versus for its chain.
+#ifndef GP2D_DEV_SKIP
+#define GP2D_DEV_SKIP 0
+#endif
+
 // ------------------------------------------------------------- Ozaki constants
 static const int kModuli[OZ_MAXMOD] = {256, 255, 253, 251, 247, 241, 239, 233,
                                        229, 227, 223, 217, 211, 199, 197, 193};
@@ -122,8 +131,14 @@ static int ozaki_nmod_bits(double log2_pmax) {
   }
   return -1;
 }
-// worst case (sizing): |Pint| ≤ n·2^{pW}·2^{pB−1}
-static int ozaki_nmod_for(int64_t n) { return ozaki_nmod_bits(std::log2((double)n) + OZ_PW + OZ_PB - 1.0); }
+// worst case (sizing): |Pint| ≤ n·2^{pW}·2^{pB−1} at the largest W precision the guard can pick
+static int ozaki_nmod_for(int64_t n) { return ozaki_nmod_bits(std::log2((double)n) + OZ_PW_MAX + OZ_PB - 1.0); }
+// W precision of a call: 0 → the default OZ_PW; otherwise OZ_PW .. OZ_PW_MAX
+static int ozaki_wbits(int wbits) { return wbits == 0 ? OZ_PW : wbits; }
+static int valid_wbits(int wbits) {
+  GP2D_REQUIRE(wbits == 0 || (wbits >= OZ_PW && wbits <= OZ_PW_MAX), "ozaki: wbits must be 0 or 49..60");
+  return 0;
+}
 
 static int64_t modinv(int64_t a, int64_t m) {  // a⁻¹ mod m (a, m coprime)
   int64_t t = 0, nt = 1, r = m, nr = ((a % m) + m) % m;
@@ -147,8 +162,9 @@ static double kstar_bound(const gp2d_kernel_t* k) {
   }
 }
 
-static int make_ozaki_consts(int nmod, const gp2d_kernel_t* k, OzakiConsts& oc) {
+static int make_ozaki_consts(int nmod, const gp2d_kernel_t* k, OzakiConsts& oc, int pw = OZ_PW) {
   oc.nmod = nmod;
+  oc.pw = pw;
   GP2D_REQUIRE(oc.nmod > 0 && oc.nmod <= OZ_MAXMOD, "ozaki: bad number of moduli");
   double M = 1.0;
   for (int l = 0; l < oc.nmod; ++l) M *= (double)kModuli[l];
@@ -157,6 +173,8 @@ static int make_ozaki_consts(int nmod, const gp2d_kernel_t* k, OzakiConsts& oc) 
     oc.m[l] = kModuli[l];
     oc.md[l] = (double)kModuli[l];
     oc.inv_m[l] = 1.0 / (double)kModuli[l];
+    const int c26 = (int)(((int64_t)1 << OZ_SPLIT) % kModuli[l]);
+    oc.c26[l] = (double)(2 * c26 > kModuli[l] ? c26 - kModuli[l] : c26);   // centred
     oc.h[l] = oc.t[l] = 0.0;
   }
   for (int l = 0; l < oc.nmod; ++l) {
@@ -514,6 +532,7 @@ static int potrf_impl(double* A, int64_t n, int64_t lda, double* dinv, int* info
   std::vector<hipEvent_t>& ev = *fc.ev;
   hipEvent_t e_pan = ev[0], e_syrk = ev[1], e_join = ev[2], e_start = ev[3];
   hipEvent_t e_auxc[2] = {ev[4], ev[5]};   // aux's first update of an even / odd block column
+  if (info_dev) GP2D_EV(hipMemsetAsync(info_dev, 0, sizeof(int) * (size_t)nprob, s));   // the call resets info
   GP2D_EV(hipEventRecord(e_join, s));
   GP2D_EV(hipStreamWaitEvent(sc, e_join, 0));
   GP2D_EV(hipStreamWaitEvent(sb, e_join, 0));
@@ -598,7 +617,7 @@ static int potrf_impl(double* A, int64_t n, int64_t lda, double* dinv, int* info
             q.C = A + f0 * lda + f0;
             q.M = (int)(n - f0); q.N = hw * NB;
             q.cyc_lower = 1; q.mask_off = 0;
-            GP2D_CHECK((launch_gemm<true, EPI_STORE>(q, 1, sb, nprob)));
+            if (!(GP2D_DEV_SKIP & 1)) GP2D_CHECK((launch_gemm<true, EPI_STORE>(q, 1, sb, nprob)));
             GP2D_EV(hipEventRecord(e_head, sb));
             q.cyc_lower = 0;
           }
@@ -608,7 +627,7 @@ static int potrf_impl(double* A, int64_t n, int64_t lda, double* dinv, int* info
             q.B = q.A;
             q.C = A + f1 * lda + f1;
             q.M = (int)(n - f1); q.N = q.M; q.c_lower = 1;
-            GP2D_CHECK((launch_gemm<true, EPI_STORE>(q, 1, sb, nprob)));
+            if (!(GP2D_DEV_SKIP & 1)) GP2D_CHECK((launch_gemm<true, EPI_STORE>(q, 1, sb, nprob)));
           }
           if (hw == 0) GP2D_EV(hipEventRecord(e_head, sb));
         } else {
@@ -728,6 +747,7 @@ int gp2d_trtri(double* A, int64_t n, int64_t lda, const double* dinv, void* work
   }
   put_diag_blocks_kernel<<<dim3(NB * NB / 256, nb), 256, 0, s>>>(A, lda, dinv);
   GP2D_CHECK(check_launch("put_diag_blocks_kernel"));
+  if (GP2D_DEV_SKIP & 2) return 0;
   return trtri_levels(A, lda, nb, T, dwork + (size_t)nb * NB * NB, s);
 }
 
@@ -1072,7 +1092,7 @@ int gp2d_predict(const double* W, int64_t n, int64_t ldw, const double* alpha, c
       }
     }
     predict_finalize_kernel<<<(unsigned)((ncols + 63) / 64), 64, 0, s>>>(
-        pm, nmseg, P, npseg, ncols, cp, cv, c0, m, kss, add, clip, compute_var, mean, var);
+        pm, nmseg, P, npseg, ncols, cp, cv, c0, m, kss, add, clip, compute_var, mean, var, nullptr);
     GP2D_CHECK(check_launch("predict_finalize_kernel"));
   }
   return 0;
@@ -1086,20 +1106,22 @@ size_t gp2d_ozaki_wres_bytes(int64_t n) {
   return nm > 0 ? (size_t)nm * (size_t)n * (size_t)n : 0;
 }
 
-static int launch_w_res(const double* W, int64_t n, int64_t ldw, const OzakiConsts& oc, int8_t* wres,
+static int launch_w_res(const double* W, int64_t n, WRows ldw, const OzakiConsts& oc, int8_t* wres,
                         const double* rowscale, hipStream_t s) {
   ozaki_w_res_kernel<<<dim3((unsigned)(n / 64), (unsigned)(n / 256)), 256, 0, s>>>(W, n, ldw, oc, wres, rowscale);
   return check_launch("ozaki_w_res_kernel");
 }
 
-int gp2d_ozaki_prepare(const double* W, int64_t n, int64_t ldw, const gp2d_kernel_t* k, int8_t* wres,
+int gp2d_ozaki_prepare(const double* W, int64_t n, int64_t ldw, const gp2d_kernel_t* k, int wbits, int8_t* wres,
                        double* rowscale, int* nmod_out, void* stream) {
   GP2D_CHECK(validate_ozaki_kernel(k));
+  GP2D_CHECK(valid_wbits(wbits));
+  const int pw = ozaki_wbits(wbits);
   GP2D_REQUIRE(n % IBM == 0 && n > 0, "ozaki: n must be a positive multiple of 256");
   GP2D_REQUIRE(nmod_out != nullptr, "ozaki: nmod_out is NULL");
   hipStream_t s = S(stream);
   double* l1 = reinterpret_cast<double*>(wres);  // scratch: the planes are written afterwards
-  ozaki_w_scale_kernel<<<(unsigned)n, 256, 0, s>>>(W, n, ldw, rowscale, l1, 0.0, 0, 0);
+  ozaki_w_scale_kernel<<<(unsigned)n, 256, 0, s>>>(W, n, WRows{ldw}, pw, rowscale, l1, 0.0, 0, 0);
   GP2D_CHECK(check_launch("ozaki_w_scale_kernel"));
   std::vector<double> hl1((size_t)n), hs((size_t)n);
   if (hipMemcpyAsync(hl1.data(), l1, sizeof(double) * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -1130,32 +1152,90 @@ int gp2d_ozaki_prepare(const double* W, int64_t n, int64_t ldw, const gp2d_kerne
   const int nmod = ozaki_nmod_bits(std::log2(bmax));
   GP2D_REQUIRE(nmod > 0, "ozaki: row bound exceeds the modulus table");
   OzakiConsts oc;
-  GP2D_CHECK(make_ozaki_consts(nmod, k, oc));
+  GP2D_CHECK(make_ozaki_consts(nmod, k, oc, pw));
   ozaki_rowscale_final_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(rowscale, n, oc.M, oc.sB);
   GP2D_CHECK(check_launch("ozaki_rowscale_final_kernel"));
-  GP2D_CHECK(launch_w_res(W, n, ldw, oc, wres, rowscale, s));
+  GP2D_CHECK(launch_w_res(W, n, WRows{ldw}, oc, wres, rowscale, s));
+  *nmod_out = nmod;
+  return 0;
+}
+
+static int prepare_apriori(const double* W, int64_t n, WRows wr, const gp2d_kernel_t* k, double diag_add,
+                           int wbits, int8_t* wres, double* rowscale, int* nmod_out, hipStream_t s) {
+  GP2D_CHECK(validate_ozaki_kernel(k));
+  GP2D_CHECK(valid_wbits(wbits));
+  const int pw = ozaki_wbits(wbits);
+  GP2D_REQUIRE(n % IBM == 0 && n > 0, "ozaki: n must be a positive multiple of 256");
+  GP2D_REQUIRE(W != nullptr && wres != nullptr && rowscale != nullptr, "ozaki: NULL buffer");
+  GP2D_REQUIRE(nmod_out != nullptr, "ozaki: nmod_out is NULL");
+  // the a-priori count bounds the data-driven one for any fit with this K_y diagonal (no host
+  // round trip); a violated bound could only come from a failed factor and is poisoned by CRT
+  const int nmod = gp2d_ozaki_nmod_apriori(n, k, diag_add, pw);
+  GP2D_REQUIRE(nmod > 0, "ozaki: a-priori bound exceeds the modulus table");
+  OzakiConsts oc;
+  GP2D_CHECK(make_ozaki_consts(nmod, k, oc, pw));
+  // no L1 norms (the count is a-priori): one pass over W for the row exponents, one for the planes
+  ozaki_w_scale_kernel<<<(unsigned)n, 256, 0, s>>>(W, n, wr, pw, rowscale, nullptr, oc.M, oc.sB, 1);
+  GP2D_CHECK(check_launch("ozaki_w_scale_kernel"));
+  GP2D_CHECK(launch_w_res(W, n, wr, oc, wres, rowscale, s));
   *nmod_out = nmod;
   return 0;
 }
 
 int gp2d_ozaki_prepare_async(const double* W, int64_t n, int64_t ldw, const gp2d_kernel_t* k, double diag_add,
-                             int8_t* wres, double* rowscale, int* nmod_out, void* stream) {
-  GP2D_CHECK(validate_ozaki_kernel(k));
-  GP2D_REQUIRE(n % IBM == 0 && n > 0, "ozaki: n must be a positive multiple of 256");
-  GP2D_REQUIRE(nmod_out != nullptr, "ozaki: nmod_out is NULL");
-  // the a-priori count bounds the data-driven one for any fit with this K_y diagonal (no host
-  // round trip); a violated bound could only come from a failed factor and is poisoned by CRT
-  const int nmod = gp2d_ozaki_nmod_apriori(n, k, diag_add);
-  GP2D_REQUIRE(nmod > 0, "ozaki: a-priori bound exceeds the modulus table");
+                             int wbits, int8_t* wres, double* rowscale, int* nmod_out, void* stream) {
+  GP2D_REQUIRE(ldw >= n, "ozaki: ldw must be >= n");
+  return prepare_apriori(W, n, WRows{ldw}, k, diag_add, wbits, wres, rowscale, nmod_out, S(stream));
+}
+
+int gp2d_ozaki_prepare_packed(const double* packed, int64_t n, const gp2d_kernel_t* k, double diag_add, int wbits,
+                              int8_t* wres, double* rowscale, int* nmod_out, void* stream) {
+  GP2D_REQUIRE(n % NB == 0, "ozaki: n must be a multiple of 128 (the packing's row blocks)");
+  return prepare_apriori(packed, n, WRows{0}, k, diag_add, wbits, wres, rowscale, nmod_out, S(stream));
+}
+
+// ---- accuracy guard: what W precision the variance needs for this fit
+size_t gp2d_ozaki_guard_workspace(int64_t n) {
+  if (n <= 0) return 0;
+  return 2 * sizeof(double) * (size_t)((n + OZ_GUARD_RSEG - 1) / OZ_GUARD_RSEG) * (size_t)n;
+}
+
+int gp2d_ozaki_guard(const double* W, int64_t n, int64_t ldw, int64_t ntr, int64_t npad, double diag_add,
+                     double* stats, void* work, size_t work_bytes, void* stream) {
+  GP2D_REQUIRE(W && stats && n > 0 && ldw >= n && ntr >= 1 && npad >= ntr && (n == npad || n == 2 * npad),
+               "ozaki_guard: bad arguments");
+  // any δ: the formula is algebra on K = K_y − δI.  δ ≤ 0 (no noise, or a caller's negative
+  // "noise") gives a latent variance ≤ 0 at the observations, where no precision bounds the
+  // relative error — stats[0] ≤ 0 sends the fit to the FP64 engine
+  GP2D_REQUIRE(std::isfinite(diag_add), "ozaki_guard: the diagonal addition (noise + jitter) must be finite");
+  GP2D_REQUIRE(work != nullptr && work_bytes >= gp2d_ozaki_guard_workspace(n), "ozaki_guard: workspace too small");
   hipStream_t s = S(stream);
-  OzakiConsts oc;
-  GP2D_CHECK(make_ozaki_consts(nmod, k, oc));
-  // no L1 norms (the count is a-priori): one pass over W for the row exponents, one for the planes
-  ozaki_w_scale_kernel<<<(unsigned)n, 256, 0, s>>>(W, n, ldw, rowscale, nullptr, oc.M, oc.sB, 1);
-  GP2D_CHECK(check_launch("ozaki_w_scale_kernel"));
-  GP2D_CHECK(launch_w_res(W, n, ldw, oc, wres, rowscale, s));
-  *nmod_out = nmod;
-  return 0;
+  const int64_t nseg = (n + OZ_GUARD_RSEG - 1) / OZ_GUARD_RSEG;
+  double* psum = static_cast<double*>(work);
+  double* pmax = psum + nseg * n;
+  ozaki_guard_colsq_kernel<<<dim3((unsigned)((n + 255) / 256), (unsigned)nseg), 256, 0, s>>>(W, n, ldw, psum, pmax);
+  GP2D_CHECK(check_launch("ozaki_guard_colsq_kernel"));
+  ozaki_guard_finish_kernel<<<1, 1024, 0, s>>>(psum, pmax, n, nseg, ntr, npad, diag_add, stats);
+  return check_launch("ozaki_guard_finish_kernel");
+}
+
+// Elementwise relative error of the ozaki variance with W rows at `wbits` bits, modelled as
+// K·2^(49 − wbits)·(kss / v_min)^1.5 (v_min: the smallest latent posterior variance at the
+// observations, gp2d_ozaki_guard's stats[0]); K from the full-grid measurements of
+// tools/probe_guard.py (ℓ 2..12 km, noise 1e-4..5e-2, profiles/r05_guard_probe.jsonl), whose
+// measured/model ratios lie in [0.45, 0.85] — the constant sits above the largest of them.
+static constexpr double OZ_GUARD_K = 3.5e-15;
+double gp2d_ozaki_error_model(double kss, double vmin, int wbits) {
+  if (!(kss > 0.0)) return INFINITY;
+  if (!(vmin > 0.0)) return INFINITY;   // a non-positive latent variance: no precision covers it
+  return OZ_GUARD_K * std::ldexp(1.0, OZ_PW - ozaki_wbits(wbits)) * std::pow(kss / vmin, 1.5);
+}
+
+int gp2d_ozaki_guard_bits(double kss, double vmin, double target) {
+  if (!(target > 0.0)) return -1;
+  for (int b = OZ_PW; b <= OZ_PW_MAX; ++b)
+    if (gp2d_ozaki_error_model(kss, vmin, b) <= target) return b;
+  return 0;   // beyond the int8 engine's precision range: the FP64 engine
 }
 
 // ---- zero-slab skipping: K* block flags → per-B-tile slab lists (ozaki_slab_list_kernel)
@@ -1202,7 +1282,8 @@ static void launch_kstar(dim3 grid, hipStream_t s, const double* xtr, int64_t nt
 static int predict_ozaki_impl(const int8_t* wres, const double* rowscale, int nmod, int64_t n,
                               const double* alpha, const double* xtr, int64_t ntr,
                               int64_t ntr_pad, const double* xg, int64_t m, const gp2d_kernel_t* k, int var_mode,
-                              double noise, int compute_var, double* mean, double* var, int64_t chunk,
+                              double noise, int compute_var, double* mean, double* var,
+                              const int64_t* out_order, int64_t chunk,
                               int8_t* bres, uint8_t* cres, double* pm, double* P, uint8_t* flags, int* skip,
                               const int8_t* pre, size_t pre_stride, size_t pre_flags, hipStream_t s) {
   OzakiConsts oc;
@@ -1274,7 +1355,7 @@ static int predict_ozaki_impl(const int8_t* wres, const double* rowscale, int nm
       GP2D_CHECK(check_launch("ozaki_crt_colsq_kernel"));
     }
     predict_finalize_kernel<<<(unsigned)((ncols + 63) / 64), 64, 0, s>>>(
-        pm, nmseg, P, npseg, ncols, cp, cv, c0, m, kss, add, clip, compute_var, mean, var);
+        pm, nmseg, P, npseg, ncols, cp, cv, c0, m, kss, add, clip, compute_var, mean, var, out_order);
     GP2D_CHECK(check_launch("predict_finalize_kernel"));
   }
   return 0;
@@ -1289,8 +1370,8 @@ static size_t ozaki_partials(int64_t n) {
 int gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int nmod, int64_t n, const double* alpha,
                        const double* xtr,
                        int64_t ntr, int64_t ntr_pad, const double* xg, int64_t m, const gp2d_kernel_t* k,
-                       int var_mode, double noise, int compute_var, double* mean, double* var, int64_t chunk,
-                       void* work, size_t work_bytes, void* stream) {
+                       int var_mode, double noise, int compute_var, double* mean, double* var,
+                       const int64_t* out_order, int64_t chunk, void* work, size_t work_bytes, void* stream) {
   GP2D_CHECK(validate_ozaki_kernel(k));
   GP2D_REQUIRE(n == 2 * ntr_pad && n % IBM == 0, "ozaki: n must equal 2·ntr_pad and be a multiple of 256");
   GP2D_REQUIRE(chunk > 0 && chunk % (IBN / 2) == 0, "ozaki: chunk must be a positive multiple of 128");
@@ -1307,27 +1388,28 @@ int gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int nmod, int
   uint8_t* flags = reinterpret_cast<uint8_t*>(P + (size_t)(n / OZ_CRT_ROWS + 1) * ncols_max);
   int* skip = reinterpret_cast<int*>(flags + oz_flag_bytes(n, chunk));
   return predict_ozaki_impl(wres, rowscale, nmod, n, alpha, xtr, ntr, ntr_pad, xg, m, k, var_mode, noise,
-                            compute_var, mean, var, chunk, bres, cres, pm, P, flags, skip, nullptr, 0, 0,
+                            compute_var, mean, var, out_order, chunk, bres, cres, pm, P, flags, skip, nullptr, 0, 0,
                             S(stream));
 }
 
 // ---- K* residue planes ahead of the fit (they depend on the points and the kernel only)
-int gp2d_ozaki_nmod_apriori(int64_t n, const gp2d_kernel_t* k, double diag_add) {
+int gp2d_ozaki_nmod_apriori(int64_t n, const gp2d_kernel_t* k, double diag_add, int wbits) {
   // gp2d_ozaki_prepare's per-row bound (b) with the largest row exponent any fit can have:
   // W_ii = 1/L_ii ≥ 1/√(K_y,ii) (L_ii² = K_y,ii − Σ L_ik²), so max_k |W_ik| ≥ 1/√(kss + diag_add)
   // and s_i = p−1−⌊log2 max|W_i|⌋ ≤ s_max.  (1 − 2^-40) absorbs the rounding of L_ii; the
   // identity rows of padded points take bound (a) = 1.01·2^{2p−2}.  prepare's data-driven
   // count never exceeds this one.
-  if (validate_ozaki_kernel(k) != 0 || n <= 0) return -1;
+  if (validate_ozaki_kernel(k) != 0 || n <= 0 || valid_wbits(wbits) != 0) return -1;
+  const int pw = ozaki_wbits(wbits);
   const double kss = gp2d_kernel_diag(k);
   const double dmin = (1.0 - std::ldexp(1.0, -40)) / std::sqrt(kss + diag_add);
-  const int smax = OZ_PW - 1 - (int)std::floor(std::log2(dmin));
+  const int smax = pw - 1 - (int)std::floor(std::log2(dmin));
   OzakiConsts probe;
   if (make_ozaki_consts(1, k, probe) != 0) return -1;
   const double sq = 2.0 * std::sqrt(kss);
-  const double b = std::ldexp(sq, smax + probe.sB) + std::ldexp((double)n, OZ_PB - 2) + std::ldexp((double)n, OZ_PW) +
+  const double b = std::ldexp(sq, smax + probe.sB) + std::ldexp((double)n, OZ_PB - 2) + std::ldexp((double)n, pw) +
                    (double)n;
-  const double a_id = 1.01 * std::ldexp(1.0, OZ_PW + OZ_PB - 2);
+  const double a_id = 1.01 * std::ldexp(1.0, pw + OZ_PB - 2);
   return ozaki_nmod_bits(std::log2(std::max(b, a_id)));
 }
 
@@ -1378,8 +1460,8 @@ size_t gp2d_predict_ozaki_planes_workspace(int64_t n, int64_t chunk) {
 int gp2d_predict_ozaki_planes(const int8_t* wres, const double* rowscale, int nmod, int64_t n, const double* alpha,
                               const double* xtr, int64_t ntr, int64_t ntr_pad, const double* xg, int64_t m,
                               const gp2d_kernel_t* k, int var_mode, double noise, const int8_t* bres, int nmod_b,
-                              double* mean, double* var, int64_t chunk, void* work, size_t work_bytes,
-                              void* stream) {
+                              double* mean, double* var, const int64_t* out_order, int64_t chunk, void* work,
+                              size_t work_bytes, void* stream) {
   GP2D_CHECK(validate_ozaki_kernel(k));
   GP2D_REQUIRE(n == 2 * ntr_pad && n % IBM == 0, "ozaki: n must equal 2·ntr_pad and be a multiple of 256");
   GP2D_REQUIRE(chunk > 0 && chunk % (IBN / 2) == 0, "ozaki: chunk must be a positive multiple of 128");
@@ -1401,7 +1483,8 @@ int gp2d_predict_ozaki_planes(const int8_t* wres, const double* rowscale, int nm
   const size_t planes = (size_t)nmod_b * (size_t)n * (size_t)ncols_max;
   const size_t stride = planes + oz_flag_bytes(n, chunk);
   return predict_ozaki_impl(wres, rowscale, nmod, n, alpha, xtr, ntr, ntr_pad, xg, m, k, var_mode, noise, 1, mean,
-                            var, chunk, nullptr, cres, pm, P, nullptr, skip, bres, stride, planes, S(stream));
+                            var, out_order, chunk, nullptr, cres, pm, P, nullptr, skip, bres, stride, planes,
+                            S(stream));
 }
 
 int gp2d_morton_codes(const double* pts, int64_t n, int dim, double* bbox, int64_t* codes, void* stream) {
@@ -1411,6 +1494,76 @@ int gp2d_morton_codes(const double* pts, int64_t n, int dim, double* bbox, int64
   GP2D_CHECK(check_launch("morton_bbox_kernel"));
   morton_code_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(pts, n, dim, bbox, codes);
   return check_launch("morton_code_kernel");
+}
+
+// ---- Morton order on the device (order.hpp): codes → stable radix sort → gathered points
+static int64_t rs_tiles(int64_t n) { return (n + RS_TILE - 1) / RS_TILE; }
+static size_t rs_hist_bytes(int64_t n) { return (size_t)round_up((int64_t)RS_BINS * rs_tiles(n) * 4, 256); }
+
+size_t gp2d_morton_sort_workspace(int64_t n) {
+  if (n <= 0) return 0;
+  // bbox | codes ×2 | index ping-pong buffer | per-tile digit counts
+  return 256 + 3 * (size_t)round_up(n * 8, 256) + rs_hist_bytes(n);
+}
+
+int gp2d_morton_sort(const double* pts, int64_t n, int dim, double* sorted, int64_t* order, void* work,
+                     size_t work_bytes, void* stream) {
+  GP2D_REQUIRE(pts && order && n > 0 && (dim == 2 || dim == 3), "morton_sort: bad arguments");
+  GP2D_REQUIRE(n < (int64_t)1 << 31, "morton_sort: at most 2^31 − 1 points");
+  GP2D_REQUIRE(work != nullptr && work_bytes >= gp2d_morton_sort_workspace(n), "morton_sort: workspace too small");
+  hipStream_t s = S(stream);
+  char* w = static_cast<char*>(work);
+  double* bbox = reinterpret_cast<double*>(w);
+  const size_t nb8 = (size_t)round_up(n * 8, 256);
+  uint64_t* ka = reinterpret_cast<uint64_t*>(w + 256);
+  uint64_t* kb = reinterpret_cast<uint64_t*>(w + 256 + nb8);
+  int64_t* vb = reinterpret_cast<int64_t*>(w + 256 + 2 * nb8);
+  uint32_t* hist = reinterpret_cast<uint32_t*>(w + 256 + 3 * nb8);
+  GP2D_CHECK(gp2d_morton_codes(pts, n, dim, bbox, reinterpret_cast<int64_t*>(ka), stream));
+  // 21 bits per coordinate: 6 digit passes in 2-D, 8 in 3-D — an even count, so the indices of
+  // the last pass land in `order` (pass p writes the ping-pong buffer of its parity)
+  const int passes = (21 * dim + RS_BITS - 1) / RS_BITS;
+  const unsigned tiles = (unsigned)rs_tiles(n);
+  for (int p = 0; p < passes; ++p) {
+    const uint64_t* kin = (p & 1) ? kb : ka;
+    uint64_t* kout = (p & 1) ? ka : kb;
+    const int64_t* vin = p == 0 ? nullptr : ((p & 1) ? vb : order);
+    int64_t* vout = (p & 1) ? order : vb;
+    radix_hist_kernel<<<tiles, RS_THREADS, 0, s>>>(kin, n, RS_BITS * p, hist);
+    GP2D_CHECK(check_launch("radix_hist_kernel"));
+    radix_scan_kernel<<<1, 1024, 0, s>>>(hist, (int64_t)RS_BINS * tiles);
+    GP2D_CHECK(check_launch("radix_scan_kernel"));
+    radix_scatter_kernel<<<tiles, RS_THREADS, 0, s>>>(kin, vin, n, RS_BITS * p, hist, kout, vout);
+    GP2D_CHECK(check_launch("radix_scatter_kernel"));
+  }
+  static_assert((((21 * 2 + RS_BITS - 1) / RS_BITS) & 1) == 0 && (((21 * 3 + RS_BITS - 1) / RS_BITS) & 1) == 0,
+                "an even number of digit passes");
+  if (sorted == nullptr) return 0;
+  return gp2d_gather_rows(pts, order, n, dim, sorted, stream);
+}
+
+int gp2d_gather_rows(const double* src, const int64_t* order, int64_t n, int64_t dim, double* dst, void* stream) {
+  GP2D_REQUIRE(src && order && dst && n >= 0 && dim >= 1, "gather_rows: bad arguments");
+  GP2D_REQUIRE(src != dst, "gather_rows: src and dst must not alias");
+  GP2D_REQUIRE(n * dim < ((int64_t)1 << 40), "gather_rows: too many elements");
+  if (n == 0) return 0;
+  gather_rows_kernel<<<(unsigned)((n * dim + 255) / 256), 256, 0, S(stream)>>>(src, order, n, dim, dst);
+  return check_launch("gather_rows_kernel");
+}
+
+int gp2d_obs_pad(const double* y, int64_t ntr, int64_t npad, int bd, const int64_t* perm, double* out,
+                 void* stream) {
+  GP2D_REQUIRE(y && out && ntr >= 0 && npad >= ntr && npad > 0 && (bd == 1 || bd == 2), "obs_pad: bad arguments");
+  const int64_t t = (int64_t)bd * npad;
+  obs_pad_kernel<<<(unsigned)((t + 255) / 256), 256, 0, S(stream)>>>(y, ntr, npad, bd, perm, out);
+  return check_launch("obs_pad_kernel");
+}
+
+int gp2d_status_flip(int* status, int count, void* stream) {
+  GP2D_REQUIRE(status && count >= 0, "status_flip: bad arguments");
+  if (count == 0) return 0;
+  status_flip_kernel<<<(unsigned)((count + 63) / 64), 64, 0, S(stream)>>>(status, count);
+  return check_launch("status_flip_kernel");
 }
 
 // ------------------------------------------------- LOG MARGINAL LIKELIHOOD (§8f.1)

@@ -40,12 +40,18 @@ constexpr int OZ_MAXMOD = 16;
 // 47 + 47 and close to 50 + 50 (13 moduli); measured in DESIGN.md §3.1.
 constexpr int OZ_PW = GP2D_OZ_PW;
 constexpr int OZ_PB = GP2D_OZ_PB;
-static_assert(OZ_PW <= 52 && OZ_PB <= 52, "ozaki: scaled operands must stay exact in fp64");
+static_assert(OZ_PW <= 50 && OZ_PB <= 50, "ozaki: the one-part residues need |x| < 2^50");
+// The W precision is a run-time choice per fit (the accuracy guard, gp2d_ozaki_guard_bits):
+// OZ_PW is the default; up to OZ_PW_MAX bits the residue kernel splits Wint = xh·2^26 + xl.
+constexpr int OZ_PW_MAX = 60;
+constexpr int OZ_SPLIT = 26;
 constexpr int OZ_HBITS = 33;       // exact high part of inv_l / m_l
 
 struct OzakiConsts {
   int nmod;
+  int pw;                          // integer bits of the scaled W rows (OZ_PW .. OZ_PW_MAX)
   int m[OZ_MAXMOD];
+  double c26[OZ_MAXMOD];           // 2^26 mod m_l, centred (the split residues of pw > 50)
   double md[OZ_MAXMOD];            // m_l as a double (the residue kernels' fma operand)
   double inv_m[OZ_MAXMOD];         // 1 / m_l
   double h[OZ_MAXMOD];             // inv_l / m_l rounded to a multiple of 2^-33
@@ -96,18 +102,31 @@ __device__ __forceinline__ double block_reduce(double v, double* red, bool is_ma
   return r;
 }
 
-__global__ __launch_bounds__(256) void ozaki_w_scale_kernel(const double* __restrict__ W, int64_t n, int64_t ldw,
+// Row addressing of W: dense (row i at W + i·ldw) or the factor broadcast's packed lower block
+// triangle (gp2d_pack_lower: 128-row block rb keeps columns [0, 128·(rb+1)), blocks one after the
+// other), so a receiving rank prepares its planes straight from the payload.
+struct WRows {
+  int64_t ldw;   // 0: packed
+  __device__ __forceinline__ int64_t off(int64_t i) const {
+    if (ldw) return i * ldw;
+    const int64_t rb = i >> 7;
+    return ((rb * (rb + 1)) << 13) + (i & 127) * ((rb + 1) << 7);   // 128²·rb(rb+1)/2 + r·128(rb+1)
+  }
+  __device__ __forceinline__ int64_t len(int64_t i, int64_t n) const { return ldw ? n : ((i >> 7) + 1) << 7; }
+};
+
+__global__ __launch_bounds__(256) void ozaki_w_scale_kernel(const double* __restrict__ W, int64_t n, WRows wr, int pw,
                                                             double* __restrict__ rowscale, double* __restrict__ l1,
                                                             double M, int sB, int final_scale) {
   __shared__ double red[256];
   const int64_t i = blockIdx.x;
   const int tid = threadIdx.x;
-  const double* w = W + i * ldw;
+  const double* w = W + wr.off(i);
   double mx = 0.0;
   for (int64_t k = tid; k <= i; k += 256) mx = fmax(mx, fabs(w[k]));
   mx = block_reduce(mx, red, true);
   const int e = (mx > 0.0) ? ilogb(mx) : 0;    // 2^e ≤ mx < 2^{e+1}
-  const int si = OZ_PW - 1 - e;                // |W·2^si| < 2^OZ_PW
+  const int si = pw - 1 - e;                   // |W·2^si| < 2^pw
   double sum = 0.0;
   if (l1 != nullptr) {   // the row's L1 norm (the data-driven moduli count only)
     for (int64_t k = tid; k <= i; k += 256) sum += fabs(rint(ldexp(w[k], si)));
@@ -139,7 +158,7 @@ __device__ __forceinline__ int ozaki_row_exp(double rowscale_i, const OzakiConst
 // 4 consecutive k per lane, 32 B of each row read contiguously — and writes, per modulus, the
 // 4 rows' 64-B runs of the slab tile: 256 contiguous bytes per wave store (the per-row form
 // wrote four 64-B pieces 16 KB apart).
-__global__ __launch_bounds__(256) void ozaki_w_res_kernel(const double* __restrict__ W, int64_t n, int64_t ldw,
+__global__ __launch_bounds__(256) void ozaki_w_res_kernel(const double* __restrict__ W, int64_t n, WRows wr,
                                                           OzakiConsts oc, int8_t* __restrict__ wres,
                                                           const double* __restrict__ rowscale) {
   const int64_t bi = blockIdx.y, ks = blockIdx.x;
@@ -151,8 +170,12 @@ __global__ __launch_bounds__(256) void ozaki_w_res_kernel(const double* __restri
   for (int it = 0; it < 16; ++it) {
     const int64_t i = bi * 256 + wv * 64 + it * 4 + (lane >> 4);
     const int si = ozaki_row_exp(rowscale[i], oc);
-    const double* w = W + i * ldw + k0;
-    const d2 p0 = *reinterpret_cast<const d2*>(w), p1 = *reinterpret_cast<const d2*>(w + 2);
+    const double* w = W + wr.off(i) + k0;
+    d2 p0 = {0.0, 0.0}, p1 = {0.0, 0.0};
+    if (k0 < wr.len(i, n)) {   // k0 and the row length are multiples of 4: all four or none stored
+      p0 = *reinterpret_cast<const d2*>(w);
+      p1 = *reinterpret_cast<const d2*>(w + 2);
+    }
     const double v[4] = {p0.x, p0.y, p1.x, p1.y};
     double x[4], xm[4];
 #pragma unroll
@@ -161,12 +184,33 @@ __global__ __launch_bounds__(256) void ozaki_w_res_kernel(const double* __restri
       xm[u] = x[u] + OZ_MAGIC52;
     }
     int8_t* dst = wres + slab_offset(i, k0, n);
-    for (int l = 0; l < oc.nmod; ++l) {
-      const double m = oc.md[l], im = oc.inv_m[l];
-      uint32_t r[4];   // |x| < 2^pW
+    if (oc.pw <= 50) {   // uniform: |x| < 2^50, one exact residue per modulus
+      for (int l = 0; l < oc.nmod; ++l) {
+        const double m = oc.md[l], im = oc.inv_m[l];
+        uint32_t r[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) r[u] = residue_low_m(x[u], xm[u], m, im);
-      *reinterpret_cast<uint32_t*>(dst + (int64_t)l * plane) = pack22(pack2_lo(r[0], r[1]), pack2_lo(r[2], r[3]));
+        for (int u = 0; u < 4; ++u) r[u] = residue_low_m(x[u], xm[u], m, im);
+        *reinterpret_cast<uint32_t*>(dst + (int64_t)l * plane) = pack22(pack2_lo(r[0], r[1]), pack2_lo(r[2], r[3]));
+      }
+    } else {             // |x| < 2^60: x = xh·2^26 + xl exactly (|xl| ≤ 2^25, |xh| < 2^35), and
+      //                    x ≡ rh·(2^26 mod m) + rl (mod m) with the centred residues rh, rl (|·| ≤ 128)
+      double xh[4], xl[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        xh[u] = rint(ldexp(x[u], -OZ_SPLIT));
+        xl[u] = x[u] - ldexp(xh[u], OZ_SPLIT);   // exact: an integer below 2^26 in magnitude
+      }
+      for (int l = 0; l < oc.nmod; ++l) {
+        const double m = oc.md[l], im = oc.inv_m[l], c = oc.c26[l];
+        uint32_t r[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const double rh = fma(-m, rint(xh[u] * im), xh[u]), rl = fma(-m, rint(xl[u] * im), xl[u]);
+          const double t = fma(rh, c, rl);         // exact: |t| ≤ 128·128 + 128
+          r[u] = residue_low_m(t, t + OZ_MAGIC52, m, im);
+        }
+        *reinterpret_cast<uint32_t*>(dst + (int64_t)l * plane) = pack22(pack2_lo(r[0], r[1]), pack2_lo(r[2], r[3]));
+      }
     }
   }
 }
@@ -657,6 +701,64 @@ __global__ __launch_bounds__(TBN * 2, (TBN == 256) ? 1 : 2) void igemm_nt_mod_ke
     const int cloc = id >> 4, ch = id & 15;
     const uint4 v = *reinterpret_cast<const uint4*>(T + cloc * TP + 16 * ch);
     *reinterpret_cast<uint4*>(C + (int64_t)(j0 + cloc) * ldc + i0 + 16 * ch) = v;
+  }
+}
+
+// ------------------------------------------------------------------ accuracy guard statistics
+// What the W precision must cover (gp2d_ozaki_guard_bits): the variance loses digits where the
+// posterior variance is small against kss, and it is smallest at the observations.  At training
+// point i the latent posterior variance is exact from the factor alone: with K_y = K + δI,
+// [K − K·K_y⁻¹·K]_ii = δ − δ²·(K_y⁻¹)_ii and (K_y⁻¹)_ii = Σ_k W_ki² (a column norm of W = L⁻¹).
+// Pass 1: per 256-row segment and column, Σ W_rc² and max |W_rc| (blocks above the diagonal skip).
+constexpr int OZ_GUARD_RSEG = 256;
+__global__ __launch_bounds__(256) void ozaki_guard_colsq_kernel(const double* __restrict__ W, int64_t n, int64_t ldw,
+                                                                double* __restrict__ psum, double* __restrict__ pmax) {
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x, seg = blockIdx.y;
+  const int64_t r0 = seg * OZ_GUARD_RSEG, r1 = min<int64_t>(n, r0 + OZ_GUARD_RSEG);
+  if (c >= n) return;
+  double sq = 0.0, mx = 0.0;
+  if (r1 > (int64_t)blockIdx.x * 256) {   // the segment reaches this column block's diagonal
+#pragma unroll 8
+    for (int64_t r = r0; r < r1; ++r) {
+      const double w = W[r * ldw + c];
+      sq = fma(w, w, sq);
+      mx = fmax(mx, fabs(w));
+    }
+  }
+  psum[seg * n + c] = sq;
+  pmax[seg * n + c] = mx;
+}
+
+// Pass 2 (one workgroup): (K_y⁻¹)_cc = Σ_seg psum in segment order (deterministic), the latent
+// variance δ(1 − δ·(K_y⁻¹)_cc) at the observed components (c < ntr or npad ≤ c < npad + ntr),
+// stats[0] = its minimum, stats[1] = max |W|.
+__global__ __launch_bounds__(1024) void ozaki_guard_finish_kernel(const double* __restrict__ psum,
+                                                                  const double* __restrict__ pmax, int64_t n,
+                                                                  int64_t nseg, int64_t ntr, int64_t npad, double delta,
+                                                                  double* __restrict__ stats) {
+  __shared__ double red[2][16];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  double vmin = INFINITY, wmax = 0.0;
+  for (int64_t c = tid; c < n; c += 1024) {
+    double sq = 0.0, mx = 0.0;
+    for (int64_t g = 0; g < nseg; ++g) {
+      sq += psum[g * n + c];
+      mx = fmax(mx, pmax[g * n + c]);
+    }
+    wmax = fmax(wmax, mx);
+    const int64_t loc = c < npad ? c : c - npad;
+    if (loc < ntr) vmin = fmin(vmin, delta * (1.0 - delta * sq));
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    vmin = fmin(vmin, __shfl_xor(vmin, o));
+    wmax = fmax(wmax, __shfl_xor(wmax, o));
+  }
+  if (lane == 0) { red[0][w] = vmin; red[1][w] = wmax; }
+  __syncthreads();
+  if (tid == 0) {
+    for (int q = 1; q < 16; ++q) { vmin = fmin(vmin, red[0][q]); wmax = fmax(wmax, red[1][q]); }
+    stats[0] = vmin;
+    stats[1] = wmax;
   }
 }
 

@@ -22,11 +22,14 @@ __global__ __launch_bounds__(256) void mean_part_kernel(const double* __restrict
   pm[(int64_t)blockIdx.y * ncols + c] = s;
 }
 
-// Combine partials in fixed order and scatter to the [u..., v...] outputs.
+// Combine partials in fixed order and scatter to the [u..., v...] outputs.  order (optional):
+// grid point c0 + loc of this (reordered) chunk is the caller's point order[c0 + loc], so the
+// outputs land in the caller's order (the ozaki engine predicts its grid in Morton order).
 __global__ __launch_bounds__(256) void predict_finalize_kernel(
     const double* __restrict__ pm, int64_t nmseg, const double* __restrict__ P, int64_t npseg,
     int64_t ncols, int64_t cpad, int64_t cvalid, int64_t c0, int64_t m, double kss, double add,
-    int clip, int compute_var, double* __restrict__ mean, double* __restrict__ var) {
+    int clip, int compute_var, double* __restrict__ mean, double* __restrict__ var,
+    const int64_t* __restrict__ order) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= ncols) return;
   const int64_t comp = c / cpad, loc = c - comp * cpad;
@@ -35,7 +38,7 @@ __global__ __launch_bounds__(256) void predict_finalize_kernel(
   // the same left-to-right sums; unrolled so that eight partials are in flight per thread
 #pragma unroll 8
   for (int64_t g = 0; g < nmseg; ++g) mu += pm[g * ncols + c];
-  const int64_t o = comp * m + c0 + loc;
+  const int64_t o = comp * m + (order ? order[c0 + loc] : c0 + loc);
   mean[o] = mu;
   if (compute_var) {
     double q = 0.0;

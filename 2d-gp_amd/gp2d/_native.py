@@ -12,7 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GP2D_LIB", os.path.join(_HERE, "libgp2d.so"))
-ABI_VERSION = 8          # GP2D_ABI_VERSION in include/gp2d.h
+ABI_VERSION = 9          # GP2D_ABI_VERSION in include/gp2d.h
 
 FAMILY_VECTOR2D, FAMILY_ARD_RBF, FAMILY_VECTOR_ST = 0, 1, 2
 KIND_SCALAR, KIND_DIVFREE, KIND_CURLFREE, KIND_MIXED = 0, 1, 2, 3
@@ -25,13 +25,15 @@ EXPORTS = (
     "gp2d_potrf_inv_workspace", "gp2d_potrf_inv", "gp2d_potrf_batched", "gp2d_trtri_batched_workspace",
     "gp2d_trtri_batched",
     "gp2d_potrs_workspace", "gp2d_potrs_inv", "gp2d_predict_workspace", "gp2d_predict",
-    "gp2d_ozaki_nmod", "gp2d_ozaki_wres_bytes", "gp2d_ozaki_prepare", "gp2d_ozaki_prepare_async",
+    "gp2d_ozaki_nmod", "gp2d_ozaki_wres_bytes", "gp2d_ozaki_prepare", "gp2d_ozaki_prepare_async", "gp2d_ozaki_prepare_packed",
+    "gp2d_ozaki_guard_workspace", "gp2d_ozaki_guard", "gp2d_ozaki_error_model", "gp2d_ozaki_guard_bits",
     "gp2d_predict_ozaki_workspace",
     "gp2d_predict_ozaki", "gp2d_ozaki_nmod_apriori", "gp2d_ozaki_kstar_bytes", "gp2d_ozaki_kstar",
-    "gp2d_predict_ozaki_planes_workspace", "gp2d_predict_ozaki_planes", "gp2d_ozaki_set_skip", "gp2d_morton_codes", "gp2d_lml", "gp2d_lml_grad_count",
+    "gp2d_predict_ozaki_planes_workspace", "gp2d_predict_ozaki_planes", "gp2d_ozaki_set_skip", "gp2d_morton_codes",
+    "gp2d_morton_sort_workspace", "gp2d_morton_sort", "gp2d_gather_rows", "gp2d_obs_pad", "gp2d_lml", "gp2d_lml_grad_count",
     "gp2d_lml_grad_workspace", "gp2d_lml_grad",
     "gp2d_kernel_grad_count", "gp2d_kernel_grad_workspace", "gp2d_kernel_grad",
-    "gp2d_gemm", "gp2d_transpose", "gp2d_bcast",
+    "gp2d_gemm", "gp2d_transpose", "gp2d_bcast", "gp2d_status_flip",
     "gp2d_dfact_sb", "gp2d_dfact_panel_doubles", "gp2d_dfact_workspace", "gp2d_dfact_panel", "gp2d_dfact_update",
     "gp2d_dfact_invstep", "gp2d_dfact_zpart", "gp2d_dfact_zsum", "gp2d_dfact_alpha_workspace", "gp2d_dfact_alpha_blocks",
     "gp2d_assemble_cols", "gp2d_copy2d", "gp2d_zero_upper", "gp2d_pack_lower_doubles", "gp2d_pack_lower",
@@ -95,19 +97,28 @@ _SIGS = {
     "gp2d_predict": (_I, [_P, _I64, _I64, _P, _P, _I64, _I64, _P, _I64, _KP, _I, _D, _I, _P, _P, _I64, _P, _SZ, _P]),
     "gp2d_ozaki_nmod": (_I, [_I64]),
     "gp2d_ozaki_wres_bytes": (_SZ, [_I64]),
-    "gp2d_ozaki_prepare": (_I, [_P, _I64, _I64, _KP, _P, _P, ctypes.POINTER(_I), _P]),
-    "gp2d_ozaki_nmod_apriori": (_I, [_I64, _KP, _D]),
-    "gp2d_ozaki_prepare_async": (_I, [_P, _I64, _I64, _KP, _D, _P, _P, ctypes.POINTER(_I), _P]),
+    "gp2d_ozaki_prepare": (_I, [_P, _I64, _I64, _KP, _I, _P, _P, ctypes.POINTER(_I), _P]),
+    "gp2d_ozaki_nmod_apriori": (_I, [_I64, _KP, _D, _I]),
+    "gp2d_ozaki_prepare_async": (_I, [_P, _I64, _I64, _KP, _D, _I, _P, _P, ctypes.POINTER(_I), _P]),
+    "gp2d_ozaki_prepare_packed": (_I, [_P, _I64, _KP, _D, _I, _P, _P, ctypes.POINTER(_I), _P]),
+    "gp2d_ozaki_guard_workspace": (_SZ, [_I64]),
+    "gp2d_ozaki_guard": (_I, [_P, _I64, _I64, _I64, _I64, _D, _P, _P, _SZ, _P]),
+    "gp2d_ozaki_error_model": (_D, [_D, _D, _I]),
+    "gp2d_ozaki_guard_bits": (_I, [_D, _D, _D]),
     "gp2d_ozaki_kstar_bytes": (_SZ, [_I64, _I64, _I64, _I]),
     "gp2d_ozaki_kstar": (_I, [_P, _I64, _I64, _P, _I64, _KP, _I, _I64, _P, _SZ, _P]),
     "gp2d_predict_ozaki_planes_workspace": (_SZ, [_I64, _I64]),
     "gp2d_predict_ozaki_planes": (_I, [_P, _P, _I, _I64, _P, _P, _I64, _I64, _P, _I64, _KP, _I, _D, _P, _I, _P, _P,
-                                       _I64, _P, _SZ, _P]),
+                                       _P, _I64, _P, _SZ, _P]),
     "gp2d_predict_ozaki_workspace": (_SZ, [_I64, _I64]),
     "gp2d_ozaki_set_skip": (None, [_I]),
     "gp2d_morton_codes": (_I, [_P, _I64, _I, _P, _P, _P]),
-    "gp2d_predict_ozaki": (_I, [_P, _P, _I, _I64, _P, _P, _I64, _I64, _P, _I64, _KP, _I, _D, _I, _P, _P, _I64, _P,
-                                _SZ, _P]),
+    "gp2d_morton_sort_workspace": (_SZ, [_I64]),
+    "gp2d_morton_sort": (_I, [_P, _I64, _I, _P, _P, _P, _SZ, _P]),
+    "gp2d_gather_rows": (_I, [_P, _P, _I64, _I64, _P, _P]),
+    "gp2d_obs_pad": (_I, [_P, _I64, _I64, _I, _P, _P, _P]),
+    "gp2d_predict_ozaki": (_I, [_P, _P, _I, _I64, _P, _P, _I64, _I64, _P, _I64, _KP, _I, _D, _I, _P, _P, _P, _I64,
+                                _P, _SZ, _P]),
     "gp2d_lml": (_I, [_P, _I64, _I64, _P, _P, _I64, _P, _P]),
     "gp2d_lml_grad_count": (_I, [_KP]),
     "gp2d_lml_grad_workspace": (_SZ, [_I64]),
@@ -118,6 +129,7 @@ _SIGS = {
     "gp2d_gemm": (_I, [_I, _I64, _I64, _I64, _D, _P, _I64, _P, _I64, _D, _P, _I64, _P]),
     "gp2d_transpose": (_I, [_P, _I64, _I64, _P, _P]),
     "gp2d_bcast": (_I, [_P, _SZ, _I, _P, _P]),
+    "gp2d_status_flip": (_I, [_P, _I, _P]),
     "gp2d_dfact_sb": (_I, []),
     "gp2d_dfact_panel_doubles": (_SZ, [_I64]),
     "gp2d_dfact_workspace": (_SZ, [_I64]),

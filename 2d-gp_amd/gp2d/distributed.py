@@ -38,19 +38,28 @@ def world():
 
 
 def broadcast_fit(gp: E.GPFit | None, spec: E.KernelSpec, noise: float, x, device, src: int = 0,
-                  error: Exception | None = None, layout: tuple | None = None) -> E.GPFit:
+                  error: Exception | None = None, layout: tuple | None = None,
+                  planes_only: float | None = None, comm: dict | None = None) -> E.GPFit:
     """Broadcast W, α and the training points from `src` to every rank (RCCL
     ncclBroadcast under the 'nccl' backend).  Ranks other than `src` pass gp=None.
 
-    layout=None: a metadata broadcast first carries the sizes and a status word, read on the
-    host (one round trip); if the fit failed on `src` (`error`, e.g. a non-positive-definite K_y)
-    EVERY rank raises here (numpy.linalg.LinAlgError for a failed factor) instead of waiting for a
-    factor that never comes.
+    layout=None: a metadata broadcast first carries the sizes, a status word and the owner's
+    accuracy-guard decision (engine.apply_guard), read on the host (one round trip); if the fit
+    failed on `src` (`error`, e.g. a non-positive-definite K_y) EVERY rank raises here
+    (numpy.linalg.LinAlgError for a failed factor) instead of waiting for a factor that never comes.
 
     layout=(n, n_train, n_pad) (the job stream, where every rank knows the job's sizes): no host
-    round trip at all — the status travels on the device beside the factor (the owner's POTRF
-    `info`, or −1 for an error raised on the host) and the returned fit carries it as pending:
-    GPFit.check() raises, on every rank, once the job's predict has been queued."""
+    round trip at all — the owner's status block (engine.status_block: POTRF `info`, or −1 for an
+    error raised on the host, and the guard's statistics) travels on the device beside the factor
+    and the returned fit carries it as pending: GPFit.check() raises on every rank, and applies
+    the same guard decision on every rank, before the job's predict is queued.
+
+    planes_only=diag_add (the receiver of a job stream that predicts with the ozaki engine): the
+    receiving ranks build their INT8 residue planes straight from the packed payload
+    (gp2d_ozaki_prepare_packed) and keep no n×n W (the returned fit has W = None) — no zero-fill
+    and no unpack of an n×n matrix per job.
+    comm (optional dict): bytes this rank sends / receives and the collectives' HIP-event times
+    are appended under 'bcast' (collect with comm_summary)."""
     ws, rank = world()
     if _solo(ws):
         if error is not None:
@@ -58,15 +67,18 @@ def broadcast_fit(gp: E.GPFit | None, spec: E.KernelSpec, noise: float, x, devic
         return gp
     dev = torch.device(device)
     status = None
+    wbits = None   # the owner's guard decision (layout=None): −1 = FP64 engine, else the W bits
     if layout is None:
-        meta = torch.zeros(4, dtype=torch.int64, device=dev)
         if rank == src:
-            if error is None:
-                meta[0], meta[1], meta[2] = gp.n, gp.n_train, gp.n_pad
-            else:
-                meta[3] = 1 if isinstance(error, np.linalg.LinAlgError) else 2
+            g = (gp.extra.get("guard") or {}) if gp is not None else {}
+            wb = -1 if g.get("engine") == "f64" else int(g.get("wbits") or 0)
+            st = 0 if error is None else (1 if isinstance(error, np.linalg.LinAlgError) else 2)
+            vals = [gp.n, gp.n_train, gp.n_pad, st, wb] if error is None else [0, 0, 0, st, 0]
+            meta = torch.tensor(vals, dtype=torch.int64).to(dev)
+        else:
+            meta = torch.empty(5, dtype=torch.int64, device=dev)
         dist.broadcast(meta, src)
-        n, ntr, npad, st = (int(v) for v in meta.tolist())
+        n, ntr, npad, st, wbits = (int(v) for v in meta.tolist())
         if st != 0:
             if rank == src:
                 raise error
@@ -75,39 +87,112 @@ def broadcast_fit(gp: E.GPFit | None, spec: E.KernelSpec, noise: float, x, devic
             raise RuntimeError(f"the fit on rank {src} failed")
     else:
         n, ntr, npad = (int(v) for v in layout)
-        status = torch.full((1,), -1, dtype=torch.int32, device=dev)
         prep_err = gp.pending[2] if (gp is not None and gp.pending is not None) else None
         if rank == src and error is None and gp is not None and prep_err is None:
-            info = gp.extra.get("info_dev")
-            if info is not None:
-                status.copy_(info)
-            else:
-                status.zero_()
-        # an error the owner's fit deferred to check() (a failed int8 preparation) keeps the
-        # status at −1: the receivers raise at this job too instead of yielding it
+            status = gp.extra["status_dev"]   # broadcast in place (the owner's pending read is its own)
+        elif rank == src:
+            # an error raised on the owner's host, or one its fit deferred to check() (a failed
+            # int8 preparation): status −1, so the receivers raise at this job too
+            status = torch.tensor([0.0, 0.0, 0.0], dtype=torch.float64)
+            status.view(torch.int32)[0] = -1
+            status = status.to(dev)
+        else:
+            status = torch.empty(3, dtype=torch.float64, device=dev)
         dist.broadcast(status, src)
     packed = torch.empty(_packed_len(n), dtype=torch.float64, device=dev)
-    if rank == src and gp is not None and error is None:
-        W, X, alpha = gp.W, gp.x, gp.alpha
-        _pack_lower(W, n, packed, unpack=False)
-    else:
-        W = torch.zeros((n, n), dtype=torch.float64, device=dev)
+    owner_ok = rank == src and gp is not None and error is None
+    if owner_ok:
+        X, alpha = gp.x, gp.alpha
+        _pack_lower(gp.W, n, packed, unpack=False)
+    elif rank == src:   # a failed fit: the receivers still expect the payload (and raise on its status)
         alpha = torch.zeros(n, dtype=torch.float64, device=dev)
         X = torch.zeros((ntr, spec.input_dim), dtype=torch.float64, device=dev)
-        if rank == src:
-            packed.zero_()
+        packed.zero_()
+    else:               # overwritten by the broadcasts
+        alpha = torch.empty(n, dtype=torch.float64, device=dev)
+        X = torch.empty((ntr, spec.input_dim), dtype=torch.float64, device=dev)
     # W = L⁻¹ is lower-triangular: only the row blocks' [0, end of their diagonal block)
     # columns travel (≈ half of n² doubles)
-    dist.broadcast(packed, src)
-    dist.broadcast(alpha, src)
-    dist.broadcast(X, src)
-    if rank == src and gp is not None and error is None:
+    with _timed(comm, "bcast", rank == src, 8 * (packed.numel() + alpha.numel() + X.numel()), ws, device=dev):
+        dist.broadcast(packed, src)
+        dist.broadcast(alpha, src)
+        dist.broadcast(X, src)
+    if owner_ok:
         out = gp
+    elif planes_only is not None and spec.is_vector and packed.is_cuda:
+        out = E.GPFit(kernel=spec, noise=float(noise), x=X, n_train=ntr, n_pad=npad, W=None, alpha=alpha, device=dev,
+                      n_mat=n)
+        E.ozaki_prepare(out, diag_add=float(planes_only), packed=packed)
+        # the owner's guard statistics arrive in the status block: check() applies the same rule
+        out.extra["guard"] = dict(pending=True, diag_add=float(planes_only),
+                                  stream=torch.cuda.current_stream(dev))
     else:
+        W = torch.zeros((n, n), dtype=torch.float64, device=dev)   # the strict upper part stays 0
         _pack_lower(W, n, packed, unpack=True)
         out = E.GPFit(kernel=spec, noise=float(noise), x=X, n_train=ntr, n_pad=npad, W=W, alpha=alpha, device=dev)
-    if status is not None and out is not gp:   # the owner's own fit keeps its pending info read
+        if wbits is not None and wbits != 0:   # the owner's guard decision, applied as is
+            out.extra["guard"] = dict(pending=False, engine="f64" if wbits < 0 else "ozaki",
+                                      wbits=None if wbits < 0 else wbits)
+    if status is not None and out is not gp:   # the owner's own fit keeps its pending status read
         out.pending = E.pending_status(status, error if rank == src else None)
+    return out
+
+
+class _timed:
+    """Context manager around one collective (or a group of them) for the N > 1 bench line's
+    `comm` block: HIP events on the current stream for device tensors (the collective's stream
+    is ordered with it both ways by torch.distributed), host wall time otherwise (the gloo CPU
+    tests).  Appends (start, end, bytes sent, bytes received) to comm[key]; comm=None records
+    nothing.  Bytes are the payload this rank puts in / takes out of the collective: the root of
+    a broadcast sends it once and the others receive it; an all-gather sends this rank's part and
+    receives the other ranks' parts (the transport's own fan-out is RCCL's)."""
+
+    def __init__(self, comm: dict | None, key: str, sends: bool, nbytes: int, ws: int, recv: int | None = None,
+                 device=None):
+        self.comm, self.key = comm, key
+        self.sent = int(nbytes) if sends else 0
+        self.recv = int(recv) if recv is not None else (0 if sends else int(nbytes))
+        dev = torch.device(device) if device is not None else None
+        self.dev = dev if (dev is not None and dev.type == "cuda") else None
+
+    def __enter__(self):
+        if self.comm is None:
+            return self
+        if self.dev is not None:
+            self.t0 = torch.cuda.Event(enable_timing=True)
+            self.t0.record(torch.cuda.current_stream(self.dev))
+        else:
+            self.t0 = time.perf_counter()
+        return self
+
+    def __exit__(self, *exc):
+        if self.comm is None or exc[0] is not None:
+            return False
+        if self.dev is not None:
+            t1 = torch.cuda.Event(enable_timing=True)
+            t1.record(torch.cuda.current_stream(self.dev))
+        else:
+            t1 = time.perf_counter()
+        self.comm.setdefault(self.key, []).append((self.t0, t1, self.sent, self.recv))
+        return False
+
+
+def comm_summary(comm: dict | None) -> dict:
+    """{key: {calls, ms, bytes_sent, bytes_recv}} from a comm dict filled by the collectives
+    (waits for their end events); the dict is emptied."""
+    out = {}
+    for key, recs in (comm or {}).items():
+        ms = 0.0
+        for t0, t1, _, _ in recs:
+            if isinstance(t0, float):
+                ms += 1e3 * (t1 - t0)
+            else:
+                t1.synchronize()
+                ms += t0.elapsed_time(t1)
+        out[key] = dict(calls=len(recs), ms=ms, bytes_sent=sum(r[2] for r in recs),
+                        bytes_recv=sum(r[3] for r in recs))
+    if comm is not None:
+        comm.clear()
     return out
 
 
@@ -163,8 +248,10 @@ def fit_sharded(spec: E.KernelSpec, x, y, noise: float, device, mode: str = "bca
         except Exception as e:   # noqa: BLE001 — re-raised on every rank by broadcast_fit
             err = e
     gp = broadcast_fit(gp, spec, noise, x, device, error=err)
-    if variance == "ozaki" and "ozaki" not in gp.extra:
-        E.ozaki_prepare(gp, diag_add=float(noise + jitter))   # a-priori moduli count: no host sync
+    g = gp.extra.get("guard") or {}
+    if variance == "ozaki" and "ozaki" not in gp.extra and g.get("engine") != "f64":
+        # a-priori moduli count (no host sync), at the owner's guard precision
+        E.ozaki_prepare(gp, diag_add=float(noise + jitter), wbits=int(g.get("wbits") or 0))
     return gp
 
 
@@ -190,7 +277,7 @@ def _owned_blocks(nsb: int, ws: int, r: int):
 
 def fit_distributed(spec: E.KernelSpec, x, y, noise: float, device=None, variance: str = "ozaki",
                     jitter: float = 0.0, lookahead: bool = True, stats: dict | None = None,
-                    emulate: tuple | None = None) -> E.GPFit:
+                    emulate: tuple | None = None, comm: dict | None = None) -> E.GPFit:
     """ONE job's fit spread over all ranks (the config-D single job: /root/reference/krig.py:541-557
     predicts one model's large grid): every rank assembles K_y, then a 1-D block-cyclic POTRF
     fused with the right-looking TRTRI (include/gp2d.h gp2d_dfact_*) — rank s mod P factors
@@ -212,7 +299,10 @@ def fit_distributed(spec: E.KernelSpec, x, y, noise: float, device=None, varianc
     emulate=(P, r) (measurement only, tools/probe_dfit.py; one process, no process group): run
     rank r's share of a P-rank factorisation — its panels, updates and inverse steps, no
     broadcast (the panels it did not factor hold stale data) and no all-gather; the returned
-    factor is NOT W."""
+    factor is NOT W.
+
+    comm (optional dict): per-collective bytes and HIP-event times — 'panel_bcast' (one per step),
+    'w_allgather', 'alpha_allgather' (comm_summary)."""
     ws, rank = world()
     if emulate is not None:
         if ws != 1:
@@ -235,8 +325,7 @@ def fit_distributed(spec: E.KernelSpec, x, y, noise: float, device=None, varianc
         raise ValueError(f"the ozaki variance engine supports n < 131072; got n = {n}")
     perm = None
     if variance == "ozaki" and ntr > 1:
-        perm = E.morton_order(X)
-        X = X[perm].contiguous()
+        perm, X = E.morton_sort(X)
     main = torch.cuda.current_stream(dev)
     sh = E._stream_handle(dev)
     P = E._ptr
@@ -259,8 +348,8 @@ def fit_distributed(spec: E.KernelSpec, x, y, noise: float, device=None, varianc
     panels = [torch.empty(pdoubles, dtype=torch.float64, device=dev) for _ in range(2)]
     wbytes = int(L.gp2d_dfact_workspace(n))
     work = torch.empty(wbytes // 8 + 1, dtype=torch.float64, device=dev)
-    info = torch.zeros(1, dtype=torch.int32, device=dev)
-    comm = E.side_stream(dev)
+    info = torch.zeros(1, dtype=torch.int32, device=dev)   # the owners' panels only ever raise it
+    cstream = E.side_stream(dev)
     t0 = time.perf_counter()
 
     factored = {}   # s → event after the owner's gp2d_dfact_panel(s) (main or crit stream)
@@ -293,13 +382,13 @@ def fit_distributed(spec: E.KernelSpec, x, y, noise: float, device=None, varianc
             # the buffer's previous user (step s − 2) is done; the owner's panel s is written —
             # the broadcast does not wait for the rest of step s − 1 (it overlaps it)
             if s >= 2:
-                wait_done(comm, s - 2)
+                wait_done(cstream, s - 2)
                 done.pop(s - 2)
             if owner == rank:
-                comm.wait_event(factored.pop(s))
-            with torch.cuda.stream(comm):
+                cstream.wait_event(factored.pop(s))
+            with torch.cuda.stream(cstream), _timed(comm, "panel_bcast", owner == rank, 8 * rows * SB, ws, device=dev):
                 dist.broadcast(buf[:rows * SB], owner)
-            main.wait_stream(comm)
+            main.wait_stream(cstream)
         elif s in factored:   # one rank: the panel was factored on the chain stream
             main.wait_event(factored.pop(s))
         nxt = s + 1
@@ -335,7 +424,7 @@ def fit_distributed(spec: E.KernelSpec, x, y, noise: float, device=None, varianc
     del panels, work
     t1 = time.perf_counter()
     if not _solo(ws) and emulate is None:
-        _allgather_w_columns(A, n, ws, rank, dev)
+        _allgather_w_columns(A, n, ws, rank, dev, comm)
         allreduce_first_failure(info)
     if multi:
         # W = L⁻¹ is zero above each super-block's diagonal block: the owned columns were reset
@@ -344,25 +433,22 @@ def fit_distributed(spec: E.KernelSpec, x, y, noise: float, device=None, varianc
             if t % ws != rank and t > 0:
                 A[:t * SB, t * SB:(t + 1) * SB].zero_()
     t2 = time.perf_counter()
-    Y = E._pad_obs(y, ntr, npad, bd, dev)
-    if perm is not None:
-        for c in range(bd):
-            Y[c * npad:c * npad + ntr] = Y[c * npad:c * npad + ntr][perm]
-    alpha = _alpha_owned(A, n, Y, ws, rank, nsb, SB, dev, collective=not _solo(ws) and emulate is None)
+    Y = E._pad_obs(y, ntr, npad, bd, dev, perm)
+    alpha = _alpha_owned(A, n, Y, ws, rank, nsb, SB, dev, collective=not _solo(ws) and emulate is None, comm=comm)
     gp = E.GPFit(kernel=spec, noise=float(noise), x=X, n_train=ntr, n_pad=npad, W=A, alpha=alpha, device=dev,
                  y=Y, perm=perm)
     if emulate is not None:
         return gp
     E._raise_fit_errors(int(info.item()), None)
-    if variance == "ozaki":
-        E.ozaki_prepare(gp, diag_add=float(noise + jitter))
+    if variance == "ozaki":   # every rank holds the whole W: each applies the guard itself (same bits)
+        E.ozaki_prepare_guarded(gp, float(noise + jitter))
     if stats is not None:
         stats.update(host_factor_s=t1 - t0, host_gather_s=t2 - t1)
     return gp
 
 
 def _alpha_owned(A: torch.Tensor, n: int, Y: torch.Tensor, ws: int, rank: int, nsb: int, SB: int, dev,
-                 collective: bool) -> torch.Tensor:
+                 collective: bool, comm: dict | None = None) -> torch.Tensor:
     """α = Wᵀ(W y) from this rank's super-columns only (gp2d_dfact_zpart / _zsum / _alpha_blocks):
     z = Σ_t W[:, t]·y[t] over the super-columns in t order (each rank's partials gathered), then
     α[t] = W[:, t]ᵀ·z for the owned t, gathered.  Every piece is computed from one super-column
@@ -378,9 +464,11 @@ def _alpha_owned(A: torch.Tensor, n: int, Y: torch.Tensor, ws: int, rank: int, n
         E.N.check(L.gp2d_dfact_zpart(P(A), n, n, mine[0], dt, len(mine), P(Y), P(zp), sh), "gp2d_dfact_zpart")
     if collective:
         allz = torch.empty((ws, cap, n), dtype=torch.float64, device=dev)
-        _all_gather(allz, zp, ws)
-        order = torch.tensor([(t % ws) * cap + t // ws for t in range(nsb)], device=dev)
-        parts = allz.view(ws * cap, n).index_select(0, order).contiguous()
+        with _timed(comm, "alpha_allgather", True, 8 * zp.numel(), ws, recv=8 * zp.numel() * (ws - 1), device=dev):
+            _all_gather(allz, zp, ws)
+        order = _cyclic_order(nsb, ws, cap, dev)
+        parts = torch.empty((nsb, n), dtype=torch.float64, device=dev)
+        E.N.check(L.gp2d_gather_rows(P(allz), P(order), nsb, n, P(parts), sh), "gp2d_gather_rows")
     elif ws > 1:   # emulate: this rank's partials only (the emulated factor is not W either)
         parts = zp[:len(mine)].contiguous()
     else:
@@ -398,9 +486,18 @@ def _alpha_owned(A: torch.Tensor, n: int, Y: torch.Tensor, ws: int, rank: int, n
             return torch.zeros(n, dtype=torch.float64, device=dev)
         return ab.reshape(-1)[:n].contiguous()
     alla = torch.empty((ws, cap, SB), dtype=torch.float64, device=dev)
-    _all_gather(alla, ab, ws)
-    order = torch.tensor([(t % ws) * cap + t // ws for t in range(nsb)], device=dev)
-    return alla.view(ws * cap, SB).index_select(0, order).reshape(-1).contiguous()
+    with _timed(comm, "alpha_allgather", True, 8 * ab.numel(), ws, recv=8 * ab.numel() * (ws - 1), device=dev):
+        _all_gather(alla, ab, ws)
+    alpha = torch.empty(nsb * SB, dtype=torch.float64, device=dev)
+    E.N.check(L.gp2d_gather_rows(P(alla), P(_cyclic_order(nsb, ws, cap, dev)), nsb, SB, P(alpha), sh),
+              "gp2d_gather_rows")
+    return alpha
+
+
+def _cyclic_order(nsb: int, ws: int, cap: int, dev) -> torch.Tensor:
+    """Row of the all-gathered (rank, slot) buffer that holds super-column t, for t < nsb (rank
+    t mod ws, its slot t div ws) — the block-cyclic deal back in column order."""
+    return torch.as_tensor(np.array([(t % ws) * cap + t // ws for t in range(nsb)], dtype=np.int64), device=dev)
 
 
 def _all_gather(out: torch.Tensor, t: torch.Tensor, ws: int):
@@ -415,14 +512,23 @@ def allreduce_first_failure(info: torch.Tensor) -> torch.Tensor:
     to the FIRST failing minor over the ranks, in place.  A non-SPD panel's NaNs spread into
     later panels that other ranks own, so a MAX would report the last failure and the message
     would change with the world size; 0 → INT32_MAX, MIN, back gives the one-rank answer."""
-    big = torch.iinfo(torch.int32).max
-    info.copy_(torch.where(info == 0, torch.full_like(info, big), info))
+    if info.is_cuda:
+        flip = lambda: E.N.check(E.N.lib().gp2d_status_flip(E._ptr(info), info.numel(),   # noqa: E731
+                                                            E._stream_handle(info.device)), "gp2d_status_flip")
+    else:   # the gloo CPU tests of the communication logic
+        big = torch.iinfo(torch.int32).max
+
+        def flip():
+            z, b = info == 0, info == big
+            info[z] = big
+            info[b] = 0
+    flip()                                 # 0 ↔ INT32_MAX, so MIN finds the first failure
     dist.all_reduce(info, op=dist.ReduceOp.MIN)
-    info.copy_(torch.where(info == big, torch.zeros_like(info), info))
+    flip()
     return info
 
 
-def _allgather_w_columns(A: torch.Tensor, n: int, ws: int, rank: int, dev):
+def _allgather_w_columns(A: torch.Tensor, n: int, ws: int, rank: int, dev, comm: dict | None = None):
     """Every rank's W super-columns to every rank: super-column t travels as its rows
     [SB·t, n) (the part below the diagonal block's top; W is zero above it)."""
     L = E.N.lib()
@@ -438,10 +544,11 @@ def _allgather_w_columns(A: torch.Tensor, n: int, ws: int, rank: int, dev):
         E.N.check(L.gp2d_copy2d(P(send[off:]), SB, P(A[t * SB:, t * SB:]), n, rows, SB, sh), "gp2d_copy2d")
         off += rows * SB
     recv = torch.empty(ws * cap, dtype=torch.float64, device=dev)
-    if dist.get_backend() == "nccl":
-        dist.all_gather_into_tensor(recv, send)
-    else:   # gloo (the CPU / shared-card rehearsals)
-        dist.all_gather(list(recv.view(ws, cap).unbind(0)), send)
+    with _timed(comm, "w_allgather", True, 8 * sizes[rank], ws, recv=8 * (sum(sizes) - sizes[rank]), device=dev):
+        if dist.get_backend() == "nccl":
+            dist.all_gather_into_tensor(recv, send)
+        else:   # gloo (the CPU / shared-card rehearsals)
+            dist.all_gather(list(recv.view(ws, cap).unbind(0)), send)
     for r in range(ws):
         if r == rank:
             continue
@@ -454,7 +561,7 @@ def _allgather_w_columns(A: torch.Tensor, n: int, ws: int, rank: int, dev):
 
 def krige_jobs_sharded(jobs, variance: str = "ozaki", chunk: int = 8192, var_mode: str = "latent",
                        compute_var: bool = True, jitter: float = 0.0, device=None, align: int = 64,
-                       stats: dict | None = None):
+                       stats: dict | None = None, comm: dict | None = None):
     """A stream of independent kriging jobs (kernel, x, y, noise, xg) — the reference's
     runKrig.py sweep / per-window krig.kriging calls — spread over all ranks: job j is FITTED
     by rank j mod world only (round robin, on a side stream, up to one job per rank ahead),
@@ -470,7 +577,9 @@ def krige_jobs_sharded(jobs, variance: str = "ozaki", chunk: int = 8192, var_mod
     owner only; x may be a tensor, an array or a nested list.  A non-SPD K_y raises
     numpy.linalg.LinAlgError on every rank at that job.  Nothing is
     read ahead before the first next(); `stats` counts the fits this rank issues (with their
-    host time stamps, engine.note_fit_issued)."""
+    host time stamps, engine.note_fit_issued); `comm` collects the factor broadcasts' bytes and
+    HIP-event times (comm_summary).  A receiving rank of the ozaki engine keeps only the INT8
+    planes of a job's factor (broadcast_fit planes_only)."""
     ws, rank = world()
     dev = E._require_device(device)
     if _solo(ws):   # one rank: the single-GPU pipelined form (the next fit under this predict)
@@ -487,7 +596,7 @@ def krige_jobs_sharded(jobs, variance: str = "ozaki", chunk: int = 8192, var_mod
         return
     main = torch.cuda.current_stream(dev)
     fit_stream = E.side_stream(dev)
-    comm = E.side_stream(dev)   # broadcasts + the receivers' int8 preparation
+    comm_stream = E.side_stream(dev)   # broadcasts + the receivers' int8 preparation
     it = iter(jobs)
     window = collections.deque()   # (index, job) read ahead
     own = {}                       # index → (gp, error, event) of this rank's fits in flight
@@ -526,19 +635,20 @@ def krige_jobs_sharded(jobs, variance: str = "ozaki", chunk: int = 8192, var_mod
         if owner == rank:
             gp, err, ev = own.pop(idx)
             if gp is not None:
-                comm.wait_event(ev)
-                gp.record_stream(comm)   # its status word is the factor's info (the owner's own
-                #                          check() also raises a preparation error)
+                comm_stream.wait_event(ev)
+                gp.record_stream(comm_stream)   # its status word is the factor's info (the owner's
+                #                                 own check() also raises a preparation error)
             else:
-                comm.wait_stream(main)
+                comm_stream.wait_stream(main)
         ntr = E._point_count(x, spec.input_dim)   # every rank passes x with the job's point count
         npad, n = E.fit_layout(spec, ntr, variance)
-        with torch.cuda.stream(comm):
-            gp = broadcast_fit(gp, spec, noise, x, dev, src=owner, error=err, layout=(n, ntr, npad))
+        with torch.cuda.stream(comm_stream):
+            gp = broadcast_fit(gp, spec, noise, x, dev, src=owner, error=err, layout=(n, ntr, npad),
+                               planes_only=float(noise + jitter) if variance == "ozaki" else None, comm=comm)
             if variance == "ozaki" and "ozaki" not in gp.extra:
                 E.ozaki_prepare(gp, diag_add=float(noise + jitter))   # a-priori moduli count
             ready = torch.cuda.Event()
-            ready.record(comm)
+            ready.record(comm_stream)
         return gp, ready
 
     refill()
@@ -549,7 +659,13 @@ def krige_jobs_sharded(jobs, variance: str = "ozaki", chunk: int = 8192, var_mod
     while window:
         idx, (spec, x, y, noise, xg) = window.popleft()
         gp, ready = cur
+        # this job's status (broadcast with its factor): raises on every rank, and applies the
+        # owner's accuracy-guard statistics on every rank (the same decision everywhere) before
+        # the predict is queued; the broadcast ran under the previous job's predict
+        gp.check()
+        E.note_guard(stats, gp)
         main.wait_event(ready)
+        gp.ready_on(main)
         gp.record_stream(main)
         if pred is None or not pred.fits(gp):
             pred = E.Predictor(gp, chunk)
@@ -559,7 +675,6 @@ def krige_jobs_sharded(jobs, variance: str = "ozaki", chunk: int = 8192, var_mod
         refill()
         # the next job's factor travels while this predict runs
         cur = receive(*window[0]) if window else None
-        gp.check()   # this job's status (broadcast with its factor): raises on every rank
         yield out
 
 

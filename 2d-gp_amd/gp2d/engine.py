@@ -12,6 +12,7 @@ Reference call sites replaced:
 from __future__ import annotations
 
 import collections
+import os
 import ctypes
 import itertools
 import time
@@ -41,22 +42,34 @@ def _require_device(device=None) -> torch.device:
     return torch.device(device if device is not None else "cuda")
 
 
-def morton_order(P: torch.Tensor) -> torch.Tensor:
-    """Permutation that sorts device points (N, d), d ∈ {2, 3}, along a Z-order (Morton) curve
-    of their bounding box (gp2d_morton_codes, 21 bits per coordinate; stable sort, so
-    deterministic).  The ozaki engine orders training and grid points this way so that 64
-    consecutive training points and 256 consecutive grid points are spatially compact: K*
-    tiles of far-apart groups are then exactly zero and the int8 GEMMs skip them
-    (csrc/ozaki.hpp, ozaki_slab_list_kernel)."""
+def morton_sort(P: torch.Tensor):
+    """(order, P[order]) for device points (N, d), d ∈ {2, 3}: the Z-order (Morton) curve of
+    their bounding box (21 bits per coordinate), sorted by a stable device radix sort and
+    gathered on the device (gp2d_morton_sort; equal codes keep their input order, so the
+    permutation is deterministic).  The ozaki engine orders training and grid points this way so
+    that 64 consecutive training points and 256 consecutive grid points are spatially compact:
+    K* tiles of far-apart groups are then exactly zero and the int8 GEMMs skip them
+    (csrc/ozaki.hpp, ozaki_slab_list_kernel).  Other shapes: (None, P) — no reordering."""
     n, d = P.shape
-    if n <= 1 or d not in (2, 3):
-        return torch.arange(n, device=P.device)
+    if n < 1 or d not in (2, 3):
+        return None, P
     P = P.contiguous()
-    scratch = torch.empty(6, dtype=torch.float64, device=P.device)
-    code = torch.empty(n, dtype=torch.int64, device=P.device)
-    N.check(N.lib().gp2d_morton_codes(_ptr(P), n, d, _ptr(scratch), _ptr(code), _stream_handle(P.device)),
-            "gp2d_morton_codes")
-    return torch.argsort(code, stable=True)
+    L = N.lib()
+    wb = int(L.gp2d_morton_sort_workspace(n))
+    work = torch.empty(wb, dtype=torch.uint8, device=P.device)
+    order = torch.empty(n, dtype=torch.int64, device=P.device)
+    out = torch.empty_like(P)
+    N.check(L.gp2d_morton_sort(_ptr(P), n, d, _ptr(out), _ptr(order), _ptr(work), wb, _stream_handle(P.device)),
+            "gp2d_morton_sort")
+    return order, out
+
+
+def morton_order(P: torch.Tensor) -> torch.Tensor:
+    """The permutation of morton_sort (sorted point j is P[order[j]])."""
+    order, _ = morton_sort(P)
+    if order is None:
+        raise ValueError("morton_order: points must be (N, 2) or (N, 3) with N ≥ 1")
+    return order
 
 
 def side_stream(device=None) -> torch.cuda.Stream:
@@ -174,18 +187,24 @@ class GPFit:
     extra: dict = field(default_factory=dict)
     y: torch.Tensor = None   # (n,) padded observations (LML)
     perm: torch.Tensor = None  # ozaki engine: x = x_input[perm] (Morton order; α, W follow x)
-    pending: tuple = None      # fit(check=False): (pinned info copy, its event, prepare error)
+    pending: tuple = None      # fit(check=False): (pinned status copy, its event, prepare error)
+    n_mat: int = 0             # matrix order when W is None (a job stream's receiving rank keeps
+    #                            only the INT8 planes, distributed.broadcast_fit)
 
     def check(self) -> "GPFit":
         """Raise what fit(check=False) deferred: LinAlgError for a non-SPD K_y (waits only
-        for the factor's info flag, not for later work on the stream)."""
+        for the factor's status word, not for later work on the stream), then apply the ozaki
+        engine's accuracy guard (apply_guard) with the statistics that travel in the same word.
+        Call it before the fit's predict is queued: the guard may re-prepare the planes."""
         if self.pending is not None:
-            info_host, ev, err = self.pending
+            host, ev, err = self.pending
             self.pending = None
             ev.synchronize()
-            inf = int(info_host.item())
-            _PINNED_INFO.append(info_host)
+            inf = int(host.view(torch.int32)[0].item())
+            vmin, wmax = float(host[1].item()), float(host[2].item())
+            _PINNED_STATUS.append(host)
             _raise_fit_errors(inf, err)
+            apply_guard(self, vmin, wmax)
         return self
 
     def record_stream(self, stream) -> "GPFit":
@@ -200,19 +219,31 @@ class GPFit:
 
     @property
     def n(self) -> int:
-        return self.W.shape[0]
+        return self.W.shape[0] if self.W is not None else self.n_mat
+
+    def ready_on(self, stream) -> "GPFit":
+        """Make `stream` wait for the work the accuracy guard queued in check() (re-prepared
+        planes, or W unpacked for the FP64 engine), if any."""
+        g = self.extra.get("guard")
+        ev = g.pop("event", None) if g else None
+        if ev is not None:
+            stream.wait_event(ev)
+        return self
 
 
-def _pad_obs(y, n_train: int, n_pad: int, bd: int, device) -> torch.Tensor:
+def _pad_obs(y, n_train: int, n_pad: int, bd: int, device, perm: torch.Tensor | None = None) -> torch.Tensor:
+    """The fit's observation vector [u(n_pad), v(n_pad)] with zeros for the padded points, in the
+    order of perm (sorted point i is input point perm[i]) — gp2d_obs_pad on the device."""
     if isinstance(y, torch.Tensor):
         yt = y.to(device=device, dtype=torch.float64).reshape(-1)
     else:
         yt = torch.as_tensor(np.asarray(y, dtype=np.float64).reshape(-1), device=device)
     if yt.numel() != bd * n_train:
         raise ValueError(f"observation vector has {yt.numel()} entries, expected {bd * n_train}")
-    out = torch.zeros(bd * n_pad, dtype=torch.float64, device=device)
-    for c in range(bd):
-        out[c * n_pad:c * n_pad + n_train] = yt[c * n_train:(c + 1) * n_train]
+    yt = yt.contiguous()
+    out = torch.empty(bd * n_pad, dtype=torch.float64, device=device)
+    N.check(N.lib().gp2d_obs_pad(_ptr(yt), n_train, n_pad, bd, None if perm is None else _ptr(perm), _ptr(out),
+                                 _stream_handle(device)), "gp2d_obs_pad")
     return out
 
 
@@ -240,9 +271,19 @@ def fit_layout(kernel: KernelSpec, n_train: int, variance: str = "f64"):
     return npad, n
 
 
-# pinned 1-int slots for fit(check=False)'s info copies, reused after GPFit.check(), so the
-# steady state allocates no pinned memory
-_PINNED_INFO: list = []
+# pinned 3-double status slots for fit(check=False) (see status_block), reused after
+# GPFit.check(), so the steady state allocates no pinned memory
+_PINNED_STATUS: list = []
+
+
+def status_block(device) -> tuple:
+    """A fit's device status word: 3 doubles — [0] holds the LAPACK-style info as an int32 in its
+    low bytes (gp2d_potrf writes it there through the returned int32 view), [1:3] the accuracy
+    guard's statistics (gp2d_ozaki_guard: min latent variance at the observations, max |W|;
+    undefined, and never read, when no guard ran).  One copy to the host (or one broadcast)
+    carries all of it."""
+    st = torch.empty(3, dtype=torch.float64, device=device)
+    return st, st.view(torch.int32)[0:1]
 
 
 def _raise_fit_errors(inf: int, err):
@@ -259,18 +300,91 @@ def _raise_fit_errors(inf: int, err):
 
 
 def pending_status(status: torch.Tensor, err=None) -> tuple:
-    """A GPFit.pending triple for a device status word (int32, LAPACK-style info; < 0: failed on
+    """A GPFit.pending triple for a device status block (status_block; info < 0: failed on
     another rank): copied to pinned host memory after the work queued so far on the current
     stream, checked by GPFit.check()."""
-    host = _PINNED_INFO.pop() if _PINNED_INFO else torch.empty(1, dtype=torch.int32, pin_memory=True)
+    host = _PINNED_STATUS.pop() if _PINNED_STATUS else torch.empty(3, dtype=torch.float64, pin_memory=True)
     host.copy_(status, non_blocking=True)
     ev = torch.cuda.Event()
     ev.record(torch.cuda.current_stream(status.device))
     return host, ev, err
 
 
+# The accuracy the guard holds the int8 variance to: north_star's fp64 posterior gate (1e-10
+# relative), elementwise.
+GUARD_TARGET = 1e-10
+OZAKI_DEFAULT_BITS = 49      # csrc/ozaki.hpp OZ_PW
+# fit(guard=None) default; GP2D_GUARD=0 turns the guard off (dev A/Bs only, tools/runs)
+GUARD_DEFAULT = os.environ.get("GP2D_GUARD", "1") != "0"
+
+
+def _guard_stats(W: torch.Tensor, n: int, ntr: int, npad: int, diag_add: float, status: torch.Tensor, dev):
+    """gp2d_ozaki_guard into status[1:3] (status_block) on the current stream."""
+    L = N.lib()
+    wb = int(L.gp2d_ozaki_guard_workspace(n))
+    work = torch.empty(wb, dtype=torch.uint8, device=dev)
+    N.check(L.gp2d_ozaki_guard(_ptr(W), n, W.stride(0), ntr, npad, float(diag_add),
+                               ctypes.c_void_p(status.data_ptr() + 8), _ptr(work), wb, _stream_handle(dev)),
+            "gp2d_ozaki_guard")
+
+
+def apply_guard(gp: GPFit, vmin: float, wmax: float) -> GPFit:
+    """The ozaki engine's accuracy guard, once the fit's statistics are on the
+    host: the variance's elementwise error grows as the posterior variance falls against kss,
+    ≈ K·2^(49 − bits)·(kss / v_min)^1.5 (gp2d_ozaki_error_model), with v_min the smallest latent
+    posterior variance at the observations (exact from W).  The W rows get the fewest bits in
+    49..60 that keep the model within GUARD_TARGET — planes re-prepared on the fit's stream when
+    that is more than the default — or, past 60 bits, the fit switches to the FP64 engine.
+    The decision is in gp.extra['guard']: engine, wbits, vmin_over_kss, wmax, est."""
+    g = gp.extra.get("guard")
+    if not g or not g.get("pending"):
+        return gp
+    L = N.lib()
+    kss = gp.kernel.kdiag()
+    bits = int(L.gp2d_ozaki_guard_bits(kss, vmin, GUARD_TARGET))
+    g.update(pending=False, vmin_over_kss=vmin / kss, wmax=wmax)
+    stream = g.pop("stream", None) or torch.cuda.current_stream(gp.device)
+    packed = gp.extra.pop("packed", None)
+    if bits <= 0:   # beyond the emulation's range (or a non-positive v_min): exact FP64 products
+        g.update(engine="f64", wbits=None, est=float(L.gp2d_ozaki_error_model(kss, vmin, 60)))
+        gp.extra.pop("ozaki", None)
+        if gp.W is None:   # a receiving rank kept only the packed payload
+            with torch.cuda.stream(stream):
+                W = torch.zeros((gp.n, gp.n), dtype=torch.float64, device=gp.device)
+                N.check(L.gp2d_pack_lower(_ptr(W), gp.n, gp.n, _ptr(packed), 1, _stream_handle(gp.device)),
+                        "gp2d_pack_lower")
+                g["event"] = torch.cuda.Event()
+                g["event"].record(stream)
+            gp.W = W
+        return gp
+    g.update(engine="ozaki", wbits=bits, est=float(L.gp2d_ozaki_error_model(kss, vmin, bits)))
+    if bits > OZAKI_DEFAULT_BITS:
+        with torch.cuda.stream(stream):
+            ozaki_prepare(gp, diag_add=g["diag_add"], wbits=bits, packed=packed)
+            gp.extra.pop("packed", None)
+            g["event"] = torch.cuda.Event()
+            g["event"].record(stream)
+    return gp
+
+
+def ozaki_prepare_guarded(gp: GPFit, diag_add: float, guard: bool = True) -> GPFit:
+    """The ozaki engine's planes for a fit whose W is already final (a loaded checkpoint, the
+    distributed factor): the accuracy guard's statistics read synchronously, then the planes at
+    the guard's precision (or none: the FP64 engine) — apply_guard without the deferred path."""
+    if not guard:
+        return ozaki_prepare(gp, diag_add=float(diag_add))
+    status, _ = status_block(gp.device)
+    _guard_stats(gp.W, gp.n, gp.n_train, gp.n_pad, diag_add, status, gp.device)
+    host = status.cpu()
+    gp.extra["guard"] = dict(pending=True, diag_add=float(diag_add), stream=torch.cuda.current_stream(gp.device))
+    apply_guard(gp, float(host[1]), float(host[2]))
+    if "ozaki" not in gp.extra and gp.extra["guard"]["engine"] == "ozaki":
+        ozaki_prepare(gp, diag_add=float(diag_add))
+    return gp.ready_on(torch.cuda.current_stream(gp.device))
+
+
 def fit(kernel: KernelSpec, x, y, noise: float, jitter: float = 0.0, device=None, variance: str = "f64",
-        check: bool = True, jitchol: int = 0, join: bool | None = None) -> GPFit:
+        check: bool = True, jitchol: int = 0, join: bool | None = None, guard: bool | None = None) -> GPFit:
     """K_y = K(x,x) + (noise+jitter)·I → L = chol(K_y) → W = L⁻¹ → α = Wᵀ W y.
 
     jitchol = k > 0: GPy's jitchol retry (GPy.util.linalg.jitchol, maxtries = k; GPy is not
@@ -282,6 +396,8 @@ def fit(kernel: KernelSpec, x, y, noise: float, jitter: float = 0.0, device=None
     variance: 'f64'   — predictive variance by the FP64-MFMA contraction;
               'ozaki' — the same contraction emulated exactly on the INT8 matrix cores
                         (Ozaki scheme II, csrc/ozaki.hpp); vector2d family only.
+    guard (ozaki): hold the emulated variance to GUARD_TARGET whatever the hyperparameters
+    (apply_guard: more W bits, or the FP64 engine); False keeps the default 49 bits.
     Raises numpy.linalg.LinAlgError if K_y is not positive definite (the
     reference's np.linalg.inv / GPy jitchol / sklearn error paths).  check=False returns
     without waiting for the factor (no host sync); the error is raised by GPFit.check().
@@ -331,15 +447,14 @@ def fit(kernel: KernelSpec, x, y, noise: float, jitter: float = 0.0, device=None
                          "use variance='f64'")
     perm = None
     if variance == "ozaki" and ntr > 1:   # Morton order: exact-zero K* slabs cluster (skipped)
-        perm = morton_order(X)
-        X = X[perm].contiguous()
+        perm, X = morton_sort(X)
     s = _stream_handle(dev)
     desc = kernel.desc()
     A = torch.empty((n, n), dtype=torch.float64, device=dev)
     N.check(L.gp2d_assemble(_ptr(X), ntr, npad, _ptr(X), ntr, npad, ctypes.byref(desc), float(noise + jitter), 1,
                             _ptr(A), n, s), "gp2d_assemble")
     dinv = torch.empty((n // NB, NB, NB), dtype=torch.float64, device=dev)
-    info = torch.zeros(1, dtype=torch.int32, device=dev)
+    status, info = status_block(dev)   # gp2d_potrf resets info
     prev_join = L.gp2d_factor_join(1 if (check if join is None else join) else 0)
     try:
         if FUSED_INVERSE:   # factor and inverse in one call, the TRTRI GEMMs overlapped with POTRF
@@ -356,43 +471,45 @@ def fit(kernel: KernelSpec, x, y, noise: float, jitter: float = 0.0, device=None
         work = torch.empty(wbytes // 8 + 1, dtype=torch.float64, device=dev)
         N.check(L.gp2d_trtri(_ptr(A), n, n, _ptr(dinv), _ptr(work), wbytes, s), "gp2d_trtri")
     del work, dinv
-    info_host = ev = None
+    guard = (GUARD_DEFAULT if guard is None else guard) and variance == "ozaki"
+    if guard:   # the guard's statistics from W, into the status word beside info
+        _guard_stats(A, n, ntr, npad, noise + jitter, status, dev)
+    pend = None
     if not check:
-        # α (and the ozaki preparation) are enqueued before `info` is read (one host sync per
-        # fit); a failed factor raises in GPFit.check()
-        info_host = _PINNED_INFO.pop() if _PINNED_INFO else torch.empty(1, dtype=torch.int32, pin_memory=True)
-        info_host.copy_(info, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(dev))
-    Y = _pad_obs(y, ntr, npad, bd, dev)
-    if perm is not None:
-        for c in range(bd):
-            Y[c * npad:c * npad + ntr] = Y[c * npad:c * npad + ntr][perm]
+        # α (and the ozaki preparation) are enqueued before the status is read (one host sync per
+        # fit); a failed factor raises in GPFit.check(), which also applies the guard
+        pend = pending_status(status)
+    Y = _pad_obs(y, ntr, npad, bd, dev, perm)
     alpha = torch.empty(n, dtype=torch.float64, device=dev)
     pbytes = int(L.gp2d_potrs_workspace(n))
     pwork = torch.empty(pbytes // 8 + 1, dtype=torch.float64, device=dev)
     N.check(L.gp2d_potrs_inv(_ptr(A), n, n, _ptr(Y), _ptr(alpha), _ptr(pwork), pbytes, s), "gp2d_potrs_inv")
     gp = GPFit(kernel=kernel, noise=float(noise), x=X, n_train=ntr, n_pad=npad, W=A, alpha=alpha, device=dev,
                y=Y, perm=perm)
-    gp.extra["info_dev"] = info   # the factor's status word on the device (the job stream broadcasts it)
+    gp.extra["status_dev"] = status   # info + guard statistics on the device (the job stream broadcasts it)
     del pwork
     err = None
     if variance == "ozaki":
-        # enqueued before `info` is read, with the a-priori moduli count: the fit's only host
-        # round trip is the info read below
+        # enqueued before the status is read, with the a-priori moduli count at the default
+        # precision: the fit's only host round trip is the status read below
+        if guard:
+            gp.extra["guard"] = dict(pending=True, diag_add=float(noise + jitter),
+                                     stream=torch.cuda.current_stream(dev))
         try:
             ozaki_prepare(gp, diag_add=float(noise + jitter))
         except N.GP2DError as e:   # a failed factor (NaN rows) makes prepare fail too: info decides
             err = e
     if not check:
-        gp.pending = (info_host, ev, err)
+        gp.pending = (pend[0], pend[1], err)
         return gp
-    _raise_fit_errors(int(info.item()), err)
+    host = status.cpu()
+    _raise_fit_errors(int(host.view(torch.int32)[0].item()), err)
+    apply_guard(gp, float(host[1]), float(host[2]))
     return gp
 
 
 def fit_batch(problems, variance: str = "f64", jitter: float = 0.0, device=None, check: bool = True,
-              join: bool | None = None) -> list:
+              join: bool | None = None, guard: bool | None = None) -> list:
     """Fit several GPs of one size together: `problems` is a sequence of (kernel, x, y, noise)
     whose matrices K_y share the order n (a hyperparameter sweep's settings over one training
     set, or a job stream's next jobs with equal point counts).  Their K_y are factored and
@@ -401,7 +518,7 @@ def fit_batch(problems, variance: str = "f64", jitter: float = 0.0, device=None,
     batch instead of once per fit; each problem's W, α (and INT8 residue planes) are those of
     engine.fit on it alone, bit for bit.  Returns one GPFit per problem (W views into one
     (B, n, n) tensor).  check=True raises LinAlgError for the first non-PD problem (the index
-    is in the message); check=False defers it to each GPFit.check().  join as in fit()."""
+    is in the message); check=False defers it to each GPFit.check().  join, guard as in fit()."""
     if variance not in VARIANCE_ENGINES:
         raise ValueError(f"variance must be one of {VARIANCE_ENGINES}")
     probs = list(problems)
@@ -423,8 +540,7 @@ def fit_batch(problems, variance: str = "f64", jitter: float = 0.0, device=None,
         npad, n = fit_layout(kernel, ntr, variance)
         perm = None
         if variance == "ozaki" and ntr > 1:
-            perm = morton_order(X)
-            X = X[perm].contiguous()
+            perm, X = morton_sort(X)
         prep.append((kernel, X, y, float(noise), ntr, npad, n, perm))
     n = prep[0][6]
     if any(p[6] != n for p in prep):
@@ -437,7 +553,7 @@ def fit_batch(problems, variance: str = "f64", jitter: float = 0.0, device=None,
         N.check(L.gp2d_assemble(_ptr(X), ntr, npad, _ptr(X), ntr, npad, ctypes.byref(kernel.desc()),
                                 float(noise + jitter), 1, _ptr(A[b]), n, s), "gp2d_assemble")
     dinv = torch.empty((B, n // NB, NB, NB), dtype=torch.float64, device=dev)
-    info = torch.zeros(B, dtype=torch.int32, device=dev)
+    info = torch.empty(B, dtype=torch.int32, device=dev)   # gp2d_potrf_batched resets them
     prev_join = L.gp2d_factor_join(1 if (check if join is None else join) else 0)
     try:
         N.check(L.gp2d_potrf_batched(_ptr(A), n, n, n * n, B, _ptr(dinv), _ptr(info), s), "gp2d_potrf_batched")
@@ -449,59 +565,77 @@ def fit_batch(problems, variance: str = "f64", jitter: float = 0.0, device=None,
     del work, dinv
     pbytes = int(L.gp2d_potrs_workspace(n))
     pwork = torch.empty(pbytes // 8 + 1, dtype=torch.float64, device=dev)
+    guard = (GUARD_DEFAULT if guard is None else guard) and variance == "ozaki"
+    statuses = torch.empty((B, 3), dtype=torch.float64, device=dev)   # status_block per problem
     fits, errs = [], []
     for b, (kernel, X, y, noise, ntr, npad, _, perm) in enumerate(prep):
+        statuses[b].view(torch.int32)[0:1].copy_(info[b:b + 1])        # a 4-byte device copy
+        if guard:
+            _guard_stats(A[b], n, ntr, npad, noise + jitter, statuses[b], dev)
         bd = kernel.block_dim
-        Y = _pad_obs(y, ntr, npad, bd, dev)
-        if perm is not None:
-            for c in range(bd):
-                Y[c * npad:c * npad + ntr] = Y[c * npad:c * npad + ntr][perm]
+        Y = _pad_obs(y, ntr, npad, bd, dev, perm)
         alpha = torch.empty(n, dtype=torch.float64, device=dev)
         W = A[b]
         N.check(L.gp2d_potrs_inv(_ptr(W), n, n, _ptr(Y), _ptr(alpha), _ptr(pwork), pbytes, s), "gp2d_potrs_inv")
         gp = GPFit(kernel=kernel, noise=noise, x=X, n_train=ntr, n_pad=npad, W=W, alpha=alpha, device=dev, y=Y,
                    perm=perm)
-        gp.extra["info_dev"] = info[b:b + 1]
+        gp.extra["status_dev"] = statuses[b]
         err = None
         if variance == "ozaki":
+            if guard:
+                gp.extra["guard"] = dict(pending=True, diag_add=float(noise + jitter),
+                                         stream=torch.cuda.current_stream(dev))
             try:
                 ozaki_prepare(gp, diag_add=float(noise + jitter))
             except N.GP2DError as e:
                 err = e
         if not check:
-            gp.pending = pending_status(info[b:b + 1], err)
+            gp.pending = pending_status(statuses[b], err)
         fits.append(gp)
         errs.append(err)
     del pwork
     if check:
-        infos = info.cpu().tolist()
-        for b, (inf, err) in enumerate(zip(infos, errs)):
+        host = statuses.cpu()
+        for b, err in enumerate(errs):
             try:
-                _raise_fit_errors(int(inf), err)
+                _raise_fit_errors(int(host[b].view(torch.int32)[0].item()), err)
             except np.linalg.LinAlgError as e:
                 raise np.linalg.LinAlgError(f"problem {b}: {e}") from None
+        for b, gp in enumerate(fits):
+            apply_guard(gp, float(host[b, 1]), float(host[b, 2]))
     return fits
 
 
-def ozaki_prepare(gp: GPFit, diag_add: float | None = None) -> GPFit:
+def ozaki_prepare(gp: GPFit, diag_add: float | None = None, packed: torch.Tensor | None = None,
+                  wbits: int = 0) -> GPFit:
     """Residue planes of W for the INT8 variance engine (once per fit).  With `diag_add`
     (the noise + jitter of K_y's diagonal) the moduli count is the a-priori bound and nothing
     synchronises (gp2d_ozaki_prepare_async); without it, the data-driven count of the
-    factor's row bounds (one device → host read)."""
+    factor's row bounds (one device → host read).  packed: W as the factor broadcast's packed
+    lower block triangle (gp2d_ozaki_prepare_packed, needs diag_add) — gp.W may then be None.
+    wbits: integer bits per W row (0 = the default 49; the accuracy guard's choice, apply_guard)."""
     L = N.lib()
     n = gp.n
     wres = torch.empty(int(L.gp2d_ozaki_wres_bytes(n)), dtype=torch.int8, device=gp.device)
     rowscale = torch.empty(n, dtype=torch.float64, device=gp.device)
     desc = gp.kernel.desc()
     nmod = ctypes.c_int(0)
-    if diag_add is not None:
-        N.check(L.gp2d_ozaki_prepare_async(_ptr(gp.W), n, n, ctypes.byref(desc), float(diag_add), _ptr(wres),
-                                           _ptr(rowscale), ctypes.byref(nmod), _stream_handle(gp.device)),
-                "gp2d_ozaki_prepare_async")
+    if packed is not None:
+        if diag_add is None:
+            raise ValueError("ozaki_prepare from the packed factor needs diag_add (the a-priori moduli count)")
+        N.check(L.gp2d_ozaki_prepare_packed(_ptr(packed), n, ctypes.byref(desc), float(diag_add), int(wbits),
+                                            _ptr(wres), _ptr(rowscale), ctypes.byref(nmod),
+                                            _stream_handle(gp.device)), "gp2d_ozaki_prepare_packed")
+    elif diag_add is not None:
+        N.check(L.gp2d_ozaki_prepare_async(_ptr(gp.W), n, n, ctypes.byref(desc), float(diag_add), int(wbits),
+                                           _ptr(wres), _ptr(rowscale), ctypes.byref(nmod),
+                                           _stream_handle(gp.device)), "gp2d_ozaki_prepare_async")
     else:
-        N.check(L.gp2d_ozaki_prepare(_ptr(gp.W), n, n, ctypes.byref(desc), _ptr(wres), _ptr(rowscale),
+        N.check(L.gp2d_ozaki_prepare(_ptr(gp.W), n, n, ctypes.byref(desc), int(wbits), _ptr(wres), _ptr(rowscale),
                                      ctypes.byref(nmod), _stream_handle(gp.device)), "gp2d_ozaki_prepare")
     gp.extra["ozaki"] = (wres, rowscale, int(nmod.value))
+    if packed is not None:
+        gp.extra["packed"] = packed   # kept until the guard has decided (it may need more bits, or W)
     return gp
 
 
@@ -535,15 +669,14 @@ def kstar_planes(kernel: KernelSpec, x, xg, noise: float, jitter: float = 0.0, c
     L = N.lib()
     d = kernel.input_dim
     X = _as_points(x, d, dev)
-    X = X[morton_order(X)].contiguous()          # the order fit() gives the training points
-    G = _as_points(xg, d, dev)
-    order = morton_order(G)
-    G = G[order].contiguous()
+    if X.shape[0] > 1:
+        X = morton_sort(X)[1]                     # the order fit() gives the training points
+    order, G = morton_sort(_as_points(xg, d, dev))
     ntr, m = X.shape[0], G.shape[0]
     npad, n = fit_layout(kernel, ntr, "ozaki")
     chunk = max(128, (int(chunk) + 127) // 128 * 128)
     desc = kernel.desc()
-    nmod = int(L.gp2d_ozaki_nmod_apriori(n, ctypes.byref(desc), float(noise + jitter)))
+    nmod = int(L.gp2d_ozaki_nmod_apriori(n, ctypes.byref(desc), float(noise + jitter), 0))
     if nmod <= 0:
         N.check(-1, "gp2d_ozaki_nmod_apriori")
     nbytes = int(L.gp2d_ozaki_kstar_bytes(n, m, chunk, nmod))
@@ -613,19 +746,21 @@ class Predictor:
         self.work = torch.empty(self.wbytes // 8 + 1, dtype=torch.float64, device=gp.device)
         self._grid = None   # (the caller's grid tensor, its version, Morton order, the grid in that order)
 
-    def _grid_order(self, xg, G: torch.Tensor):
-        """Morton order of the grid and the grid in that order.  A job stream predicts the same
-        device grid job after job (the reference's per-window krig.predict on one grid): for the
-        same tensor object, unmodified since (its version counter), the order of the previous call
-        is reused — the tensor is held, so its memory cannot be reused by another grid."""
+    def _grid_order(self, xg, G: torch.Tensor, reuse: bool):
+        """Morton order of the grid and the grid in that order.  reuse=True (a job stream predicting
+        one device grid job after job — the reference's per-window krig.predict on one grid): for the
+        same tensor, at the same address and unmodified by version-tracked ops since (its version
+        counter), the order of the previous call is reused — the tensor is held, so its memory cannot
+        be handed to another grid.  Writes that bypass the version counter (DLPack aliases, raw
+        data_ptr kernels) are not seen: callers that modify a grid that way must not ask for reuse."""
         c = self._grid
         st = torch.cuda.current_stream(G.device)
-        if isinstance(xg, torch.Tensor) and c is not None and c[0] is xg and c[1] == xg._version \
-                and c[3].shape == G.shape and c[4] == st:   # made on this stream: ordered before
+        if reuse and isinstance(xg, torch.Tensor) and c is not None and c[0] is xg and c[1] == xg._version \
+                and c[5] == xg.data_ptr() and c[3].shape == G.shape and c[4] == st:   # made on this stream
             return c[2], c[3]
-        order = morton_order(G)
-        Gs = G[order].contiguous()
-        self._grid = (xg, xg._version, order, Gs, st) if isinstance(xg, torch.Tensor) and xg.is_cuda else None
+        order, Gs = morton_sort(G)
+        self._grid = (xg, xg._version, order, Gs, st, xg.data_ptr()) \
+            if reuse and isinstance(xg, torch.Tensor) and xg.is_cuda else None
         return order, Gs
 
     def fits(self, gp: GPFit) -> bool:
@@ -635,9 +770,10 @@ class Predictor:
                 and self.gp.kernel.block_dim == gp.kernel.block_dim)
 
     def __call__(self, xg, var_mode: str = "latent", compute_var: bool = True, out=None,
-                 planes: KstarPlanes | None = None):
+                 planes: KstarPlanes | None = None, reuse_grid: bool = False):
         """planes: K* residue planes of this same grid from kstar_planes() (ozaki engine):
-        the variance GEMMs read them and the K* kernel runs mean-only (same results as without)."""
+        the variance GEMMs read them and the K* kernel runs mean-only (same results as without).
+        reuse_grid: the grid is the one of the previous call, unmodified (_grid_order)."""
         gp = self.gp
         L = N.lib()
         d, bd = gp.kernel.input_dim, gp.kernel.block_dim
@@ -656,16 +792,14 @@ class Predictor:
                 raise ValueError("K* planes were made for another grid, fit layout or chunk size")
             # the variance runs on the grid in Morton order (zero K* tiles cluster and are
             # skipped); every output point is independent of the others, so reordering
-            # changes no bits — the results are scattered back to the input order
-            order = None
-            Gs, ms, vs = G, mean, var
+            # changes no bits — the epilogue stores each result at its input position
+            order, Gs = None, G
             if compute_var and m > 1:
                 if use_planes:
                     order, Gs = planes.order, planes.xg
                 else:
-                    order, Gs = self._grid_order(xg, G)
-                ms = torch.empty(bd * m, dtype=torch.float64, device=gp.device)
-                vs = torch.empty(bd * m, dtype=torch.float64, device=gp.device)
+                    order, Gs = self._grid_order(xg, G, reuse_grid)
+            po = None if order is None else _ptr(order)
             rc = -3
             if use_planes:
                 s = torch.cuda.current_stream(gp.device)
@@ -673,7 +807,7 @@ class Predictor:
                 rc = L.gp2d_predict_ozaki_planes(_ptr(wres), _ptr(rowscale), nmod, gp.n, _ptr(gp.alpha), _ptr(gp.x),
                                                  gp.n_train, gp.n_pad, _ptr(Gs), m, ctypes.byref(desc),
                                                  _VAR_MODES[var_mode], float(gp.noise), _ptr(planes.bres),
-                                                 planes.nmod, _ptr(ms), _ptr(vs), self.chunk, _ptr(self.work),
+                                                 planes.nmod, _ptr(mean), _ptr(var), po, self.chunk, _ptr(self.work),
                                                  self.wbytes, ctypes.c_void_p(s.cuda_stream))
                 if rc != -3:   # −3: the fit needs more moduli than the planes carry → inline K*
                     N.check(rc, "gp2d_predict_ozaki_planes")
@@ -681,11 +815,8 @@ class Predictor:
                 N.check(L.gp2d_predict_ozaki(_ptr(wres), _ptr(rowscale), nmod, gp.n, _ptr(gp.alpha), _ptr(gp.x),
                                              gp.n_train, gp.n_pad, _ptr(Gs), m, ctypes.byref(desc),
                                              _VAR_MODES[var_mode], float(gp.noise), int(bool(compute_var)),
-                                             _ptr(ms), _ptr(vs), self.chunk, _ptr(self.work), self.wbytes,
+                                             _ptr(mean), _ptr(var), po, self.chunk, _ptr(self.work), self.wbytes,
                                              _stream_handle(gp.device)), "gp2d_predict_ozaki")
-            if order is not None:
-                mean.view(bd, m)[:, order] = ms.view(bd, m)
-                var.view(bd, m)[:, order] = vs.view(bd, m)
             return mean, (var if compute_var else None)
         N.check(L.gp2d_predict(_ptr(gp.W), gp.n, gp.n, _ptr(gp.alpha), _ptr(gp.x), gp.n_train, gp.n_pad,
                                _ptr(G), m, ctypes.byref(desc), _VAR_MODES[var_mode], float(gp.noise),
@@ -696,6 +827,15 @@ class Predictor:
 
 def predict(gp: GPFit, xg, var_mode: str = "latent", compute_var: bool = True, chunk: int = 8192):
     return Predictor(gp, chunk)(xg, var_mode=var_mode, compute_var=compute_var)
+
+
+def note_guard(stats: dict | None, gp: GPFit):
+    """Record a checked fit's accuracy-guard decision in a job stream's `stats` (stats['guard'],
+    one dict per job in job order: engine, wbits, vmin_over_kss, wmax, est)."""
+    if stats is not None:
+        g = gp.extra.get("guard")
+        stats.setdefault("guard", []).append(
+            {k: v for k, v in g.items() if k in ("engine", "wbits", "vmin_over_kss", "wmax", "est")} if g else None)
 
 
 def note_fit_issued(stats: dict | None):
@@ -802,6 +942,12 @@ def krige_jobs(jobs, variance: str = "ozaki", chunk: int = 8192, var_mode: str =
             if k > 1:
                 fill(k)   # before the predict stream waits for the head job's fit
             job, side, gp = queue.popleft()
+            # this job's status (LinAlgError, the accuracy guard — which may re-prepare the
+            # planes on `side`) before its predict is queued; the host waits for this fit only,
+            # which ran under the previous job's predict, so the GPU never waits for the host
+            with torch.cuda.stream(side):
+                gp.check()
+            note_guard(stats, gp)
             main.wait_stream(side)
             gp.record_stream(main)
             if k == 1:
@@ -809,8 +955,7 @@ def krige_jobs(jobs, variance: str = "ozaki", chunk: int = 8192, var_mode: str =
             if pred is None or not pred.fits(gp):
                 pred = Predictor(gp, chunk)
             pred.gp = gp
-            out = pred(job[4], var_mode=var_mode, compute_var=compute_var)
-            gp.check()
+            out = pred(job[4], var_mode=var_mode, compute_var=compute_var, reuse_grid=True)
             yield out
     finally:
         if prev_sets is not None:
@@ -930,14 +1075,19 @@ def _krige_jobs_batched(jobs, b, variance, chunk, var_mode, compute_var, jitter,
                 gp.record_stream(main)
         nxt, nfits = None, None
         for q, (job, gp) in enumerate(zip(group, fits)):
+            with torch.cuda.stream(side if side is not None else main):
+                gp.check()   # status + accuracy guard before the predict (planes re-prepared there)
+            note_guard(stats, gp)
+            if side is not None:
+                gp.ready_on(main)   # only the guard's own work: `side` may carry the next batch's fit
+                gp.record_stream(main)
             if pred is None or not pred.fits(gp):
                 pred = Predictor(gp, chunk)
             pred.gp = gp
-            out = pred(job[4], var_mode=var_mode, compute_var=compute_var)
+            out = pred(job[4], var_mode=var_mode, compute_var=compute_var, reuse_grid=True)
             if q == 0 and side is not None:   # the next batch's fit under this batch's predicts
                 nxt = next(groups, None)
                 nfits = issue(nxt, False) if nxt else None
-            gp.check()
             yield out
         if side is None:
             nxt = next(groups, None)
@@ -951,11 +1101,12 @@ def _krige_jobs_serial(jobs, variance, chunk, var_mode, compute_var, jitter, dev
         kernel, x, y, noise, xg = job
         note_fit_issued(stats)
         gp = fit(kernel, x, y, noise, jitter=jitter, device=dev, variance=variance, check=False)
+        gp.check()   # status + accuracy guard before the predict
+        note_guard(stats, gp)
         if pred is None or not pred.fits(gp):
             pred = Predictor(gp, chunk)
         pred.gp = gp
-        out = pred(xg, var_mode=var_mode, compute_var=compute_var)
-        gp.check()
+        out = pred(xg, var_mode=var_mode, compute_var=compute_var, reuse_grid=True)
         yield out
 
 
@@ -1096,7 +1247,7 @@ def spd_inverse(K, device=None, return_factor: bool = False):
     A[:n0, :n0] = K
     s = _stream_handle(dev)
     dinv = torch.empty((n // NB, NB, NB), dtype=torch.float64, device=dev)
-    info = torch.zeros(1, dtype=torch.int32, device=dev)
+    info = torch.empty(1, dtype=torch.int32, device=dev)
     N.check(L.gp2d_potrf(_ptr(A), n, n, _ptr(dinv), _ptr(info), None, 0, s), "gp2d_potrf")
     wbytes = int(L.gp2d_trtri_workspace(n))
     work = torch.empty(wbytes // 8 + 1, dtype=torch.float64, device=dev)

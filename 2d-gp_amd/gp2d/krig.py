@@ -79,13 +79,18 @@ class Krig:
     (incl. family='ard' for the sklearn model of krig.scikit_prior).
     var_mode: 'latent' (GP_laser.py:128-131), 'gpy' (+noise, GPy model.predict),
     'sklearn' (+noise, clipped at 0, _gpr.py:473-485).
+    variance: None (default) — the int8 Ozaki-II engine held to the 1e-10 gate by its accuracy
+    guard for the vector kernels (engine.apply_guard: more W bits, or FP64 past its range), the
+    FP64 engine for the ARD family; 'ozaki' / 'f64' force one.
     """
 
     def __init__(self, kernel="df", l_df: float = 5.0, l_cf: float = 5.0, ratio: float = None,
                  noise: float = 0.0025, jitter: float = 0.0, var_mode: str = "latent", device=None,
-                 chunk: int = 8192, variance: str = "f64", jitchol: int = 0):
+                 chunk: int = 8192, variance: str | None = None, jitchol: int = 0):
         self.spec = self._make_spec(kernel, l_df, l_cf, ratio)
         self.jitchol = int(jitchol)   # GPy jitchol retries on a non-PD K_y (engine.fit)
+        if variance is None:   # the int8 engine under its accuracy guard where it applies (vector kernels)
+            variance = "ozaki" if self.spec.is_vector else "f64"
         if variance not in E.VARIANCE_ENGINES:
             raise ValueError(f"variance must be one of {E.VARIANCE_ENGINES}")
         self.variance = variance
@@ -256,17 +261,17 @@ class Krig:
         pm = None
         if perm is not None:
             pm = torch.as_tensor(np.asarray(perm, dtype=np.int64), device=dev)
-            Xd = Xd[pm].contiguous()
-        Y = E._pad_obs(y, ntr, npad, bd, dev)
-        if pm is not None:
-            for c in range(bd):
-                Y[c * npad:c * npad + ntr] = Y[c * npad:c * npad + ntr][pm]
+            Xs = torch.empty_like(Xd)
+            E.N.check(E.N.lib().gp2d_gather_rows(E._ptr(Xd), E._ptr(pm), ntr, Xd.shape[1], E._ptr(Xs),
+                                                 E._stream_handle(dev)), "gp2d_gather_rows")
+            Xd = Xs
+        Y = E._pad_obs(y, ntr, npad, bd, dev, pm)
         gp = E.GPFit(kernel=spec, noise=self.noise, x=Xd, n_train=ntr, n_pad=npad,
                      W=torch.as_tensor(np.ascontiguousarray(W), device=dev),
                      alpha=torch.as_tensor(np.ascontiguousarray(alpha), device=dev), device=dev, y=Y, perm=pm)
         gp.extra["jitchol"] = float(jitchol_used)
         if self.variance == "ozaki":
-            E.ozaki_prepare(gp, diag_add=float(self.noise + (self.jitter + jitchol_used)))
+            E.ozaki_prepare_guarded(gp, float(self.noise + (self.jitter + jitchol_used)))
         self.gp = gp
         self._pred = E.Predictor(gp, self.chunk)
         self._X, self._y = X, y

@@ -111,6 +111,10 @@ def parse():
                          "library's hyper.auto_batch)")
     ap.add_argument("--single-job-dist", type=int, default=0,
                     help="also time one job with distributed.fit_distributed at N = 1 (always at N > 1)")
+    ap.add_argument("--f64-steps", type=int, default=5,
+                    help="N = 1: also time this many jobs of the same stream on the strict FP64 engine (f64_value)")
+    ap.add_argument("--dropin-steps", type=int, default=3,
+                    help="N = 1: also time this many krig.Krig(...).fit(...).predict_device(grid) jobs (dropin)")
     a = ap.parse_args()
     if a.config == "B":
         a.kind, a.ntrain, a.grid = "df", 1024, 128
@@ -295,6 +299,23 @@ def run_sweep(args, ws, rank, dev):
         dist.destroy_process_group()
 
 
+def comm_block(comm: dict, keys, per: int, ws: int, dev) -> dict:
+    """The `comm` block of the N > 1 line: per collective kind, the HIP-event-timed milliseconds
+    and the payload bytes this rank sent / received (distributed._timed), divided by `per` jobs,
+    each the MAX over the ranks (all-reduce; every rank calls this)."""
+    from gp2d import distributed as GD
+    summ = GD.comm_summary(comm)
+    vals = torch.tensor([[summ.get(k, {}).get(f, 0) for f in ("ms", "bytes_sent", "bytes_recv", "calls")]
+                         for k in keys], dtype=torch.float64, device=dev)
+    if is_multi(ws):
+        dist.all_reduce(vals, op=dist.ReduceOp.MAX)
+    out = {}
+    for k, (ms, sent, recv, calls) in zip(keys, vals.tolist()):
+        out[k] = {"ms_per_job_max_over_ranks": ms / per, "bytes_sent_per_job_max": sent / per,
+                  "bytes_recv_per_job_max": recv / per, "calls_per_job": calls / per}
+    return out
+
+
 def single_job_distributed(args, ws, spec, xt, yt, noise, xg, m_all, dev, pred_cache, mean, var, reps):
     """One job with its FIT spread over the ranks too (distributed.fit_distributed: block-cyclic
     POTRF + TRTRI, panel broadcasts, W all-gathered), then each rank's grid shard predicted —
@@ -314,11 +335,13 @@ def single_job_distributed(args, ws, spec, xt, yt, noise, xg, m_all, dev, pred_c
 
     job()
     barrier(ws)
+    comm = {}
     tf = time.perf_counter()
-    gp = GD.fit_distributed(spec, xt, yt, noise, dev, variance=args.variance)
+    gp = GD.fit_distributed(spec, xt, yt, noise, dev, variance=args.variance, comm=comm)
     barrier(ws)
     fit_s = time.perf_counter() - tf
     del gp
+    cblock = comm_block(comm, ("panel_bcast", "w_allgather", "alpha_allgather"), 1, ws, dev)
     ts = time.perf_counter()
     for _ in range(reps):
         job()
@@ -329,7 +352,68 @@ def single_job_distributed(args, ws, spec, xt, yt, noise, xg, m_all, dev, pred_c
     ms = 1e3 * float(dts[0].item()) / reps
     return {"ms": ms, "value": m_all / (ms * 1e-3), "reps": reps, "fit_ms": 1e3 * float(dts[1].item()),
             "fit": f"distributed.fit_distributed over {ws} rank(s): 512-column block-cyclic POTRF + TRTRI, "
-                   "panel broadcasts, W columns all-gathered"}
+                   "panel broadcasts, W columns all-gathered",
+            "comm": cblock}
+
+
+def extra_readings_n1(args, spec, xt, yt, noise, xg, m_all):
+    """N = 1 readings beside the headline, each timed on its own:
+    * f64_value: the same job stream (engine.krige_jobs) with the strict FP64 variance engine;
+    * dropin: the reference-shaped surface — krig.Krig(...).fit(X, obs) then predict_device(grid)
+      (krig.py:471-574 / GP_plots.py:760-768), the variance engine its accuracy guard picks."""
+    from gp2d import engine as E
+    from gp2d import krig as K
+    out = {}
+    if args.f64_steps > 0:
+        job = (spec, xt, yt, noise, xg)
+        for _ in E.krige_jobs(itertools.repeat(job, 1), variance="f64", chunk=args.chunk):
+            pass
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in E.krige_jobs(itertools.repeat(job, args.f64_steps), variance="f64", chunk=args.chunk):
+            pass
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        out["f64_value"] = m_all * args.f64_steps / dt
+        out["f64"] = {"value": m_all * args.f64_steps / dt, "ms_per_step": 1e3 * dt / args.f64_steps,
+                      "steps": args.f64_steps, "api": "engine.krige_jobs(variance='f64')"}
+    if args.dropin_steps > 0:
+        def one():
+            k = K.Krig(spec.kind, l_df=spec.l_df, l_cf=spec.l_cf, ratio=spec.ratio, noise=noise).fit(xt, yt)
+            mu, var = k.predict_device(xg)
+            return k, mu, var
+        k, _, _ = one()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.dropin_steps):
+            k, _, _ = one()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        g = k.gp.extra.get("guard") or {}
+        out["dropin"] = {"value": m_all * args.dropin_steps / dt, "ms_per_step": 1e3 * dt / args.dropin_steps,
+                         "steps": args.dropin_steps,
+                         "api": "krig.Krig(kind, l_df, noise).fit(X, obs).predict_device(grid)",
+                         "variance_engine": k.variance if k.variance == "f64" else g.get("engine", "ozaki"),
+                         "guard_wbits": g.get("wbits")}
+    return out
+
+
+def job_stream_shape(args, spec, m, api) -> dict:
+    """fits_ahead / batch_fits / batch_ahead exactly as engine.krige_jobs resolved them for this
+    job shape (None off the engine.krige_jobs path): a batch is used only with fits_ahead = 0, and
+    batch_ahead only for a batch of more than one fit."""
+    from gp2d import engine as E
+    if api != "engine.krige_jobs":
+        return {"fits_ahead": None, "batch_fits": None, "batch_ahead": None}
+    fa = E.auto_fits_ahead(spec, args.ntrain, m, args.variance) if args.fits_ahead is None else args.fits_ahead
+    if fa > 0:
+        return {"fits_ahead": fa, "batch_fits": 1, "batch_ahead": False}
+    bf = E.auto_fit_batch(spec, args.ntrain, args.variance) if args.batch_fits is None else args.batch_fits
+    if bf <= 1:
+        return {"fits_ahead": fa, "batch_fits": 1, "batch_ahead": False}
+    ba = bool(args.batch_ahead) if args.batch_ahead is not None else \
+        E.auto_batch_ahead(spec, args.ntrain, m, bf, args.variance)
+    return {"fits_ahead": fa, "batch_fits": bf, "batch_ahead": ba}
 
 
 def main():
@@ -381,12 +465,7 @@ def main():
         cfg["ahead"] = args.variance == "ozaki" and (a == 1 or (a == -1 and is_multi(ws) and mode == "bcast"))
 
     stats = {}      # fits issued (engine.note_fit_issued): every timed job's fit must be issued after t0
-    last = [None]   # the previous step's fit: its non-SPD check runs one step late (no host sync)
-
-    def check_last():
-        if last[0] is not None:
-            last[0].check()
-            last[0] = None
+    comm = {} if is_multi(ws) else None   # the N > 1 line's `comm` block (distributed._timed)
 
     fit_stream = E.side_stream(dev)
     main_stream = torch.cuda.current_stream(dev)
@@ -411,14 +490,14 @@ def main():
             planes = E.kstar_planes(spec, xt, xg, noise, chunk=args.chunk, stream=side, out=pred_cache.get("k"))
             pred_cache["k"] = planes
         gp = do_fit()
+        gp.check()   # status + the accuracy guard before the predict (the guard may re-prepare)
+        gp.ready_on(main_stream)
         pr = pred_cache.get("p")
         if pr is None or not pr.fits(gp):
             pr = E.Predictor(gp, args.chunk)
             pred_cache["p"] = pr
         pr.gp = gp
         pr(xg, out=(mean, var), planes=planes)
-        check_last()   # waits for the previous fit's info flag only: this step is already queued
-        last[0] = gp
         return gp
 
     probe = {}
@@ -444,14 +523,12 @@ def main():
         cfg["pipeline"] = False
         for _ in range(args.warmup):
             step()
-        check_last()
         barrier(ws)
         E.timing_enable(True)
         E.timing_read()
         tu0 = time.perf_counter()
         for _ in range(args.unpipelined_steps):
             step()
-        check_last()
         barrier(ws)
         tu1 = time.perf_counter()
         ukms, uklaunch, ukflops = E.timing_read()
@@ -471,7 +548,7 @@ def main():
 
         def stream(k):
             return GD.krige_jobs_sharded(itertools.repeat(job, k), variance=args.variance, chunk=args.chunk,
-                                         stats=stats)
+                                         stats=stats, comm=comm)
         api = "distributed.krige_jobs_sharded"
     elif cfg["pipeline"] and cfg["mode"] in ("local", "replicate") and not cfg["ahead"]:
         job = (spec, xt, yt, noise, xg)
@@ -490,7 +567,6 @@ def main():
                 torch.cuda.synchronize()
                 print(f"[rank {rank}] step {i}: {1e3 * (time.perf_counter() - t_ref):.1f} ms since start",
                       file=sys.stderr, flush=True)
-        check_last()
 
     # round robin: at least one warmup job per rank, so every rank has fitted before the clock
     warm = max(args.warmup, ws) if cfg["mode"] == "rr" else args.warmup
@@ -499,6 +575,8 @@ def main():
     E.timing_enable(True)
     E.timing_read()
     stats.clear()
+    if comm is not None:
+        comm.clear()
     barrier(ws)
     t0 = time.perf_counter()
     run_jobs(args.steps, t0)
@@ -521,6 +599,13 @@ def main():
                   "expected": fits_expected, "warmup_jobs_run": warm}
     if timed_fits["issued_in_window"] != fits_expected or timed_fits["issued_total"] != fits_expected:
         raise RuntimeError(f"bench: timed region holds {timed_fits} fits, expected {fits_expected}")
+    guard = (stats.get("guard") or [None])[0]   # the accuracy guard's decision for the first timed job
+    comm_out = None
+    if cfg["mode"] == "rr" and comm is not None:
+        # every rank receives (or sends) every job's factor: bytes and HIP-event ms per job
+        comm_out = comm_block(comm, ("bcast",), args.steps, ws, dev)
+        comm_out["what"] = ("per timed job, MAX over ranks: the job's factor broadcast from its fitting rank (packed "
+                            "W + alpha + X_train + the status block), RCCL on the comm stream under the predict")
 
     # one job alone (unpipelined, its grid sharded over the ranks; at N > 1 fitted on rank 0 and
     # broadcast): the single-job reading beside the job-stream value
@@ -528,7 +613,7 @@ def main():
     barrier(ws)
     ts = time.perf_counter()
     for _ in range(reps):
-        run_jobs(1) if stream is not None else (step(), check_last())
+        run_jobs(1) if stream is not None else step()
     barrier(ws)
     dts = torch.tensor([time.perf_counter() - ts], dtype=torch.float64, device=dev)
     if is_multi(ws):
@@ -639,21 +724,17 @@ def main():
         "roofline": roof,
         "pipelined": cfg["pipeline"],
         "api": api,
-        "fits_ahead": (E.auto_fits_ahead(spec, args.ntrain, m, args.variance) if args.fits_ahead is None
-                       else args.fits_ahead) if api == "engine.krige_jobs" else None,
-        "batch_fits": ((E.auto_fit_batch(spec, args.ntrain, args.variance) if args.batch_fits is None
-                        else args.batch_fits) if (args.fits_ahead if args.fits_ahead is not None else
-                                                  E.auto_fits_ahead(spec, args.ntrain, m, args.variance)) <= 0
-                       else 1) if api == "engine.krige_jobs" else None,
-        "batch_ahead": (bool(args.batch_ahead) if args.batch_ahead is not None else
-                        E.auto_batch_ahead(spec, args.ntrain, m, E.auto_fit_batch(spec, args.ntrain, args.variance)
-                                           if args.batch_fits is None else args.batch_fits, args.variance))
-                       if api == "engine.krige_jobs" else None,
+        **job_stream_shape(args, spec, m, api),
         "unpipelined": unpiped,
         "single_job": single_job,
         "timed_fits": timed_fits,
         "mean_only_value": mean_only,
+        "guard": guard,
     }
+    if comm_out is not None:
+        out["comm"] = comm_out
+    if not is_multi(ws):
+        out.update(extra_readings_n1(args, spec, xt, yt, noise, xg, m_all))
     if not is_multi(ws) and (args.cpu_baseline > 0 or (args.cpu_baseline < 0 and args.ntrain <= 4096)):
         out["cpu_baseline"] = cpu_baseline(x, y, xg_all, args.kind, 5.0, noise, args.cpu_sample_points)
     print(json.dumps(out), flush=True)

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define GP2D_ABI_VERSION 8
+#define GP2D_ABI_VERSION 9
 
 /* kernel families */
 #define GP2D_FAMILY_VECTOR2D 0   /* 2×2 matrix-valued SE kernels on (x1, x2)          */
@@ -89,7 +89,8 @@ int gp2d_assemble(const double* xa, int64_t na, int64_t na_pad,
  * 128).  Replaces np.linalg.inv(K) (GP_laser.py:118, GP_scripts.py:50) and the
  * Cholesky inside GPy / sklearn (_gpr.py:349).  On return the strict upper
  * triangle is zero.  If dinv != NULL it receives the (n/128) inverted 128×128
- * diagonal blocks (input to gp2d_trtri).  *info_dev as LAPACK potrf.
+ * diagonal blocks (input to gp2d_trtri).  *info_dev as LAPACK potrf (the call resets it to
+ * 0 on `stream` first; the batched form resets all nprob words).
  * Concurrency: the factorisation runs on internal streams joined to `stream` at both
  * ends.  By default every call shares one set of internal streams per device;
  * gp2d_factor_sets(k) (k ≤ 4, returns the previous k) puts k sets in use — a caller
@@ -173,17 +174,44 @@ int gp2d_predict(const double* W, int64_t n, int64_t ldw, const double* alpha,
  * gp2d_ozaki_prepare: once per fit, W → residue planes wres (≤ gp2d_ozaki_wres_bytes(n)
  * bytes) and per-row scales rowscale (n doubles); *nmod_out receives the number of moduli
  * the data needs (from per-row L1 bounds of the scaled W; synchronises the stream once).
- * gp2d_ozaki_nmod(n) is the worst-case count used for sizing.                           */
+ * wbits: integer bits per scaled W row, 0 (the default, 49) or 49..60 (the accuracy guard's
+ * choice, gp2d_ozaki_guard_bits; more bits cost about one modulus per 8).
+ * gp2d_ozaki_nmod(n) is the worst-case count used for sizing (at 60 bits).              */
 int    gp2d_ozaki_nmod(int64_t n);
 size_t gp2d_ozaki_wres_bytes(int64_t n);
-int    gp2d_ozaki_prepare(const double* W, int64_t n, int64_t ldw, const gp2d_kernel_t* k,
+int    gp2d_ozaki_prepare(const double* W, int64_t n, int64_t ldw, const gp2d_kernel_t* k, int wbits,
                           int8_t* wres, double* rowscale, int* nmod_out, void* stream);
 /* gp2d_ozaki_prepare_async: as gp2d_ozaki_prepare without the host round trip — the moduli
- * count is gp2d_ozaki_nmod_apriori(n, k, diag_add) (diag_add = the noise + jitter on K_y's
+ * count is gp2d_ozaki_nmod_apriori(n, k, diag_add, wbits) (diag_add = the noise + jitter on K_y's
  * diagonal), which bounds the data-driven count for any fit of these hyperparameters.     */
 int    gp2d_ozaki_prepare_async(const double* W, int64_t n, int64_t ldw, const gp2d_kernel_t* k,
-                                double diag_add, int8_t* wres, double* rowscale, int* nmod_out,
+                                double diag_add, int wbits, int8_t* wres, double* rowscale, int* nmod_out,
                                 void* stream);
+/* gp2d_ozaki_prepare_packed: gp2d_ozaki_prepare_async reading W from the factor broadcast's
+ * payload (gp2d_pack_lower's packed lower block triangle, gp2d_pack_lower_doubles(n) doubles):
+ * a rank that receives a job's factor only to predict with the ozaki engine builds its planes
+ * without unpacking W into an n×n matrix.  Same planes and row scales, bit for bit.          */
+int    gp2d_ozaki_prepare_packed(const double* packed, int64_t n, const gp2d_kernel_t* k, double diag_add,
+                                 int wbits, int8_t* wres, double* rowscale, int* nmod_out, void* stream);
+/* Accuracy guard.  The int8 engine rounds each W row to `wbits` integer bits (0 = the default
+ * 49; up to 60): the variance kss − ‖W k*‖² then carries an elementwise relative error that
+ * grows where the posterior variance is small against kss — at the observations.
+ * gp2d_ozaki_guard: stats_dev[0] = the smallest latent posterior variance at the observed
+ *   training components, δ − δ²·(K_y⁻¹)_ii with (K_y⁻¹)_ii = Σ_k W_ki² and δ = diag_add (the
+ *   noise + jitter on K_y's diagonal; GP_laser.py:114-115; δ ≤ 0 gives stats_dev[0] ≤ 0, which the
+ *   policy sends to the FP64 engine), stats_dev[1] = max |W_ik|
+ *   (device doubles; workspace gp2d_ozaki_guard_workspace(n) bytes; fixed reduction order).
+ * gp2d_ozaki_error_model: the modelled elementwise error K·2^(49 − wbits)·(kss/v_min)^1.5
+ *   (K fitted to full-grid measurements).
+ * gp2d_ozaki_guard_bits: the smallest wbits in 49..60 whose modelled error is ≤ target (the
+ *   north-star gate is 1e-10), 0 if none (use the FP64 engine, gp2d_predict), −1 on bad input.
+ * Replaces nothing in the reference (its variance is fp64 throughout, GP_laser.py:128-131): it
+ * keeps the emulation inside the reference's accuracy contract for any hyperparameters.     */
+size_t gp2d_ozaki_guard_workspace(int64_t n);
+int    gp2d_ozaki_guard(const double* W, int64_t n, int64_t ldw, int64_t ntr, int64_t npad, double diag_add,
+                        double* stats_dev, void* work, size_t work_bytes, void* stream);
+double gp2d_ozaki_error_model(double kss, double vmin, int wbits);
+int    gp2d_ozaki_guard_bits(double kss, double vmin, double target);
 size_t gp2d_predict_ozaki_workspace(int64_t n, int64_t chunk);
 /* The variance GEMMs skip K slabs (64 training components) whose K* tile is exactly zero for
  * a 256-row grid tile — exact, such slabs add nothing.  gp2d_ozaki_set_skip(0) runs them
@@ -193,19 +221,40 @@ void   gp2d_ozaki_set_skip(int on);
  * coordinate (bbox: 6 doubles of device scratch).  The ozaki engine sorts training and grid
  * points by these codes so that all-zero K* tiles cluster into skippable slabs.          */
 int    gp2d_morton_codes(const double* pts, int64_t n, int dim, double* bbox, int64_t* codes, void* stream);
+/* gp2d_morton_sort: the engine's point order — Morton codes, a stable LSD radix sort of them
+ *   (8-bit digits; equal codes keep their input order, so the permutation is deterministic) into
+ *   order[n] (int64: sorted point j is input point order[j]) and, if `sorted` is not NULL, the
+ *   points gathered into that order (n × dim).  Workspace: gp2d_morton_sort_workspace(n) bytes.
+ * gp2d_gather_rows: dst[j] = src[order[j]] for rows of `dim` doubles (no aliasing).
+ * gp2d_obs_pad: a fit's observation vector — out[c·npad + i] = y[c·ntr + perm[i]] for i < ntr
+ *   (perm NULL: the identity), 0 for the padded points; y is the reference's stacking
+ *   [u_1..u_N, v_1..v_N] (GP_laser.py:98-99; krig.py:375-394 for bd = 2), out has bd·npad doubles.
+ * There is no reference call these replace: the reference never reorders points;
+ * they keep the ozaki engine's ordering off any framework kernel.                          */
+size_t gp2d_morton_sort_workspace(int64_t n);
+int    gp2d_morton_sort(const double* pts, int64_t n, int dim, double* sorted, int64_t* order, void* work,
+                        size_t work_bytes, void* stream);
+int    gp2d_gather_rows(const double* src, const int64_t* order, int64_t n, int64_t dim, double* dst,
+                        void* stream);
+int    gp2d_obs_pad(const double* y, int64_t ntr, int64_t npad, int bd, const int64_t* perm, double* out,
+                    void* stream);
 /* gp2d_predict_ozaki / _planes need n < 131072 (N_train < 65536): the int8 GEMM's biased
- * 32-bit sums must stay below 2^32 (the FP64 engine, gp2d_predict, has no such bound).    */
+ * 32-bit sums must stay below 2^32 (the FP64 engine, gp2d_predict, has no such bound).
+ * out_order (optional, int64[m]): xg is the caller's grid permuted (gp2d_morton_sort's sorted
+ * points, so K*'s zero tiles cluster); the outputs of point j go to position out_order[j] of
+ * mean / var — the caller's own order, scattered in the epilogue.  NULL: xg's order.      */
 int    gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int nmod, int64_t n,
                           const double* alpha, const double* xtr, int64_t ntr, int64_t ntr_pad,
                           const double* xg, int64_t m, const gp2d_kernel_t* k,
                           int var_mode, double noise, int compute_var,
-                          double* mean, double* var, int64_t chunk,
+                          double* mean, double* var, const int64_t* out_order, int64_t chunk,
                           void* work, size_t work_bytes, void* stream);
 /* K* residue planes ahead of the fit.  The int8 residues of K* depend only on the training
  * points, the grid and the kernel, so they can be generated before / concurrently with the
  * fit (e.g. while a rank waits for the factor broadcast):
  * gp2d_ozaki_nmod_apriori: a moduli count that bounds gp2d_ozaki_prepare's data-driven one
- *   for any fit of this kernel with diagonal K_y,ii = kdiag + diag_add (−1 on bad input);
+ *   for any fit of this kernel with diagonal K_y,ii = kdiag + diag_add at W precision wbits
+ *   (0 = default; −1 on bad input);
  * gp2d_ozaki_kstar: the planes of every chunk of the m grid points (per chunk: nmod planes
  *   of n·2·⌈chunk/256⌉·256 bytes, then the K* block flags the GEMMs' zero-slab skipping
  *   reads; size gp2d_ozaki_kstar_bytes);
@@ -215,7 +264,7 @@ int    gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int nmod, 
  *   nmod_b (the caller regenerates).
  * Replaces the same reference calls as gp2d_predict_ozaki (compute_Ks + getMean + the
  * variance diagonal, GP_laser.py:122-136).                                              */
-int    gp2d_ozaki_nmod_apriori(int64_t n, const gp2d_kernel_t* k, double diag_add);
+int    gp2d_ozaki_nmod_apriori(int64_t n, const gp2d_kernel_t* k, double diag_add, int wbits);
 size_t gp2d_ozaki_kstar_bytes(int64_t n, int64_t m, int64_t chunk, int nmod);
 int    gp2d_ozaki_kstar(const double* xtr, int64_t ntr, int64_t ntr_pad, const double* xg, int64_t m,
                         const gp2d_kernel_t* k, int nmod, int64_t chunk, int8_t* bres, size_t bres_bytes,
@@ -225,7 +274,8 @@ int    gp2d_predict_ozaki_planes(const int8_t* wres, const double* rowscale, int
                                  const double* alpha, const double* xtr, int64_t ntr, int64_t ntr_pad,
                                  const double* xg, int64_t m, const gp2d_kernel_t* k, int var_mode,
                                  double noise, const int8_t* bres, int nmod_b, double* mean, double* var,
-                                 int64_t chunk, void* work, size_t work_bytes, void* stream);
+                                 const int64_t* out_order, int64_t chunk, void* work, size_t work_bytes,
+                                 void* stream);
 
 /* ---- hyperparameters: log marginal likelihood and its gradient -----
  * Replaces the objective of GPy model.optimize / optimize_restarts (krig.py:450,
@@ -344,6 +394,11 @@ int gp2d_pack_lower(double* W, int64_t n, int64_t ldw, double* packed, int unpac
  *   resolved at first call (no link-time dependency).  Returns −100 − ncclResult_t on an RCCL
  *   failure.                                                                             */
 int gp2d_bcast(void* buf, size_t bytes, int root, void* comm, void* stream);
+/* gp2d_status_flip: 0 ↔ INT32_MAX on `count` device status words (an involution).  Applied
+ *   before and after an all-reduce MIN of LAPACK-style info words (0 = success, k > 0 = first
+ *   non-PD minor), it makes the reduction return the FIRST failing minor over the ranks, or 0 —
+ *   the one-rank answer (the distributed factor's status, gp2d/distributed.py).              */
+int gp2d_status_flip(int* status, int count, void* stream);
 
 /* ---- instrumentation ------------------------------------------------------------
  * When enabled, every launch of the predict variance kernel (the dominant

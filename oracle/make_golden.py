@@ -245,6 +245,33 @@ def config_subsample(xa, xg, n_near=256, n_rand=256, seed=5):
     return np.unique(np.concatenate([near, rnd]))
 
 
+_LD = {}
+
+
+def _ld_residual_part(cols):
+    """rhs[:, cols] − K·z[:, cols] in x87 long double (a worker of _ld_residual)."""
+    ld = np.longdouble
+    K, rhs, z = _LD["K"], _LD["rhs"], _LD["z"]
+    return rhs[:, cols].astype(ld) - K.astype(ld) @ z[:, cols].astype(ld)
+
+
+def _ld_residual(K, rhs, z, procs=None):
+    """The refinement residual rhs − K·z in long double, its columns split over worker processes
+    (numpy's long-double matmul has no BLAS: one process takes tens of minutes at n = 8192).
+    Every column's arithmetic is the same as in one process."""
+    import multiprocessing as mp
+    procs = procs or min(8, os.cpu_count() or 1)
+    if procs <= 1 or z.shape[1] < 2 * procs:
+        _LD.update(K=K, rhs=rhs, z=z)
+        return _ld_residual_part(np.arange(z.shape[1]))
+    _LD.update(K=K, rhs=rhs, z=z)   # inherited by the forked workers
+    chunks = np.array_split(np.arange(z.shape[1]), procs)
+    with mp.get_context("fork").Pool(procs) as pool:
+        parts = pool.map(_ld_residual_part, chunks)
+    _LD.clear()
+    return np.concatenate(parts, axis=1)
+
+
 def _refined_posterior(K, ks, kss, obs):
     """Posterior mean / variance at the fixture points, accurate well past fp64 working
     precision: Cholesky solve of K z = ks, one step of iterative refinement with the residual
@@ -256,8 +283,7 @@ def _refined_posterior(K, ks, kss, obs):
     c = sla.cho_factor(K, lower=True)
     rhs = np.concatenate([ks.T, obs[:, None]], 1)       # (n, 2m + 1)
     z = sla.cho_solve(c, rhs)
-    Kl = K.astype(ld)
-    r = rhs.astype(ld) - Kl @ z.astype(ld)
+    r = _ld_residual(K, rhs, z)
     z = z.astype(ld) + sla.cho_solve(c, r.astype(np.float64)).astype(ld)
     ksl = ks.astype(ld)
     var = kss.astype(ld) - np.einsum("ij,ji->i", ksl, z[:, :-1])
@@ -306,6 +332,47 @@ def gen_configs(gs, out):
         d[f"{name}_kss"] = kss
         d[f"{name}_K_rowsum"] = K.sum(1)
     np.savez_compressed(os.path.join(out, "configs_N4096.npz"), **d)
+
+
+GUARD_SETTINGS = ((12.0, 1e-3), (2.0, 5e-2), (5.0, 1e-4))   # (ℓ, noise): VERDICT r04 "next" item 1
+
+
+def gen_guard(gs, out):
+    """The headline workload (div-free, the bench's seeded N_train = 4096 tracks, the 256² bbox
+    grid at the 512-point config_subsample) at hyperparameters away from the bench's ℓ = 5 km,
+    noise 0.0025 — GUARD_SETTINGS, inside config E's range (ℓ ∈ [2, 12] km, noise ∈ [1e-3, 5e-2],
+    bench.py) and one step past it (noise 1e-4): the reference's GP_laser.py:113-134 recipe with
+    its vectorised myKernel and np.linalg.inv, plus the refined posterior (_refined_posterior).
+    The yardstick for the ozaki engine's accuracy guard (tests/test_gpu_guard.py)."""
+    x, y, u, v = synthetic_tracks(4096)
+    xa = np.stack([x, y], 1)
+    gx = np.linspace(x.min() - 5, x.max() + 5, 256)      # = gp2d.data.bbox_grid(x, y, 256, pad=5)
+    gy = np.linspace(y.min() - 5, y.max() + 5, 256)
+    GX, GY = np.meshgrid(gx, gy)
+    xg_all = np.stack([GX.reshape(-1), GY.reshape(-1)], 1)
+    idx = config_subsample(xa, xg_all)
+    xg = xg_all[idx]
+    obs = np.concatenate([u, v])
+    d = dict(x_sum=np.array([x.sum(), y.sum()]), u_sum=np.array([u.sum(), v.sum()]), idx=idx, xg=xg,
+             settings=np.array(GUARD_SETTINGS))
+    for k, (l, nz) in enumerate(GUARD_SETTINGS):
+        t0 = time.time()
+        K = gs["myKernel"](xa, xa, l, l, 1.0)
+        K = K + np.identity(K.shape[0]) * nz              # GP_laser.py:114-115
+        Ki = np.linalg.inv(K)                            # GP_laser.py:118
+        Ks = gs["myKernel"](xg, xa, l, l, 1.0)           # GP_laser.py:122 (vectorised form)
+        f = np.ravel(gs["getMean"](Ks, Ki, obs[:, None]))   # GP_laser.py:134
+        kss = np.diag(gs["myKernel"](xg, xg, l, l, 1.0))
+        var = kss - np.einsum("ij,ij->i", Ks, Ks @ Ki)   # diag of GP_laser.py:129
+        del Ki
+        mr, vr = _refined_posterior(K, Ks, kss, obs)
+        print(f"  guard l={l} noise={nz}: {time.time() - t0:.1f}s; inv recipe vs refined: var elementwise "
+              f"{np.max(np.abs(var - vr) / vr):.1e}, normwise {np.max(np.abs(var - vr)) / np.max(vr):.1e}, "
+              f"mean {np.max(np.abs(f - mr)) / np.max(np.abs(mr)):.1e}; min var/kss {np.min(vr / kss):.1e}")
+        d[f"s{k}_mean"], d[f"s{k}_var"] = f, var
+        d[f"s{k}_mean_refined"], d[f"s{k}_var_refined"] = mr, vr
+        d[f"s{k}_kss"] = kss
+    np.savez_compressed(os.path.join(out, "guard_N4096.npz"), **d)
 
 
 def gen_config_b(gs, out):
@@ -735,7 +802,7 @@ def main():
                 prep=lambda: gen_prep(a.out), window=lambda: gen_prior_window(a.out),
                 configs=lambda: gen_configs(gs, a.out), config_b=lambda: gen_config_b(gs, a.out),
                 config_d=lambda: gen_config_d(gs, a.out),
-                config_e=lambda: gen_config_e(gs, a.out))
+                config_e=lambda: gen_config_e(gs, a.out), guard=lambda: gen_guard(gs, a.out))
     for name, fn in jobs.items():
         if a.only and name not in a.only.split(","):
             continue

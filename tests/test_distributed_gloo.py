@@ -52,13 +52,16 @@ def _worker(rank, world, port, out_dir):
                      device=torch.device("cpu"))
     else:
         gp = None
-    got = GD.broadcast_fit(gp, spec, 0.01, None, "cpu")
+    comm = {}
+    got = GD.broadcast_fit(gp, spec, 0.01, None, "cpu", comm=comm)
+    cs = GD.comm_summary(comm)["bcast"]
     m = 1000
     xg = torch.stack([torch.linspace(0, 9, m, dtype=torch.float64), torch.linspace(3, -2, m, dtype=torch.float64)], 1)
     lo, hi, mean, var = GD.predict_shard(_fake_predict, xg)
     fm, fv = GD.gather_shards(m, 2, lo, hi, mean, var, "cpu")
     torch.save({"W": got.W, "alpha": got.alpha, "x": got.x, "n_pad": got.n_pad, "lo": lo, "hi": hi,
-                "mean": fm, "var": fv}, os.path.join(out_dir, f"rank{rank}.pt"))
+                "mean": fm, "var": fv, "comm": [cs["calls"], cs["bytes_sent"], cs["bytes_recv"], cs["ms"]]},
+               os.path.join(out_dir, f"rank{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -75,6 +78,12 @@ def test_broadcast_and_shards_world2(tmp_path):
     em, ev = _fake_predict(xg)
     for i in range(world):
         assert torch.equal(r[i]["mean"], em) and torch.equal(r[i]["var"], ev)
+    # the comm accounting (bench.py's N > 1 `comm` block): the root sends the payload once, the
+    # other rank receives it — packed W (≈ n²/2 doubles), α and X_train
+    from gp2d import distributed as GD
+    payload = 8 * (GD._packed_len(256) + 256 + 100 * 2)
+    assert r[0]["comm"][:3] == [1, payload, 0] and r[1]["comm"][:3] == [1, 0, payload]
+    assert r[0]["comm"][3] >= 0 and r[1]["comm"][3] >= 0
 
 
 def test_assemble_from_shards_numpy():

@@ -38,6 +38,13 @@ def test_bench_json_contract(variance):
     assert r["bound"] == "mfma" and 0 < r["frac"] < 1 and abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-12
     c = d["cpu_baseline"]
     assert c["value"] > 0 and c["kind"] == "port" and c["cores"] >= 1 and c["sample"]
+    # N = 1 readings beside the headline: the strict FP64 engine and the Krig drop-in surface
+    assert d["f64_value"] > 0 and d["f64"]["steps"] == 5
+    assert d["dropin"]["value"] > 0 and d["dropin"]["variance_engine"] in ("ozaki", "f64")
+    if variance == "ozaki":   # the accuracy guard's decision for the timed jobs
+        assert d["guard"]["engine"] in ("ozaki", "f64") and d["guard"]["vmin_over_kss"] > 0
+    # the job shape krige_jobs resolved: a batch only back to back, batch_ahead only for a batch
+    assert d["batch_ahead"] is False or (d["fits_ahead"] == 0 and d["batch_fits"] > 1)
 
 
 def test_bench_two_ranks_default_contract():
@@ -66,6 +73,14 @@ def test_bench_two_ranks_default_contract():
     assert d["timed_fits"]["warmup_jobs_run"] >= 2
     sj = d["single_job"]
     assert sj["ms"] > 0 and sj["distributed_fit"]["ms"] > 0 and sj["distributed_fit"]["fit_ms"] > 0
+    # the N > 1 line's communication accounting: every job's factor reaches both ranks
+    cb = d["comm"]["bcast"]
+    assert cb["calls_per_job"] == 1 and cb["ms_per_job_max_over_ranks"] > 0
+    n = 2 * 256   # padded matrix order at N_train = 256 (ozaki layout)
+    # each rank fits (and sends) every other job's factor and receives the rest
+    assert cb["bytes_recv_per_job_max"] + cb["bytes_sent_per_job_max"] >= 8 * n * n // 2
+    dc = sj["distributed_fit"]["comm"]
+    assert dc["panel_bcast"]["calls_per_job"] >= 1 and dc["w_allgather"]["calls_per_job"] == 1
 
 
 def test_bench_multi_rank_paths_under_rccl():
@@ -91,6 +106,7 @@ def test_bench_multi_rank_paths_under_rccl():
     assert d["api"] == "distributed.krige_jobs_sharded" and d["scaling"] == "strong"
     assert d["timed_fits"]["issued_in_window"] == d["timed_fits"]["issued_total"] == 3
     assert d["single_job"]["distributed_fit"]["ms"] > 0
+    assert d["comm"]["bcast"]["calls_per_job"] == 1 and d["comm"]["bcast"]["ms_per_job_max_over_ranks"] > 0
 
 
 def test_bench_gpus2_self_launch():

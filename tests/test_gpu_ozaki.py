@@ -131,9 +131,15 @@ def test_kstar_ahead_matches_oracle(ntr, m, kind, l, chunk):
 def test_nmod_apriori_bounds_data_driven(kind, l, noise, jitter):
     x, y = tracks(700, 5)
     ks = E.KernelSpec(kind=kind, l_df=l, l_cf=l * 1.1, ratio=0.5 if kind == "mixed" else 1.0)
-    gp = E.fit(ks, x, y, noise=noise, jitter=jitter, variance="ozaki")
-    apriori = int(E.N.lib().gp2d_ozaki_nmod_apriori(gp.n, __import__("ctypes").byref(ks.desc()), noise + jitter))
+    gp = E.fit(ks, x, y, noise=noise, jitter=jitter, variance="ozaki", guard=False)
+    apriori = int(E.N.lib().gp2d_ozaki_nmod_apriori(gp.n, __import__("ctypes").byref(ks.desc()), noise + jitter, 0))
     assert gp.extra["ozaki"][2] <= apriori <= gp.extra["ozaki"][2] + 1
+    # at every W precision the accuracy guard can pick: the data-driven count (synchronous
+    # prepare) never exceeds the a-priori one the engine uses
+    for wb in (49, 53, 57, 60):
+        E.ozaki_prepare(gp, wbits=wb)
+        ap = int(E.N.lib().gp2d_ozaki_nmod_apriori(gp.n, __import__("ctypes").byref(ks.desc()), noise + jitter, wb))
+        assert gp.extra["ozaki"][2] <= ap <= gp.extra["ozaki"][2] + 1, wb
 
 
 def test_kstar_ahead_too_few_moduli_falls_back_inline():
@@ -188,7 +194,7 @@ def test_async_prepare_matches_data_driven(kind, l, noise):
     rng = np.random.default_rng(18)
     xg = np.stack([rng.uniform(-5, 65, 1200), rng.uniform(-5, 50, 1200)], 1)
     ks = E.KernelSpec(kind=kind, l_df=l, l_cf=l * 1.2, ratio=0.5 if kind == "mixed" else 1.0)
-    gp = E.fit(ks, x, y, noise=noise, variance="ozaki")
+    gp = E.fit(ks, x, y, noise=noise, variance="ozaki", guard=False)   # both at the default precision
     n_async = gp.extra["ozaki"][2]
     ma, va = (t.cpu().numpy() for t in E.predict(gp, xg, chunk=512))
     E.ozaki_prepare(gp)   # data-driven count (synchronises)

@@ -24,7 +24,7 @@ def test_library_exports_every_header_symbol():
     for s in syms:
         assert hasattr(L, s), s
     assert set(syms) == set(_native.EXPORTS)
-    assert L.gp2d_abi_version() == _native.ABI_VERSION == 8
+    assert L.gp2d_abi_version() == _native.ABI_VERSION == 9
     assert L.gp2d_padded_points(1) == 64 and L.gp2d_padded_points(64) == 64 and L.gp2d_padded_points(65) == 128
 
 
@@ -92,13 +92,13 @@ def test_ozaki_rejects_ratio_outside_unit_interval():
     L = N.lib()
     for r in (-0.25, 1.5):
         k = N.vector_kernel_desc(N.KIND_MIXED, 5.0, 5.0, r)
-        assert L.gp2d_ozaki_nmod_apriori(8192, ctypes.byref(k), 0.0025) == -1
+        assert L.gp2d_ozaki_nmod_apriori(8192, ctypes.byref(k), 0.0025, 0) == -1
         nm = ctypes.c_int(0)
         one = ctypes.c_void_p(1)
-        rc = L.gp2d_ozaki_prepare_async(one, 512, 512, ctypes.byref(k), 0.0025, one, one, ctypes.byref(nm), None)
+        rc = L.gp2d_ozaki_prepare_async(one, 512, 512, ctypes.byref(k), 0.0025, 0, one, one, ctypes.byref(nm), None)
         assert rc < 0 and b"ratio" in L.gp2d_last_error()
     k = N.vector_kernel_desc(N.KIND_MIXED, 5.0, 5.0, 0.5)
-    assert L.gp2d_ozaki_nmod_apriori(8192, ctypes.byref(k), 0.0025) > 0
+    assert L.gp2d_ozaki_nmod_apriori(8192, ctypes.byref(k), 0.0025, 0) > 0
 
 
 def test_no_cpu_fallback():
