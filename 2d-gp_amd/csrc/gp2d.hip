@@ -118,8 +118,10 @@ static int assemble_impl(const double* xa, int64_t na, int64_t na_pad, const dou
 #endif
 
 // ------------------------------------------------------------- Ozaki constants
-static const int kModuli[OZ_MAXMOD] = {256, 255, 253, 251, 247, 241, 239, 233,
-                                       229, 227, 223, 217, 211, 199, 197, 193};
+// pairwise coprime, largest first (the count a product needs takes the first nmod); the last four
+// (primes) are reached only by the guard's widest precisions at large n
+static const int kModuli[OZ_MAXMOD] = {256, 255, 253, 251, 247, 241, 239, 233, 229, 227,
+                                       223, 217, 211, 199, 197, 193, 191, 181, 179, 173};
 
 // number of moduli for a bound on log2 max|Pint| (one guard bit: Π m_l > 2·max|Pint|)
 static int ozaki_nmod_bits(double log2_pmax) {
@@ -132,11 +134,14 @@ static int ozaki_nmod_bits(double log2_pmax) {
   return -1;
 }
 // worst case (sizing): |Pint| ≤ n·2^{pW}·2^{pB−1} at the largest W precision the guard can pick
-static int ozaki_nmod_for(int64_t n) { return ozaki_nmod_bits(std::log2((double)n) + OZ_PW_MAX + OZ_PB - 1.0); }
-// W precision of a call: 0 → the default OZ_PW; otherwise OZ_PW .. OZ_PW_MAX
+static int ozaki_nmod_for(int64_t n) { return ozaki_nmod_bits(std::log2((double)n) + OZ_PW_MAX + OZ_PB_MAX - 1.0); }
+// precisions of a call: 0 → the defaults OZ_PW / OZ_PB; otherwise OZ_PW .. OZ_PW_MAX (W rows)
+// and OZ_PB .. OZ_PB_MAX (K*)
 static int ozaki_wbits(int wbits) { return wbits == 0 ? OZ_PW : wbits; }
-static int valid_wbits(int wbits) {
+static int ozaki_kbits(int kbits) { return kbits == 0 ? OZ_PB : kbits; }
+static int valid_bits(int wbits, int kbits) {
   GP2D_REQUIRE(wbits == 0 || (wbits >= OZ_PW && wbits <= OZ_PW_MAX), "ozaki: wbits must be 0 or 49..60");
+  GP2D_REQUIRE(kbits == 0 || (kbits >= OZ_PB && kbits <= OZ_PB_MAX), "ozaki: kbits must be 0 or 45..50");
   return 0;
 }
 
@@ -162,9 +167,10 @@ static double kstar_bound(const gp2d_kernel_t* k) {
   }
 }
 
-static int make_ozaki_consts(int nmod, const gp2d_kernel_t* k, OzakiConsts& oc, int pw = OZ_PW) {
+static int make_ozaki_consts(int nmod, const gp2d_kernel_t* k, OzakiConsts& oc, int pw = OZ_PW, int pb = OZ_PB) {
   oc.nmod = nmod;
   oc.pw = pw;
+  oc.pb = pb;
   GP2D_REQUIRE(oc.nmod > 0 && oc.nmod <= OZ_MAXMOD, "ozaki: bad number of moduli");
   double M = 1.0;
   for (int l = 0; l < oc.nmod; ++l) M *= (double)kModuli[l];
@@ -189,7 +195,7 @@ static int make_ozaki_consts(int nmod, const gp2d_kernel_t* k, OzakiConsts& oc, 
     oc.t[l] = ((double)inv - h * (double)ml) / (double)ml;  // h·m_l is exact (≤ 41 bits)
   }
   const double bmax = kstar_bound(k);
-  oc.sB = OZ_PB - 1 - (int)std::ceil(std::log2(bmax));
+  oc.sB = pb - 1 - (int)std::ceil(std::log2(bmax));
   oc.vlimit = 4.0 * std::sqrt(gp2d_kernel_diag(k));
   return 0;
 }
@@ -1112,11 +1118,11 @@ static int launch_w_res(const double* W, int64_t n, WRows ldw, const OzakiConsts
   return check_launch("ozaki_w_res_kernel");
 }
 
-int gp2d_ozaki_prepare(const double* W, int64_t n, int64_t ldw, const gp2d_kernel_t* k, int wbits, int8_t* wres,
-                       double* rowscale, int* nmod_out, void* stream) {
+int gp2d_ozaki_prepare(const double* W, int64_t n, int64_t ldw, const gp2d_kernel_t* k, int wbits, int kbits,
+                       int8_t* wres, double* rowscale, int* nmod_out, void* stream) {
   GP2D_CHECK(validate_ozaki_kernel(k));
-  GP2D_CHECK(valid_wbits(wbits));
-  const int pw = ozaki_wbits(wbits);
+  GP2D_CHECK(valid_bits(wbits, kbits));
+  const int pw = ozaki_wbits(wbits), pb = ozaki_kbits(kbits);
   GP2D_REQUIRE(n % IBM == 0 && n > 0, "ozaki: n must be a positive multiple of 256");
   GP2D_REQUIRE(nmod_out != nullptr, "ozaki: nmod_out is NULL");
   hipStream_t s = S(stream);
@@ -1139,20 +1145,20 @@ int gp2d_ozaki_prepare(const double* W, int64_t n, int64_t ldw, const gp2d_kerne
   int sB = 0;
   {
     OzakiConsts probe;
-    GP2D_CHECK(make_ozaki_consts(1, k, probe));
+    GP2D_CHECK(make_ozaki_consts(1, k, probe, pw, pb));
     sB = probe.sB;
   }
   const double sq = 2.0 * std::sqrt(gp2d_kernel_diag(k));
   double bmax = 1.0;
   for (int64_t i = 0; i < n; ++i) {
-    const double a = std::ldexp(hl1[i] * 1.01, OZ_PB - 1);
-    const double b = std::ldexp(sq, (int)hs[i] + sB) + std::ldexp((double)n, OZ_PB - 2) + hl1[i] + (double)n;
+    const double a = std::ldexp(hl1[i] * 1.01, pb - 1);
+    const double b = std::ldexp(sq, (int)hs[i] + sB) + std::ldexp((double)n, pb - 2) + hl1[i] + (double)n;
     bmax = std::max(bmax, std::min(a, b));
   }
   const int nmod = ozaki_nmod_bits(std::log2(bmax));
   GP2D_REQUIRE(nmod > 0, "ozaki: row bound exceeds the modulus table");
   OzakiConsts oc;
-  GP2D_CHECK(make_ozaki_consts(nmod, k, oc, pw));
+  GP2D_CHECK(make_ozaki_consts(nmod, k, oc, pw, pb));
   ozaki_rowscale_final_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(rowscale, n, oc.M, oc.sB);
   GP2D_CHECK(check_launch("ozaki_rowscale_final_kernel"));
   GP2D_CHECK(launch_w_res(W, n, WRows{ldw}, oc, wres, rowscale, s));
@@ -1161,19 +1167,19 @@ int gp2d_ozaki_prepare(const double* W, int64_t n, int64_t ldw, const gp2d_kerne
 }
 
 static int prepare_apriori(const double* W, int64_t n, WRows wr, const gp2d_kernel_t* k, double diag_add,
-                           int wbits, int8_t* wres, double* rowscale, int* nmod_out, hipStream_t s) {
+                           int wbits, int kbits, int8_t* wres, double* rowscale, int* nmod_out, hipStream_t s) {
   GP2D_CHECK(validate_ozaki_kernel(k));
-  GP2D_CHECK(valid_wbits(wbits));
-  const int pw = ozaki_wbits(wbits);
+  GP2D_CHECK(valid_bits(wbits, kbits));
+  const int pw = ozaki_wbits(wbits), pb = ozaki_kbits(kbits);
   GP2D_REQUIRE(n % IBM == 0 && n > 0, "ozaki: n must be a positive multiple of 256");
   GP2D_REQUIRE(W != nullptr && wres != nullptr && rowscale != nullptr, "ozaki: NULL buffer");
   GP2D_REQUIRE(nmod_out != nullptr, "ozaki: nmod_out is NULL");
   // the a-priori count bounds the data-driven one for any fit with this K_y diagonal (no host
   // round trip); a violated bound could only come from a failed factor and is poisoned by CRT
-  const int nmod = gp2d_ozaki_nmod_apriori(n, k, diag_add, pw);
+  const int nmod = gp2d_ozaki_nmod_apriori(n, k, diag_add, pw, pb);
   GP2D_REQUIRE(nmod > 0, "ozaki: a-priori bound exceeds the modulus table");
   OzakiConsts oc;
-  GP2D_CHECK(make_ozaki_consts(nmod, k, oc, pw));
+  GP2D_CHECK(make_ozaki_consts(nmod, k, oc, pw, pb));
   // no L1 norms (the count is a-priori): one pass over W for the row exponents, one for the planes
   ozaki_w_scale_kernel<<<(unsigned)n, 256, 0, s>>>(W, n, wr, pw, rowscale, nullptr, oc.M, oc.sB, 1);
   GP2D_CHECK(check_launch("ozaki_w_scale_kernel"));
@@ -1183,15 +1189,15 @@ static int prepare_apriori(const double* W, int64_t n, WRows wr, const gp2d_kern
 }
 
 int gp2d_ozaki_prepare_async(const double* W, int64_t n, int64_t ldw, const gp2d_kernel_t* k, double diag_add,
-                             int wbits, int8_t* wres, double* rowscale, int* nmod_out, void* stream) {
+                             int wbits, int kbits, int8_t* wres, double* rowscale, int* nmod_out, void* stream) {
   GP2D_REQUIRE(ldw >= n, "ozaki: ldw must be >= n");
-  return prepare_apriori(W, n, WRows{ldw}, k, diag_add, wbits, wres, rowscale, nmod_out, S(stream));
+  return prepare_apriori(W, n, WRows{ldw}, k, diag_add, wbits, kbits, wres, rowscale, nmod_out, S(stream));
 }
 
 int gp2d_ozaki_prepare_packed(const double* packed, int64_t n, const gp2d_kernel_t* k, double diag_add, int wbits,
-                              int8_t* wres, double* rowscale, int* nmod_out, void* stream) {
+                              int kbits, int8_t* wres, double* rowscale, int* nmod_out, void* stream) {
   GP2D_REQUIRE(n % NB == 0, "ozaki: n must be a multiple of 128 (the packing's row blocks)");
-  return prepare_apriori(packed, n, WRows{0}, k, diag_add, wbits, wres, rowscale, nmod_out, S(stream));
+  return prepare_apriori(packed, n, WRows{0}, k, diag_add, wbits, kbits, wres, rowscale, nmod_out, S(stream));
 }
 
 // ---- accuracy guard: what W precision the variance needs for this fit
@@ -1219,22 +1225,42 @@ int gp2d_ozaki_guard(const double* W, int64_t n, int64_t ldw, int64_t ntr, int64
   return check_launch("ozaki_guard_finish_kernel");
 }
 
-// Elementwise relative error of the ozaki variance with W rows at `wbits` bits, modelled as
-// K·2^(49 − wbits)·(kss / v_min)^1.5 (v_min: the smallest latent posterior variance at the
-// observations, gp2d_ozaki_guard's stats[0]); K from the full-grid measurements of
-// tools/probe_guard.py (ℓ 2..12 km, noise 1e-4..5e-2, profiles/r05_guard_probe.jsonl), whose
-// measured/model ratios lie in [0.45, 0.85] — the constant sits above the largest of them.
-static constexpr double OZ_GUARD_K = 3.5e-15;
-double gp2d_ozaki_error_model(double kss, double vmin, int wbits) {
+// Elementwise relative error of the ozaki variance, modelled as the sum of its two rounding
+// terms, with X = kss / v_min (v_min: the smallest latent posterior variance at the observations,
+// gp2d_ozaki_guard's stats[0]):
+//   W rows at wbits:  A·2^(49 − wbits)·X^1.5   (Σ_i V_ij·δV_ij with δW ∝ the row maxima)
+//   K* at kbits:      B·2^(45 − kbits)·X       (2·δK*·K_y⁻¹k*, ‖K_y⁻¹k*‖ ≲ 1 at the observations)
+// A, B fitted to full-grid measurements of the emulation against the FP64 products (ℓ 2..12 km,
+// noise 1e-4..5e-2, W 46..56 bits, K* 45..50 bits; tools/probe_guard.py, profiles/r05_guard_*.jsonl)
+// and raised by 1.4× over the fit, which reproduces every measurement within 1.3×.
+static constexpr double OZ_GUARD_A = 1.95e-15, OZ_GUARD_B = 2.9e-14;
+double gp2d_ozaki_error_model(double kss, double vmin, int wbits, int kbits) {
   if (!(kss > 0.0)) return INFINITY;
   if (!(vmin > 0.0)) return INFINITY;   // a non-positive latent variance: no precision covers it
-  return OZ_GUARD_K * std::ldexp(1.0, OZ_PW - ozaki_wbits(wbits)) * std::pow(kss / vmin, 1.5);
+  const double X = kss / vmin;
+  return OZ_GUARD_A * std::ldexp(1.0, OZ_PW - ozaki_wbits(wbits)) * X * std::sqrt(X) +
+         OZ_GUARD_B * std::ldexp(1.0, OZ_PB - ozaki_kbits(kbits)) * X;
 }
 
-int gp2d_ozaki_guard_bits(double kss, double vmin, double target) {
-  if (!(target > 0.0)) return -1;
-  for (int b = OZ_PW; b <= OZ_PW_MAX; ++b)
-    if (gp2d_ozaki_error_model(kss, vmin, b) <= target) return b;
+// The cheapest (wbits, kbits) — fewest total bits, i.e. moduli; then the smaller model — whose
+// modelled error is ≤ target: 1 and the bits; 0 if none (the FP64 engine); −1 on bad input.
+int gp2d_ozaki_guard_bits(double kss, double vmin, double target, int* wbits, int* kbits) {
+  if (!(target > 0.0) || wbits == nullptr || kbits == nullptr) return -1;
+  for (int tot = OZ_PW + OZ_PB; tot <= OZ_PW_MAX + OZ_PB_MAX; ++tot) {
+    int bw = 0, bk = 0;
+    double best = INFINITY;
+    for (int pb = OZ_PB; pb <= OZ_PB_MAX; ++pb) {
+      const int pw = tot - pb;
+      if (pw < OZ_PW || pw > OZ_PW_MAX) continue;
+      const double e = gp2d_ozaki_error_model(kss, vmin, pw, pb);
+      if (e <= target && e < best) { best = e; bw = pw; bk = pb; }
+    }
+    if (bw) {
+      *wbits = bw;
+      *kbits = bk;
+      return 1;
+    }
+  }
   return 0;   // beyond the int8 engine's precision range: the FP64 engine
 }
 
@@ -1279,7 +1305,7 @@ static void launch_kstar(dim3 grid, hipStream_t s, const double* xtr, int64_t nt
 // block flags pre_flags bytes further; the same kernel then runs mean-only, so the mean is
 // bit-identical to the inline path).  The int8 GEMMs skip the K slabs whose K* tile is all
 // zero (exact: they add nothing); flags → slab lists per chunk in `skip` (oz_list_bytes).
-static int predict_ozaki_impl(const int8_t* wres, const double* rowscale, int nmod, int64_t n,
+static int predict_ozaki_impl(const int8_t* wres, const double* rowscale, int nmod, int kbits, int64_t n,
                               const double* alpha, const double* xtr, int64_t ntr,
                               int64_t ntr_pad, const double* xg, int64_t m, const gp2d_kernel_t* k, int var_mode,
                               double noise, int compute_var, double* mean, double* var,
@@ -1287,7 +1313,7 @@ static int predict_ozaki_impl(const int8_t* wres, const double* rowscale, int nm
                               int8_t* bres, uint8_t* cres, double* pm, double* P, uint8_t* flags, int* skip,
                               const int8_t* pre, size_t pre_stride, size_t pre_flags, hipStream_t s) {
   OzakiConsts oc;
-  GP2D_CHECK(make_ozaki_consts(nmod, k, oc));
+  GP2D_CHECK(make_ozaki_consts(nmod, k, oc, OZ_PW, ozaki_kbits(kbits)));   // pw is in the row scales already
   const int nm = oc.nmod;
   // the GEMM epilogue's biased sums (ozaki_mod_u32) stay below 2^32 for K = n < 2^17
   GP2D_REQUIRE(n < 131072, "ozaki: the int8 GEMM epilogue needs n < 131072 (N_train < 65536)");
@@ -1367,7 +1393,7 @@ static size_t ozaki_partials(int64_t n) {
   return (size_t)std::max<int64_t>(n / 2 / OZ_KS_T + 1, n / OZ_CRT_ROWS + 1) + (size_t)(n / OZ_CRT_ROWS + 1);
 }
 
-int gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int nmod, int64_t n, const double* alpha,
+int gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int nmod, int kbits, int64_t n, const double* alpha,
                        const double* xtr,
                        int64_t ntr, int64_t ntr_pad, const double* xg, int64_t m, const gp2d_kernel_t* k,
                        int var_mode, double noise, int compute_var, double* mean, double* var,
@@ -1379,6 +1405,7 @@ int gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int nmod, int
   GP2D_REQUIRE(var_mode >= 0 && var_mode <= 2, "predict: bad var_mode");
   if (m <= 0) return 0;
   GP2D_REQUIRE(nmod > 0 && nmod <= ozaki_nmod_for(n), "ozaki: nmod exceeds the worst-case count the workspace is sized for");
+  GP2D_CHECK(valid_bits(0, kbits));
   const int nm = nmod;
   const int64_t ncols_max = 2 * round_up(chunk, IBN);
   int8_t* bres = reinterpret_cast<int8_t*>(work);
@@ -1387,29 +1414,29 @@ int gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int nmod, int
   double* P = pm + (size_t)(n / 2 / OZ_KS_T + 1) * ncols_max;
   uint8_t* flags = reinterpret_cast<uint8_t*>(P + (size_t)(n / OZ_CRT_ROWS + 1) * ncols_max);
   int* skip = reinterpret_cast<int*>(flags + oz_flag_bytes(n, chunk));
-  return predict_ozaki_impl(wres, rowscale, nmod, n, alpha, xtr, ntr, ntr_pad, xg, m, k, var_mode, noise,
+  return predict_ozaki_impl(wres, rowscale, nmod, kbits, n, alpha, xtr, ntr, ntr_pad, xg, m, k, var_mode, noise,
                             compute_var, mean, var, out_order, chunk, bres, cres, pm, P, flags, skip, nullptr, 0, 0,
                             S(stream));
 }
 
 // ---- K* residue planes ahead of the fit (they depend on the points and the kernel only)
-int gp2d_ozaki_nmod_apriori(int64_t n, const gp2d_kernel_t* k, double diag_add, int wbits) {
+int gp2d_ozaki_nmod_apriori(int64_t n, const gp2d_kernel_t* k, double diag_add, int wbits, int kbits) {
   // gp2d_ozaki_prepare's per-row bound (b) with the largest row exponent any fit can have:
   // W_ii = 1/L_ii ≥ 1/√(K_y,ii) (L_ii² = K_y,ii − Σ L_ik²), so max_k |W_ik| ≥ 1/√(kss + diag_add)
   // and s_i = p−1−⌊log2 max|W_i|⌋ ≤ s_max.  (1 − 2^-40) absorbs the rounding of L_ii; the
   // identity rows of padded points take bound (a) = 1.01·2^{2p−2}.  prepare's data-driven
   // count never exceeds this one.
-  if (validate_ozaki_kernel(k) != 0 || n <= 0 || valid_wbits(wbits) != 0) return -1;
-  const int pw = ozaki_wbits(wbits);
+  if (validate_ozaki_kernel(k) != 0 || n <= 0 || valid_bits(wbits, kbits) != 0) return -1;
+  const int pw = ozaki_wbits(wbits), pb = ozaki_kbits(kbits);
   const double kss = gp2d_kernel_diag(k);
   const double dmin = (1.0 - std::ldexp(1.0, -40)) / std::sqrt(kss + diag_add);
   const int smax = pw - 1 - (int)std::floor(std::log2(dmin));
   OzakiConsts probe;
-  if (make_ozaki_consts(1, k, probe) != 0) return -1;
+  if (make_ozaki_consts(1, k, probe, pw, pb) != 0) return -1;
   const double sq = 2.0 * std::sqrt(kss);
-  const double b = std::ldexp(sq, smax + probe.sB) + std::ldexp((double)n, OZ_PB - 2) + std::ldexp((double)n, pw) +
+  const double b = std::ldexp(sq, smax + probe.sB) + std::ldexp((double)n, pb - 2) + std::ldexp((double)n, pw) +
                    (double)n;
-  const double a_id = 1.01 * std::ldexp(1.0, pw + OZ_PB - 2);
+  const double a_id = 1.01 * std::ldexp(1.0, pw + pb - 2);
   return ozaki_nmod_bits(std::log2(std::max(b, a_id)));
 }
 
@@ -1420,18 +1447,19 @@ size_t gp2d_ozaki_kstar_bytes(int64_t n, int64_t m, int64_t chunk, int nmod) {
 }
 
 int gp2d_ozaki_kstar(const double* xtr, int64_t ntr, int64_t ntr_pad, const double* xg, int64_t m,
-                     const gp2d_kernel_t* k, int nmod, int64_t chunk, int8_t* bres, size_t bres_bytes,
+                     const gp2d_kernel_t* k, int nmod, int kbits, int64_t chunk, int8_t* bres, size_t bres_bytes,
                      void* stream) {
   GP2D_CHECK(validate_ozaki_kernel(k));
   const int64_t n = 2 * ntr_pad;
   GP2D_REQUIRE(ntr_pad > 0 && n % IBM == 0 && ntr <= ntr_pad, "ozaki_kstar: 2·ntr_pad must be a multiple of 256");
   GP2D_REQUIRE(chunk > 0 && chunk % (IBN / 2) == 0, "ozaki_kstar: chunk must be a positive multiple of 128");
   GP2D_REQUIRE(nmod > 0 && nmod <= OZ_MAXMOD, "ozaki_kstar: bad number of moduli");
+  GP2D_CHECK(valid_bits(0, kbits));
   if (m <= 0) return 0;
   GP2D_REQUIRE(bres != nullptr && bres_bytes >= gp2d_ozaki_kstar_bytes(n, m, chunk, nmod),
                "ozaki_kstar: plane buffer too small");
   OzakiConsts oc;
-  GP2D_CHECK(make_ozaki_consts(nmod, k, oc));
+  GP2D_CHECK(make_ozaki_consts(nmod, k, oc, OZ_PW, ozaki_kbits(kbits)));
   const VecParams vp = make_vec_params(k);
   const int64_t nmseg = (ntr_pad + OZ_KS_T - 1) / OZ_KS_T;
   const size_t planes = (size_t)nmod * (size_t)n * (size_t)(2 * round_up(chunk, IBN));
@@ -1457,10 +1485,10 @@ size_t gp2d_predict_ozaki_planes_workspace(int64_t n, int64_t chunk) {
          oz_list_bytes(n, chunk);
 }
 
-int gp2d_predict_ozaki_planes(const int8_t* wres, const double* rowscale, int nmod, int64_t n, const double* alpha,
-                              const double* xtr, int64_t ntr, int64_t ntr_pad, const double* xg, int64_t m,
-                              const gp2d_kernel_t* k, int var_mode, double noise, const int8_t* bres, int nmod_b,
-                              double* mean, double* var, const int64_t* out_order, int64_t chunk, void* work,
+int gp2d_predict_ozaki_planes(const int8_t* wres, const double* rowscale, int nmod, int kbits, int64_t n,
+                              const double* alpha, const double* xtr, int64_t ntr, int64_t ntr_pad, const double* xg,
+                              int64_t m, const gp2d_kernel_t* k, int var_mode, double noise, const int8_t* bres,
+                              int nmod_b, int kbits_b, double* mean, double* var, const int64_t* out_order, int64_t chunk, void* work,
                               size_t work_bytes, void* stream) {
   GP2D_CHECK(validate_ozaki_kernel(k));
   GP2D_REQUIRE(n == 2 * ntr_pad && n % IBM == 0, "ozaki: n must equal 2·ntr_pad and be a multiple of 256");
@@ -1471,8 +1499,9 @@ int gp2d_predict_ozaki_planes(const int8_t* wres, const double* rowscale, int nm
   GP2D_REQUIRE(alpha != nullptr && bres != nullptr, "ozaki_planes: alpha and the K* planes are required");
   if (m <= 0) return 0;
   GP2D_REQUIRE(nmod > 0 && nmod <= ozaki_nmod_for(n), "ozaki: nmod exceeds the worst-case count");
-  if (nmod > nmod_b) {
-    set_error("ozaki_planes: the fit needs more moduli than the K* planes carry");
+  GP2D_CHECK(valid_bits(0, kbits));
+  if (nmod > nmod_b || ozaki_kbits(kbits) != ozaki_kbits(kbits_b)) {
+    set_error("ozaki_planes: the fit needs more moduli, or another K* precision, than the planes carry");
     return -3;
   }
   const int64_t ncols_max = 2 * round_up(chunk, IBN);
@@ -1482,7 +1511,7 @@ int gp2d_predict_ozaki_planes(const int8_t* wres, const double* rowscale, int nm
   int* skip = reinterpret_cast<int*>(P + (size_t)(n / OZ_CRT_ROWS + 1) * ncols_max);
   const size_t planes = (size_t)nmod_b * (size_t)n * (size_t)ncols_max;
   const size_t stride = planes + oz_flag_bytes(n, chunk);
-  return predict_ozaki_impl(wres, rowscale, nmod, n, alpha, xtr, ntr, ntr_pad, xg, m, k, var_mode, noise, 1, mean,
+  return predict_ozaki_impl(wres, rowscale, nmod, kbits, n, alpha, xtr, ntr, ntr_pad, xg, m, k, var_mode, noise, 1, mean,
                             var, out_order, chunk, nullptr, cres, pm, P, nullptr, skip, bres, stride, planes,
                             S(stream));
 }
@@ -1762,6 +1791,15 @@ int gp2d_bcast(void* buf, size_t bytes, int root, void* comm, void* stream) {
     return -100 - rc;
   }
   return 0;
+}
+
+// An empty kernel whose dispatch marks a point of the stream in a rocprofv3 kernel trace (bench.py
+// brackets its timed region with tags 1 and 2; tools/timed_kernels.py lists what ran between).
+__global__ void trace_mark_kernel(int) {}
+
+int gp2d_trace_mark(int tag, void* stream) {
+  trace_mark_kernel<<<1, 64, 0, S(stream)>>>(tag);
+  return check_launch("trace_mark_kernel");
 }
 
 void gp2d_timing_enable(int on) {

@@ -23,7 +23,7 @@
 
 namespace gp2d {
 
-constexpr int OZ_MAXMOD = 16;
+constexpr int OZ_MAXMOD = 20;   // a multiple of 4: the CRT kernel reads the constants in groups of four
 #ifdef GP2D_OZ_P                   // one precision for both operands (dev builds)
 #define GP2D_OZ_PW GP2D_OZ_P
 #define GP2D_OZ_PB GP2D_OZ_P
@@ -41,15 +41,18 @@ constexpr int OZ_MAXMOD = 16;
 constexpr int OZ_PW = GP2D_OZ_PW;
 constexpr int OZ_PB = GP2D_OZ_PB;
 static_assert(OZ_PW <= 50 && OZ_PB <= 50, "ozaki: the one-part residues need |x| < 2^50");
-// The W precision is a run-time choice per fit (the accuracy guard, gp2d_ozaki_guard_bits):
-// OZ_PW is the default; up to OZ_PW_MAX bits the residue kernel splits Wint = xh·2^26 + xl.
+// Both precisions are run-time choices per fit (the accuracy guard, gp2d_ozaki_guard_bits):
+// OZ_PW / OZ_PB are the defaults; up to OZ_PW_MAX W bits the residue kernel splits
+// Wint = xh·2^26 + xl; the K* residues stay one-part (|Bint| < 2^50) up to OZ_PB_MAX.
 constexpr int OZ_PW_MAX = 60;
+constexpr int OZ_PB_MAX = 50;
 constexpr int OZ_SPLIT = 26;
 constexpr int OZ_HBITS = 33;       // exact high part of inv_l / m_l
 
 struct OzakiConsts {
   int nmod;
   int pw;                          // integer bits of the scaled W rows (OZ_PW .. OZ_PW_MAX)
+  int pb;                          // integer bits of the scaled K* (OZ_PB .. OZ_PB_MAX)
   int m[OZ_MAXMOD];
   double c26[OZ_MAXMOD];           // 2^26 mod m_l, centred (the split residues of pw > 50)
   double md[OZ_MAXMOD];            // m_l as a double (the residue kernels' fma operand)

@@ -37,7 +37,7 @@ EXPORTS = (
     "gp2d_dfact_sb", "gp2d_dfact_panel_doubles", "gp2d_dfact_workspace", "gp2d_dfact_panel", "gp2d_dfact_update",
     "gp2d_dfact_invstep", "gp2d_dfact_zpart", "gp2d_dfact_zsum", "gp2d_dfact_alpha_workspace", "gp2d_dfact_alpha_blocks",
     "gp2d_assemble_cols", "gp2d_copy2d", "gp2d_zero_upper", "gp2d_pack_lower_doubles", "gp2d_pack_lower",
-    "gp2d_timing_enable", "gp2d_timing_read", "gp2d_last_error",
+    "gp2d_timing_enable", "gp2d_timing_read", "gp2d_trace_mark", "gp2d_last_error",
 )
 
 
@@ -97,19 +97,19 @@ _SIGS = {
     "gp2d_predict": (_I, [_P, _I64, _I64, _P, _P, _I64, _I64, _P, _I64, _KP, _I, _D, _I, _P, _P, _I64, _P, _SZ, _P]),
     "gp2d_ozaki_nmod": (_I, [_I64]),
     "gp2d_ozaki_wres_bytes": (_SZ, [_I64]),
-    "gp2d_ozaki_prepare": (_I, [_P, _I64, _I64, _KP, _I, _P, _P, ctypes.POINTER(_I), _P]),
-    "gp2d_ozaki_nmod_apriori": (_I, [_I64, _KP, _D, _I]),
-    "gp2d_ozaki_prepare_async": (_I, [_P, _I64, _I64, _KP, _D, _I, _P, _P, ctypes.POINTER(_I), _P]),
-    "gp2d_ozaki_prepare_packed": (_I, [_P, _I64, _KP, _D, _I, _P, _P, ctypes.POINTER(_I), _P]),
+    "gp2d_ozaki_prepare": (_I, [_P, _I64, _I64, _KP, _I, _I, _P, _P, ctypes.POINTER(_I), _P]),
+    "gp2d_ozaki_nmod_apriori": (_I, [_I64, _KP, _D, _I, _I]),
+    "gp2d_ozaki_prepare_async": (_I, [_P, _I64, _I64, _KP, _D, _I, _I, _P, _P, ctypes.POINTER(_I), _P]),
+    "gp2d_ozaki_prepare_packed": (_I, [_P, _I64, _KP, _D, _I, _I, _P, _P, ctypes.POINTER(_I), _P]),
     "gp2d_ozaki_guard_workspace": (_SZ, [_I64]),
     "gp2d_ozaki_guard": (_I, [_P, _I64, _I64, _I64, _I64, _D, _P, _P, _SZ, _P]),
-    "gp2d_ozaki_error_model": (_D, [_D, _D, _I]),
-    "gp2d_ozaki_guard_bits": (_I, [_D, _D, _D]),
+    "gp2d_ozaki_error_model": (_D, [_D, _D, _I, _I]),
+    "gp2d_ozaki_guard_bits": (_I, [_D, _D, _D, ctypes.POINTER(_I), ctypes.POINTER(_I)]),
     "gp2d_ozaki_kstar_bytes": (_SZ, [_I64, _I64, _I64, _I]),
-    "gp2d_ozaki_kstar": (_I, [_P, _I64, _I64, _P, _I64, _KP, _I, _I64, _P, _SZ, _P]),
+    "gp2d_ozaki_kstar": (_I, [_P, _I64, _I64, _P, _I64, _KP, _I, _I, _I64, _P, _SZ, _P]),
     "gp2d_predict_ozaki_planes_workspace": (_SZ, [_I64, _I64]),
-    "gp2d_predict_ozaki_planes": (_I, [_P, _P, _I, _I64, _P, _P, _I64, _I64, _P, _I64, _KP, _I, _D, _P, _I, _P, _P,
-                                       _P, _I64, _P, _SZ, _P]),
+    "gp2d_predict_ozaki_planes": (_I, [_P, _P, _I, _I, _I64, _P, _P, _I64, _I64, _P, _I64, _KP, _I, _D, _P, _I, _I,
+                                       _P, _P, _P, _I64, _P, _SZ, _P]),
     "gp2d_predict_ozaki_workspace": (_SZ, [_I64, _I64]),
     "gp2d_ozaki_set_skip": (None, [_I]),
     "gp2d_morton_codes": (_I, [_P, _I64, _I, _P, _P, _P]),
@@ -117,8 +117,8 @@ _SIGS = {
     "gp2d_morton_sort": (_I, [_P, _I64, _I, _P, _P, _P, _SZ, _P]),
     "gp2d_gather_rows": (_I, [_P, _P, _I64, _I64, _P, _P]),
     "gp2d_obs_pad": (_I, [_P, _I64, _I64, _I, _P, _P, _P]),
-    "gp2d_predict_ozaki": (_I, [_P, _P, _I, _I64, _P, _P, _I64, _I64, _P, _I64, _KP, _I, _D, _I, _P, _P, _P, _I64,
-                                _P, _SZ, _P]),
+    "gp2d_predict_ozaki": (_I, [_P, _P, _I, _I, _I64, _P, _P, _I64, _I64, _P, _I64, _KP, _I, _D, _I, _P, _P, _P,
+                                _I64, _P, _SZ, _P]),
     "gp2d_lml": (_I, [_P, _I64, _I64, _P, _P, _I64, _P, _P]),
     "gp2d_lml_grad_count": (_I, [_KP]),
     "gp2d_lml_grad_workspace": (_SZ, [_I64]),
@@ -146,6 +146,7 @@ _SIGS = {
     "gp2d_pack_lower_doubles": (_SZ, [_I64]),
     "gp2d_pack_lower": (_I, [_P, _I64, _I64, _P, _I, _P]),
     "gp2d_timing_enable": (None, [_I]),
+    "gp2d_trace_mark": (_I, [_I, _P]),
     "gp2d_timing_read": (_I, [ctypes.POINTER(_D), ctypes.POINTER(_I64), ctypes.POINTER(_D)]),
     "gp2d_last_error": (ctypes.c_char_p, []),
 }

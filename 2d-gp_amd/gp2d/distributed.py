@@ -67,18 +67,19 @@ def broadcast_fit(gp: E.GPFit | None, spec: E.KernelSpec, noise: float, x, devic
         return gp
     dev = torch.device(device)
     status = None
-    wbits = None   # the owner's guard decision (layout=None): −1 = FP64 engine, else the W bits
+    wbits = kbits = None   # the owner's guard decision (layout=None): wbits −1 = FP64 engine
     if layout is None:
         if rank == src:
             g = (gp.extra.get("guard") or {}) if gp is not None else {}
             wb = -1 if g.get("engine") == "f64" else int(g.get("wbits") or 0)
+            kb = int(g.get("kbits") or 0)
             st = 0 if error is None else (1 if isinstance(error, np.linalg.LinAlgError) else 2)
-            vals = [gp.n, gp.n_train, gp.n_pad, st, wb] if error is None else [0, 0, 0, st, 0]
+            vals = [gp.n, gp.n_train, gp.n_pad, st, wb, kb] if error is None else [0, 0, 0, st, 0, 0]
             meta = torch.tensor(vals, dtype=torch.int64).to(dev)
         else:
-            meta = torch.empty(5, dtype=torch.int64, device=dev)
+            meta = torch.empty(6, dtype=torch.int64, device=dev)
         dist.broadcast(meta, src)
-        n, ntr, npad, st, wbits = (int(v) for v in meta.tolist())
+        n, ntr, npad, st, wbits, kbits = (int(v) for v in meta.tolist())
         if st != 0:
             if rank == src:
                 raise error
@@ -132,7 +133,7 @@ def broadcast_fit(gp: E.GPFit | None, spec: E.KernelSpec, noise: float, x, devic
         out = E.GPFit(kernel=spec, noise=float(noise), x=X, n_train=ntr, n_pad=npad, W=W, alpha=alpha, device=dev)
         if wbits is not None and wbits != 0:   # the owner's guard decision, applied as is
             out.extra["guard"] = dict(pending=False, engine="f64" if wbits < 0 else "ozaki",
-                                      wbits=None if wbits < 0 else wbits)
+                                      wbits=None if wbits < 0 else wbits, kbits=None if wbits < 0 else kbits)
     if status is not None and out is not gp:   # the owner's own fit keeps its pending status read
         out.pending = E.pending_status(status, error if rank == src else None)
     return out
@@ -251,7 +252,8 @@ def fit_sharded(spec: E.KernelSpec, x, y, noise: float, device, mode: str = "bca
     g = gp.extra.get("guard") or {}
     if variance == "ozaki" and "ozaki" not in gp.extra and g.get("engine") != "f64":
         # a-priori moduli count (no host sync), at the owner's guard precision
-        E.ozaki_prepare(gp, diag_add=float(noise + jitter), wbits=int(g.get("wbits") or 0))
+        E.ozaki_prepare(gp, diag_add=float(noise + jitter), wbits=int(g.get("wbits") or 0),
+                        kbits=int(g.get("kbits") or 0))
     return gp
 
 

@@ -313,7 +313,8 @@ def pending_status(status: torch.Tensor, err=None) -> tuple:
 # The accuracy the guard holds the int8 variance to: north_star's fp64 posterior gate (1e-10
 # relative), elementwise.
 GUARD_TARGET = 1e-10
-OZAKI_DEFAULT_BITS = 49      # csrc/ozaki.hpp OZ_PW
+OZAKI_DEFAULT_BITS = (49, 45)   # (W, K*) integer bits: csrc/ozaki.hpp OZ_PW, OZ_PB
+OZAKI_MAX_BITS = (60, 50)       # OZ_PW_MAX, OZ_PB_MAX
 # fit(guard=None) default; GP2D_GUARD=0 turns the guard off (dev A/Bs only, tools/runs)
 GUARD_DEFAULT = os.environ.get("GP2D_GUARD", "1") != "0"
 
@@ -331,22 +332,25 @@ def _guard_stats(W: torch.Tensor, n: int, ntr: int, npad: int, diag_add: float, 
 def apply_guard(gp: GPFit, vmin: float, wmax: float) -> GPFit:
     """The ozaki engine's accuracy guard, once the fit's statistics are on the
     host: the variance's elementwise error grows as the posterior variance falls against kss,
-    ≈ K·2^(49 − bits)·(kss / v_min)^1.5 (gp2d_ozaki_error_model), with v_min the smallest latent
-    posterior variance at the observations (exact from W).  The W rows get the fewest bits in
-    49..60 that keep the model within GUARD_TARGET — planes re-prepared on the fit's stream when
-    that is more than the default — or, past 60 bits, the fit switches to the FP64 engine.
-    The decision is in gp.extra['guard']: engine, wbits, vmin_over_kss, wmax, est."""
+    ≈ A·2^(49 − wbits)·X^1.5 + B·2^(45 − kbits)·X with X = kss / v_min (gp2d_ozaki_error_model;
+    v_min: the smallest latent posterior variance at the observations, exact from W).  The cheapest
+    W / K* precisions (wbits 49..60, kbits 45..50) that keep the model within GUARD_TARGET are
+    taken — the planes re-prepared on the fit's stream when that is more than the defaults — or,
+    past them, the fit switches to the FP64 engine.  The decision is in gp.extra['guard']:
+    engine, wbits, kbits, vmin_over_kss, wmax, est."""
     g = gp.extra.get("guard")
     if not g or not g.get("pending"):
         return gp
     L = N.lib()
     kss = gp.kernel.kdiag()
-    bits = int(L.gp2d_ozaki_guard_bits(kss, vmin, GUARD_TARGET))
+    wb, kb = ctypes.c_int(0), ctypes.c_int(0)
+    ok = int(L.gp2d_ozaki_guard_bits(kss, vmin, GUARD_TARGET, ctypes.byref(wb), ctypes.byref(kb)))
     g.update(pending=False, vmin_over_kss=vmin / kss, wmax=wmax)
     stream = g.pop("stream", None) or torch.cuda.current_stream(gp.device)
     packed = gp.extra.pop("packed", None)
-    if bits <= 0:   # beyond the emulation's range (or a non-positive v_min): exact FP64 products
-        g.update(engine="f64", wbits=None, est=float(L.gp2d_ozaki_error_model(kss, vmin, 60)))
+    if ok <= 0:   # beyond the emulation's range (or a non-positive v_min): exact FP64 products
+        g.update(engine="f64", wbits=None, kbits=None,
+                 est=float(L.gp2d_ozaki_error_model(kss, vmin, OZAKI_MAX_BITS[0], OZAKI_MAX_BITS[1])))
         gp.extra.pop("ozaki", None)
         if gp.W is None:   # a receiving rank kept only the packed payload
             with torch.cuda.stream(stream):
@@ -357,10 +361,11 @@ def apply_guard(gp: GPFit, vmin: float, wmax: float) -> GPFit:
                 g["event"].record(stream)
             gp.W = W
         return gp
-    g.update(engine="ozaki", wbits=bits, est=float(L.gp2d_ozaki_error_model(kss, vmin, bits)))
-    if bits > OZAKI_DEFAULT_BITS:
+    wbits, kbits = wb.value, kb.value
+    g.update(engine="ozaki", wbits=wbits, kbits=kbits, est=float(L.gp2d_ozaki_error_model(kss, vmin, wbits, kbits)))
+    if (wbits, kbits) != OZAKI_DEFAULT_BITS:
         with torch.cuda.stream(stream):
-            ozaki_prepare(gp, diag_add=g["diag_add"], wbits=bits, packed=packed)
+            ozaki_prepare(gp, diag_add=g["diag_add"], wbits=wbits, kbits=kbits, packed=packed)
             gp.extra.pop("packed", None)
             g["event"] = torch.cuda.Event()
             g["event"].record(stream)
@@ -607,13 +612,14 @@ def fit_batch(problems, variance: str = "f64", jitter: float = 0.0, device=None,
 
 
 def ozaki_prepare(gp: GPFit, diag_add: float | None = None, packed: torch.Tensor | None = None,
-                  wbits: int = 0) -> GPFit:
+                  wbits: int = 0, kbits: int = 0) -> GPFit:
     """Residue planes of W for the INT8 variance engine (once per fit).  With `diag_add`
     (the noise + jitter of K_y's diagonal) the moduli count is the a-priori bound and nothing
     synchronises (gp2d_ozaki_prepare_async); without it, the data-driven count of the
     factor's row bounds (one device → host read).  packed: W as the factor broadcast's packed
     lower block triangle (gp2d_ozaki_prepare_packed, needs diag_add) — gp.W may then be None.
-    wbits: integer bits per W row (0 = the default 49; the accuracy guard's choice, apply_guard)."""
+    wbits / kbits: integer bits per W row and of K* (0 = the defaults 49 / 45; the accuracy guard's
+    choice, apply_guard).  gp.extra['ozaki'] = (residue planes, row scales, moduli count, kbits)."""
     L = N.lib()
     n = gp.n
     wres = torch.empty(int(L.gp2d_ozaki_wres_bytes(n)), dtype=torch.int8, device=gp.device)
@@ -624,16 +630,17 @@ def ozaki_prepare(gp: GPFit, diag_add: float | None = None, packed: torch.Tensor
         if diag_add is None:
             raise ValueError("ozaki_prepare from the packed factor needs diag_add (the a-priori moduli count)")
         N.check(L.gp2d_ozaki_prepare_packed(_ptr(packed), n, ctypes.byref(desc), float(diag_add), int(wbits),
-                                            _ptr(wres), _ptr(rowscale), ctypes.byref(nmod),
+                                            int(kbits), _ptr(wres), _ptr(rowscale), ctypes.byref(nmod),
                                             _stream_handle(gp.device)), "gp2d_ozaki_prepare_packed")
     elif diag_add is not None:
         N.check(L.gp2d_ozaki_prepare_async(_ptr(gp.W), n, n, ctypes.byref(desc), float(diag_add), int(wbits),
-                                           _ptr(wres), _ptr(rowscale), ctypes.byref(nmod),
+                                           int(kbits), _ptr(wres), _ptr(rowscale), ctypes.byref(nmod),
                                            _stream_handle(gp.device)), "gp2d_ozaki_prepare_async")
     else:
-        N.check(L.gp2d_ozaki_prepare(_ptr(gp.W), n, n, ctypes.byref(desc), int(wbits), _ptr(wres), _ptr(rowscale),
+        N.check(L.gp2d_ozaki_prepare(_ptr(gp.W), n, n, ctypes.byref(desc), int(wbits), int(kbits), _ptr(wres),
+                                     _ptr(rowscale),
                                      ctypes.byref(nmod), _stream_handle(gp.device)), "gp2d_ozaki_prepare")
-    gp.extra["ozaki"] = (wres, rowscale, int(nmod.value))
+    gp.extra["ozaki"] = (wres, rowscale, int(nmod.value), int(kbits))
     if packed is not None:
         gp.extra["packed"] = packed   # kept until the guard has decided (it may need more bits, or W)
     return gp
@@ -676,7 +683,7 @@ def kstar_planes(kernel: KernelSpec, x, xg, noise: float, jitter: float = 0.0, c
     npad, n = fit_layout(kernel, ntr, "ozaki")
     chunk = max(128, (int(chunk) + 127) // 128 * 128)
     desc = kernel.desc()
-    nmod = int(L.gp2d_ozaki_nmod_apriori(n, ctypes.byref(desc), float(noise + jitter), 0))
+    nmod = int(L.gp2d_ozaki_nmod_apriori(n, ctypes.byref(desc), float(noise + jitter), 0, 0))
     if nmod <= 0:
         N.check(-1, "gp2d_ozaki_nmod_apriori")
     nbytes = int(L.gp2d_ozaki_kstar_bytes(n, m, chunk, nmod))
@@ -686,7 +693,7 @@ def kstar_planes(kernel: KernelSpec, x, xg, noise: float, jitter: float = 0.0, c
     st = stream if stream is not None else main
     if st is not main:
         st.wait_stream(main)   # the points (and a reused buffer's last reader) are ordered before
-    N.check(L.gp2d_ozaki_kstar(_ptr(X), ntr, npad, _ptr(G), m, ctypes.byref(desc), nmod, chunk, _ptr(bres),
+    N.check(L.gp2d_ozaki_kstar(_ptr(X), ntr, npad, _ptr(G), m, ctypes.byref(desc), nmod, 0, chunk, _ptr(bres),
                                bres.numel(), ctypes.c_void_p(st.cuda_stream)), "gp2d_ozaki_kstar")
     if st is not main:
         # the caching allocator must not hand these blocks to main-stream work (the fit)
@@ -786,7 +793,7 @@ class Predictor:
             mean, var = out
         desc = gp.kernel.desc()
         if self.ozaki and "ozaki" in gp.extra:
-            wres, rowscale, nmod = gp.extra["ozaki"]
+            wres, rowscale, nmod, kbits = gp.extra["ozaki"]
             use_planes = planes is not None and compute_var
             if use_planes and (planes.m != m or planes.n != gp.n or planes.chunk != self.chunk):
                 raise ValueError("K* planes were made for another grid, fit layout or chunk size")
@@ -804,15 +811,15 @@ class Predictor:
             if use_planes:
                 s = torch.cuda.current_stream(gp.device)
                 s.wait_event(planes.event)
-                rc = L.gp2d_predict_ozaki_planes(_ptr(wres), _ptr(rowscale), nmod, gp.n, _ptr(gp.alpha), _ptr(gp.x),
-                                                 gp.n_train, gp.n_pad, _ptr(Gs), m, ctypes.byref(desc),
+                rc = L.gp2d_predict_ozaki_planes(_ptr(wres), _ptr(rowscale), nmod, kbits, gp.n, _ptr(gp.alpha),
+                                                 _ptr(gp.x), gp.n_train, gp.n_pad, _ptr(Gs), m, ctypes.byref(desc),
                                                  _VAR_MODES[var_mode], float(gp.noise), _ptr(planes.bres),
-                                                 planes.nmod, _ptr(mean), _ptr(var), po, self.chunk, _ptr(self.work),
+                                                 planes.nmod, 0, _ptr(mean), _ptr(var), po, self.chunk, _ptr(self.work),
                                                  self.wbytes, ctypes.c_void_p(s.cuda_stream))
                 if rc != -3:   # −3: the fit needs more moduli than the planes carry → inline K*
                     N.check(rc, "gp2d_predict_ozaki_planes")
             if rc == -3:
-                N.check(L.gp2d_predict_ozaki(_ptr(wres), _ptr(rowscale), nmod, gp.n, _ptr(gp.alpha), _ptr(gp.x),
+                N.check(L.gp2d_predict_ozaki(_ptr(wres), _ptr(rowscale), nmod, kbits, gp.n, _ptr(gp.alpha), _ptr(gp.x),
                                              gp.n_train, gp.n_pad, _ptr(Gs), m, ctypes.byref(desc),
                                              _VAR_MODES[var_mode], float(gp.noise), int(bool(compute_var)),
                                              _ptr(mean), _ptr(var), po, self.chunk, _ptr(self.work), self.wbytes,
@@ -831,11 +838,12 @@ def predict(gp: GPFit, xg, var_mode: str = "latent", compute_var: bool = True, c
 
 def note_guard(stats: dict | None, gp: GPFit):
     """Record a checked fit's accuracy-guard decision in a job stream's `stats` (stats['guard'],
-    one dict per job in job order: engine, wbits, vmin_over_kss, wmax, est)."""
+    one dict per job in job order: engine, wbits, kbits, vmin_over_kss, wmax, est)."""
     if stats is not None:
         g = gp.extra.get("guard")
         stats.setdefault("guard", []).append(
-            {k: v for k, v in g.items() if k in ("engine", "wbits", "vmin_over_kss", "wmax", "est")} if g else None)
+            {k: v for k, v in g.items() if k in ("engine", "wbits", "kbits", "vmin_over_kss", "wmax", "est")}
+            if g else None)
 
 
 def note_fit_issued(stats: dict | None):

@@ -394,7 +394,7 @@ def extra_readings_n1(args, spec, xt, yt, noise, xg, m_all):
                          "steps": args.dropin_steps,
                          "api": "krig.Krig(kind, l_df, noise).fit(X, obs).predict_device(grid)",
                          "variance_engine": k.variance if k.variance == "f64" else g.get("engine", "ozaki"),
-                         "guard_wbits": g.get("wbits")}
+                         "guard_bits": [g.get("wbits"), g.get("kbits")]}
     return out
 
 
@@ -577,9 +577,14 @@ def main():
     stats.clear()
     if comm is not None:
         comm.clear()
+    marks = os.environ.get("GP2D_TRACE_MARKS") == "1"   # bracket the timed region in a kernel trace
     barrier(ws)
     t0 = time.perf_counter()
+    if marks:
+        E.N.lib().gp2d_trace_mark(1, E._stream_handle(dev))
     run_jobs(args.steps, t0)
+    if marks:
+        E.N.lib().gp2d_trace_mark(2, E._stream_handle(dev))
     barrier(ws)
     t1 = time.perf_counter()
     kms, klaunch, kflops = E.timing_read()

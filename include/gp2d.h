@@ -174,44 +174,47 @@ int gp2d_predict(const double* W, int64_t n, int64_t ldw, const double* alpha,
  * gp2d_ozaki_prepare: once per fit, W → residue planes wres (≤ gp2d_ozaki_wres_bytes(n)
  * bytes) and per-row scales rowscale (n doubles); *nmod_out receives the number of moduli
  * the data needs (from per-row L1 bounds of the scaled W; synchronises the stream once).
- * wbits: integer bits per scaled W row, 0 (the default, 49) or 49..60 (the accuracy guard's
- * choice, gp2d_ozaki_guard_bits; more bits cost about one modulus per 8).
- * gp2d_ozaki_nmod(n) is the worst-case count used for sizing (at 60 bits).              */
+ * wbits / kbits: integer bits per scaled W row, 0 (the default, 49) or 49..60, and of the scaled
+ * K*, 0 (45) or 45..50 — the accuracy guard's choice (gp2d_ozaki_guard_bits; more bits cost about
+ * one modulus per 8).  The row scales carry wbits; every later call that makes or reads K* planes
+ * for this fit takes its kbits.  gp2d_ozaki_nmod(n) is the worst-case count (60 + 50 bits), used
+ * for sizing.                                                                            */
 int    gp2d_ozaki_nmod(int64_t n);
 size_t gp2d_ozaki_wres_bytes(int64_t n);
-int    gp2d_ozaki_prepare(const double* W, int64_t n, int64_t ldw, const gp2d_kernel_t* k, int wbits,
+int    gp2d_ozaki_prepare(const double* W, int64_t n, int64_t ldw, const gp2d_kernel_t* k, int wbits, int kbits,
                           int8_t* wres, double* rowscale, int* nmod_out, void* stream);
 /* gp2d_ozaki_prepare_async: as gp2d_ozaki_prepare without the host round trip — the moduli
- * count is gp2d_ozaki_nmod_apriori(n, k, diag_add, wbits) (diag_add = the noise + jitter on K_y's
+ * count is gp2d_ozaki_nmod_apriori(n, k, diag_add, wbits, kbits) (diag_add = the noise + jitter on K_y's
  * diagonal), which bounds the data-driven count for any fit of these hyperparameters.     */
 int    gp2d_ozaki_prepare_async(const double* W, int64_t n, int64_t ldw, const gp2d_kernel_t* k,
-                                double diag_add, int wbits, int8_t* wres, double* rowscale, int* nmod_out,
-                                void* stream);
+                                double diag_add, int wbits, int kbits, int8_t* wres, double* rowscale,
+                                int* nmod_out, void* stream);
 /* gp2d_ozaki_prepare_packed: gp2d_ozaki_prepare_async reading W from the factor broadcast's
  * payload (gp2d_pack_lower's packed lower block triangle, gp2d_pack_lower_doubles(n) doubles):
  * a rank that receives a job's factor only to predict with the ozaki engine builds its planes
  * without unpacking W into an n×n matrix.  Same planes and row scales, bit for bit.          */
 int    gp2d_ozaki_prepare_packed(const double* packed, int64_t n, const gp2d_kernel_t* k, double diag_add,
-                                 int wbits, int8_t* wres, double* rowscale, int* nmod_out, void* stream);
-/* Accuracy guard.  The int8 engine rounds each W row to `wbits` integer bits (0 = the default
- * 49; up to 60): the variance kss − ‖W k*‖² then carries an elementwise relative error that
- * grows where the posterior variance is small against kss — at the observations.
+                                 int wbits, int kbits, int8_t* wres, double* rowscale, int* nmod_out, void* stream);
+/* Accuracy guard.  The int8 engine rounds each W row to `wbits` integer bits and K* to `kbits`:
+ * the variance kss − ‖W k*‖² then carries an elementwise relative error that grows where the
+ * posterior variance is small against kss — at the observations.
  * gp2d_ozaki_guard: stats_dev[0] = the smallest latent posterior variance at the observed
  *   training components, δ − δ²·(K_y⁻¹)_ii with (K_y⁻¹)_ii = Σ_k W_ki² and δ = diag_add (the
  *   noise + jitter on K_y's diagonal; GP_laser.py:114-115; δ ≤ 0 gives stats_dev[0] ≤ 0, which the
  *   policy sends to the FP64 engine), stats_dev[1] = max |W_ik|
  *   (device doubles; workspace gp2d_ozaki_guard_workspace(n) bytes; fixed reduction order).
- * gp2d_ozaki_error_model: the modelled elementwise error K·2^(49 − wbits)·(kss/v_min)^1.5
- *   (K fitted to full-grid measurements).
- * gp2d_ozaki_guard_bits: the smallest wbits in 49..60 whose modelled error is ≤ target (the
- *   north-star gate is 1e-10), 0 if none (use the FP64 engine, gp2d_predict), −1 on bad input.
+ * gp2d_ozaki_error_model: the modelled elementwise error A·2^(49 − wbits)·X^1.5 + B·2^(45 − kbits)·X,
+ *   X = kss/v_min (A, B fitted to full-grid measurements).
+ * gp2d_ozaki_guard_bits: the cheapest (*wbits, *kbits) (fewest total bits) whose modelled error is
+ *   ≤ target (the north-star gate is 1e-10): returns 1; 0 if none (use the FP64 engine,
+ *   gp2d_predict); −1 on bad input.
  * Replaces nothing in the reference (its variance is fp64 throughout, GP_laser.py:128-131): it
  * keeps the emulation inside the reference's accuracy contract for any hyperparameters.     */
 size_t gp2d_ozaki_guard_workspace(int64_t n);
 int    gp2d_ozaki_guard(const double* W, int64_t n, int64_t ldw, int64_t ntr, int64_t npad, double diag_add,
                         double* stats_dev, void* work, size_t work_bytes, void* stream);
-double gp2d_ozaki_error_model(double kss, double vmin, int wbits);
-int    gp2d_ozaki_guard_bits(double kss, double vmin, double target);
+double gp2d_ozaki_error_model(double kss, double vmin, int wbits, int kbits);
+int    gp2d_ozaki_guard_bits(double kss, double vmin, double target, int* wbits, int* kbits);
 size_t gp2d_predict_ozaki_workspace(int64_t n, int64_t chunk);
 /* The variance GEMMs skip K slabs (64 training components) whose K* tile is exactly zero for
  * a 256-row grid tile — exact, such slabs add nothing.  gp2d_ozaki_set_skip(0) runs them
@@ -243,7 +246,7 @@ int    gp2d_obs_pad(const double* y, int64_t ntr, int64_t npad, int bd, const in
  * out_order (optional, int64[m]): xg is the caller's grid permuted (gp2d_morton_sort's sorted
  * points, so K*'s zero tiles cluster); the outputs of point j go to position out_order[j] of
  * mean / var — the caller's own order, scattered in the epilogue.  NULL: xg's order.      */
-int    gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int nmod, int64_t n,
+int    gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int nmod, int kbits, int64_t n,
                           const double* alpha, const double* xtr, int64_t ntr, int64_t ntr_pad,
                           const double* xg, int64_t m, const gp2d_kernel_t* k,
                           int var_mode, double noise, int compute_var,
@@ -261,19 +264,19 @@ int    gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int nmod, 
  * gp2d_predict_ozaki_planes: gp2d_predict_ozaki (compute_var = 1) with the variance GEMMs
  *   reading those planes; the mean K*α is evaluated in fp64 as in gp2d_predict_ozaki, so
  *   both outputs are bit-identical to it.  Returns −3 if the fit needs more moduli than
- *   nmod_b (the caller regenerates).
+ *   nmod_b, or another K* precision than the planes' kbits_b (the caller regenerates).
  * Replaces the same reference calls as gp2d_predict_ozaki (compute_Ks + getMean + the
  * variance diagonal, GP_laser.py:122-136).                                              */
-int    gp2d_ozaki_nmod_apriori(int64_t n, const gp2d_kernel_t* k, double diag_add, int wbits);
+int    gp2d_ozaki_nmod_apriori(int64_t n, const gp2d_kernel_t* k, double diag_add, int wbits, int kbits);
 size_t gp2d_ozaki_kstar_bytes(int64_t n, int64_t m, int64_t chunk, int nmod);
 int    gp2d_ozaki_kstar(const double* xtr, int64_t ntr, int64_t ntr_pad, const double* xg, int64_t m,
-                        const gp2d_kernel_t* k, int nmod, int64_t chunk, int8_t* bres, size_t bres_bytes,
-                        void* stream);
+                        const gp2d_kernel_t* k, int nmod, int kbits, int64_t chunk, int8_t* bres,
+                        size_t bres_bytes, void* stream);
 size_t gp2d_predict_ozaki_planes_workspace(int64_t n, int64_t chunk);
-int    gp2d_predict_ozaki_planes(const int8_t* wres, const double* rowscale, int nmod, int64_t n,
+int    gp2d_predict_ozaki_planes(const int8_t* wres, const double* rowscale, int nmod, int kbits, int64_t n,
                                  const double* alpha, const double* xtr, int64_t ntr, int64_t ntr_pad,
                                  const double* xg, int64_t m, const gp2d_kernel_t* k, int var_mode,
-                                 double noise, const int8_t* bres, int nmod_b, double* mean, double* var,
+                                 double noise, const int8_t* bres, int nmod_b, int kbits_b, double* mean, double* var,
                                  const int64_t* out_order, int64_t chunk, void* work, size_t work_bytes,
                                  void* stream);
 
@@ -406,6 +409,10 @@ int gp2d_status_flip(int* status, int count, void* stream);
  * synchronises those events and returns the summed milliseconds, the launch
  * count and the summed algorithmic flop count, then resets the counters.        */
 void gp2d_timing_enable(int on);
+/* gp2d_trace_mark: one empty kernel (trace_mark_kernel) on `stream` — a marker a rocprofv3 kernel
+ * trace shows, so a tool can list the kernels that ran between two of them (bench.py's timed
+ * region, GP2D_TRACE_MARKS=1).                                                              */
+int  gp2d_trace_mark(int tag, void* stream);
 int  gp2d_timing_read(double* total_ms, int64_t* launches, double* flops);
 
 const char* gp2d_last_error(void);

@@ -57,13 +57,13 @@ int main() {
   for (int t = 0; t < 2; ++t) for (int d = 0; d < 3; ++d) ard.ls[t][d] = 1.0 + t + d;
   EXPECT(gp2d_block_dim(&ard) == 1 && std::fabs(gp2d_kernel_diag(&ard) - 1.0) < 1e-15);
   for (int64_t n : {256, 1024, 8192, 32768}) {
-    EXPECT(gp2d_ozaki_nmod(n) > 0 && gp2d_ozaki_nmod(n) <= 16);
+    EXPECT(gp2d_ozaki_nmod(n) > 0 && gp2d_ozaki_nmod(n) <= 20);
     EXPECT(gp2d_ozaki_wres_bytes(n) > 0);
     EXPECT(gp2d_potrf_inv_workspace(n) > 0 && gp2d_trtri_workspace(n) > 0 && gp2d_potrs_workspace(n) > 0);
     EXPECT(gp2d_predict_workspace(n, 8192, 2) > 0 && gp2d_predict_ozaki_workspace(n, 8192) > 0);
     EXPECT(gp2d_lml_grad_workspace(n) > 0 && gp2d_predict_ozaki_planes_workspace(n, 8192) > 0);
-    const int a = gp2d_ozaki_nmod_apriori(n, &df, 0.0025, 0);
-    EXPECT(a > 0 && a <= 16);
+    const int a = gp2d_ozaki_nmod_apriori(n, &df, 0.0025, 0, 0);
+    EXPECT(a > 0 && a <= 20 && a <= gp2d_ozaki_nmod(n));
   }
   EXPECT(gp2d_potrf_inv_workspace(128) == 0);
   EXPECT(gp2d_ozaki_kstar_bytes(8192, 65536, 8192, 12) > 0);
@@ -123,39 +123,43 @@ int main() {
   // ---- Ozaki engine
   int nmod = 0;
   int8_t* wb = reinterpret_cast<int8_t*>(buf);
-  EXPECT_ERR(gp2d_ozaki_prepare(buf, 384, 384, &df, 0, wb, buf, &nmod, nullptr));               // n not ×256
-  EXPECT_ERR(gp2d_ozaki_prepare_async(buf, 384, 384, &df, 0.0025, 0, wb, buf, &nmod, nullptr));
+  EXPECT_ERR(gp2d_ozaki_prepare(buf, 384, 384, &df, 0, 0, wb, buf, &nmod, nullptr));               // n not ×256
+  EXPECT_ERR(gp2d_ozaki_prepare_async(buf, 384, 384, &df, 0.0025, 0, 0, wb, buf, &nmod, nullptr));
   gp2d_kernel_t mbad = mixed; mbad.ratio = 1.5;                                              // ratio ∉ [0, 1]
-  EXPECT_ERR(gp2d_ozaki_prepare_async(buf, 256, 256, &mbad, 0.0025, 0, wb, buf, &nmod, nullptr));
+  EXPECT_ERR(gp2d_ozaki_prepare_async(buf, 256, 256, &mbad, 0.0025, 0, 0, wb, buf, &nmod, nullptr));
   mbad.ratio = -0.1;
-  EXPECT_ERR(gp2d_ozaki_prepare(buf, 256, 256, &mbad, 0, wb, buf, &nmod, nullptr));
-  EXPECT_ERR(gp2d_ozaki_prepare_async(buf, 256, 256, &ard, 0.0025, 0, wb, buf, &nmod, nullptr)); // vector only
-  EXPECT(gp2d_ozaki_nmod_apriori(256, &mbad, 0.0025, 0) < 0);
-  EXPECT(gp2d_ozaki_nmod_apriori(256, &df, 0.0025, 61) < 0 && gp2d_ozaki_nmod_apriori(256, &df, 0.0025, 48) < 0);
-  EXPECT_ERR(gp2d_ozaki_prepare_async(buf, 256, 256, &df, 0.0025, 61, wb, buf, &nmod, nullptr));  // wbits
-  EXPECT(gp2d_ozaki_nmod_apriori(8192, &df, 0.0025, 60) > gp2d_ozaki_nmod_apriori(8192, &df, 0.0025, 49));
-  EXPECT(gp2d_ozaki_nmod_apriori(8192, &df, 0.0025, 60) <= gp2d_ozaki_nmod(8192));   // the workspace covers it
+  EXPECT_ERR(gp2d_ozaki_prepare(buf, 256, 256, &mbad, 0, 0, wb, buf, &nmod, nullptr));
+  EXPECT_ERR(gp2d_ozaki_prepare_async(buf, 256, 256, &ard, 0.0025, 0, 0, wb, buf, &nmod, nullptr)); // vector only
+  EXPECT(gp2d_ozaki_nmod_apriori(256, &mbad, 0.0025, 0, 0) < 0);
+  EXPECT(gp2d_ozaki_nmod_apriori(256, &df, 0.0025, 61, 0) < 0 && gp2d_ozaki_nmod_apriori(256, &df, 0.0025, 48, 0) < 0);
+  EXPECT(gp2d_ozaki_nmod_apriori(256, &df, 0.0025, 0, 51) < 0 && gp2d_ozaki_nmod_apriori(256, &df, 0.0025, 0, 44) < 0);
+  EXPECT_ERR(gp2d_ozaki_prepare_async(buf, 256, 256, &df, 0.0025, 61, 0, wb, buf, &nmod, nullptr));  // wbits
+  EXPECT_ERR(gp2d_ozaki_prepare_async(buf, 256, 256, &df, 0.0025, 0, 51, wb, buf, &nmod, nullptr));  // kbits
+  EXPECT(gp2d_ozaki_nmod_apriori(8192, &df, 0.0025, 60, 50) > gp2d_ozaki_nmod_apriori(8192, &df, 0.0025, 49, 45));
+  EXPECT(gp2d_ozaki_nmod_apriori(8192, &df, 0.0025, 60, 50) <= gp2d_ozaki_nmod(8192));   // the workspace covers it
   // the accuracy guard's policy (host arithmetic only)
-  EXPECT(gp2d_ozaki_guard_bits(0.04, 0.04 * 1.2e-3, 1e-10) == 49);
-  EXPECT(gp2d_ozaki_guard_bits(0.04, 0.04 * 6e-5, 1e-10) > 52 && gp2d_ozaki_guard_bits(0.04, 0.04 * 6e-5, 1e-10) <= 60);
-  EXPECT(gp2d_ozaki_guard_bits(0.04, 0.04 * 1e-7, 1e-10) == 0 && gp2d_ozaki_guard_bits(0.04, 0.0, 1e-10) == 0);
-  EXPECT(gp2d_ozaki_guard_bits(0.04, 0.01, 0.0) == -1);
-  EXPECT(gp2d_ozaki_error_model(0.04, 0.001, 50) < gp2d_ozaki_error_model(0.04, 0.001, 49));
+  int gw = 0, gk = 0;   // the bench's own setting keeps the defaults; a hard one needs both raised
+  EXPECT(gp2d_ozaki_guard_bits(0.04, 0.04 * 1.2e-3, 1e-10, &gw, &gk) == 1 && gw == 49 && gk == 45);
+  EXPECT(gp2d_ozaki_guard_bits(0.04, 0.04 * 6e-5, 1e-10, &gw, &gk) == 1 && gw > 52 && gk > 45 && gw <= 60 && gk <= 50);
+  EXPECT(gp2d_ozaki_guard_bits(0.04, 0.04 * 1e-7, 1e-10, &gw, &gk) == 0 && gp2d_ozaki_guard_bits(0.04, 0.0, 1e-10, &gw, &gk) == 0);
+  EXPECT(gp2d_ozaki_guard_bits(0.04, 0.01, 0.0, &gw, &gk) == -1 && gp2d_ozaki_guard_bits(0.04, 0.01, 1e-10, nullptr, &gk) == -1);
+  EXPECT(gp2d_ozaki_error_model(0.04, 0.001, 50, 45) < gp2d_ozaki_error_model(0.04, 0.001, 49, 45));
+  EXPECT(gp2d_ozaki_error_model(0.04, 0.001, 49, 46) < gp2d_ozaki_error_model(0.04, 0.001, 49, 45));
   EXPECT(gp2d_ozaki_guard_workspace(8192) > 0 && gp2d_ozaki_guard_workspace(0) == 0);
   EXPECT_ERR(gp2d_ozaki_guard(buf, 256, 256, 200, 128, 0.0025, buf, buf, 16, nullptr));   // workspace
   EXPECT_ERR(gp2d_ozaki_guard(buf, 256, 256, 200, 128, 0.0025, buf, buf, 1 << 20, nullptr)); // ntr > npad
   EXPECT_ERR(gp2d_ozaki_guard(buf, 256, 256, 100, 128, INFINITY, buf, buf, 1 << 20, nullptr));  // diag_add
   const size_t ow = gp2d_predict_ozaki_workspace(256, 128);
-  EXPECT_ERR(gp2d_predict_ozaki(wb, buf, 12, 256, buf, buf, 100, 128, buf, 10, &df, 0, 0.0, 1, buf, buf, nullptr, 100, buf, ow, nullptr)); // chunk
-  EXPECT_ERR(gp2d_predict_ozaki(wb, buf, 12, 384, buf, buf, 100, 192, buf, 10, &df, 0, 0.0, 1, buf, buf, nullptr, 128, buf, ow, nullptr)); // n
-  EXPECT_ERR(gp2d_predict_ozaki(wb, buf, 12, 256, buf, buf, 100, 128, buf, 10, &df, 0, 0.0, 1, buf, buf, nullptr, 128, buf, ow - 8, nullptr));
-  EXPECT_ERR(gp2d_predict_ozaki(wb, buf, 0, 256, buf, buf, 100, 128, buf, 10, &df, 0, 0.0, 1, buf, buf, nullptr, 128, buf, ow, nullptr)); // nmod
-  EXPECT_ERR(gp2d_predict_ozaki(wb, buf, 17, 256, buf, buf, 100, 128, buf, 10, &df, 0, 0.0, 1, buf, buf, nullptr, 128, buf, ow, nullptr));
-  EXPECT_ERR(gp2d_ozaki_kstar(buf, 100, 128, buf, 10, &df, 12, 100, wb, 1 << 20, nullptr));     // chunk
-  EXPECT_ERR(gp2d_ozaki_kstar(buf, 100, 128, buf, 10, &df, 12, 128, wb, 16, nullptr));          // bres too small
+  EXPECT_ERR(gp2d_predict_ozaki(wb, buf, 12, 0, 256, buf, buf, 100, 128, buf, 10, &df, 0, 0.0, 1, buf, buf, nullptr, 100, buf, ow, nullptr)); // chunk
+  EXPECT_ERR(gp2d_predict_ozaki(wb, buf, 12, 0, 384, buf, buf, 100, 192, buf, 10, &df, 0, 0.0, 1, buf, buf, nullptr, 128, buf, ow, nullptr)); // n
+  EXPECT_ERR(gp2d_predict_ozaki(wb, buf, 12, 0, 256, buf, buf, 100, 128, buf, 10, &df, 0, 0.0, 1, buf, buf, nullptr, 128, buf, ow - 8, nullptr));
+  EXPECT_ERR(gp2d_predict_ozaki(wb, buf, 0, 0, 256, buf, buf, 100, 128, buf, 10, &df, 0, 0.0, 1, buf, buf, nullptr, 128, buf, ow, nullptr)); // nmod
+  EXPECT_ERR(gp2d_predict_ozaki(wb, buf, 17, 0, 256, buf, buf, 100, 128, buf, 10, &df, 0, 0.0, 1, buf, buf, nullptr, 128, buf, ow, nullptr));
+  EXPECT_ERR(gp2d_ozaki_kstar(buf, 100, 128, buf, 10, &df, 12, 0, 100, wb, 1 << 20, nullptr));     // chunk
+  EXPECT_ERR(gp2d_ozaki_kstar(buf, 100, 128, buf, 10, &df, 12, 0, 128, wb, 16, nullptr));          // bres too small
   EXPECT_ERR(gp2d_morton_codes(buf, 10, 4, buf, nullptr, nullptr));                               // dim
-  EXPECT_ERR(gp2d_ozaki_prepare_packed(buf, 200, &df, 0.0025, 0, wb, buf, &nmod, nullptr));     // n not ×128
-  EXPECT_ERR(gp2d_ozaki_prepare_packed(buf, 256, &df, 0.0025, 0, wb, buf, nullptr, nullptr));  // nmod_out
+  EXPECT_ERR(gp2d_ozaki_prepare_packed(buf, 200, &df, 0.0025, 0, 0, wb, buf, &nmod, nullptr));     // n not ×128
+  EXPECT_ERR(gp2d_ozaki_prepare_packed(buf, 256, &df, 0.0025, 0, 0, wb, buf, nullptr, nullptr));  // nmod_out
   int64_t* ib = reinterpret_cast<int64_t*>(buf);
   const size_t sw = gp2d_morton_sort_workspace(100);
   EXPECT(sw > 0 && gp2d_morton_sort_workspace(0) == 0);

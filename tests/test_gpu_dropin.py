@@ -190,6 +190,7 @@ def test_krig_checkpoint_of_jitchol_rescued_fit(tmp_path, variance, monkeypatch)
     if variance == "ozaki":   # the reload reaches the guard's decision again (here: jitter, no noise)
         assert k2.gp.extra["guard"]["engine"] == k.gp.extra["guard"]["engine"]
         assert k2.gp.extra["guard"]["wbits"] == k.gp.extra["guard"]["wbits"]
+        assert k2.gp.extra["guard"]["kbits"] == k.gp.extra["guard"]["kbits"]
         if "ozaki" in k.gp.extra:
             assert k2.gp.extra["ozaki"][2] == k.gp.extra["ozaki"][2]
     mu2, var2 = k2.predict(xg)

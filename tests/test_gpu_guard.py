@@ -50,12 +50,13 @@ def guard_case(golden):
         torch.tensor(xg, device=dev)
 
 
-# (fixture setting index, the guard's expected engine, W bits (None: FP64))
-CASES = [(0, "ozaki", 51), (1, "ozaki", 49), (2, "ozaki", 56)]
+# (fixture setting index, the guard's expected engine, (W bits, K* bits)): the cheapest precisions
+# whose modelled error (gp2d_ozaki_error_model) is within the gate for each setting's statistics
+CASES = [(0, "ozaki", (51, 45)), (1, "ozaki", (49, 45)), (2, "ozaki", (56, 48))]
 
 
-@pytest.mark.parametrize("k,engine,wbits", CASES)
-def test_guarded_default_engine_meets_the_gate(guard_case, k, engine, wbits):
+@pytest.mark.parametrize("k,engine,bits", CASES)
+def test_guarded_default_engine_meets_the_gate(guard_case, k, engine, bits):
     g, x, y, xg = guard_case
     l, nz = (float(v) for v in g["settings"][k])
     spec = E.KernelSpec(kind="df", l_df=l)
@@ -63,7 +64,7 @@ def test_guarded_default_engine_meets_the_gate(guard_case, k, engine, wbits):
     (mu, var), = list(E.krige_jobs([(spec, x, y, nz, xg)], stats=stats))   # the default engine
     dec = stats["guard"][0]
     print(f"l={l} noise={nz}: guard {dec}")
-    assert dec["engine"] == engine and dec["wbits"] == wbits
+    assert dec["engine"] == engine and (dec["wbits"], dec["kbits"]) == bits
     m = xg.shape[0]
     idx = g["idx"]
     mu, var = mu.cpu().numpy(), var.cpu().numpy()
@@ -76,12 +77,32 @@ def test_guarded_default_engine_meets_the_gate(guard_case, k, engine, wbits):
     ev, em = elem_var(var_s, g[f"s{k}_var_refined"]), elem_mean(mu_s, g[f"s{k}_mean_refined"])
     print(f"  var elementwise {ev:.2e} (model {dec['est']:.1e}), mean elementwise {em:.2e}, "
           f"min var/kss {dec['vmin_over_kss']:.2e}")
-    assert ev < GATE and em < GATE
+    # the FP64 engine on the same factor (the training points in the guarded fit's Morton order, so
+    # W and α are the same bits): what an fp64 factor reaches here, and the emulation's own error
+    # against it (the reference's own np.linalg.inv recipe is 2.5e-10 / 1.2e-12 / 1.3e-7 elementwise
+    # from the refined posterior at the three settings, make_golden gen_guard)
+    p = E.morton_order(x)
+    ys = torch.cat([y[:4096][p], y[4096:][p]])
+    gf = E.fit(spec, x[p], ys, nz, variance="f64")
+    mf, vf = (t.cpu().numpy() for t in E.Predictor(gf, 8192)(xg))
+    emu = elem_var(var, vf)   # all 131,072 outputs
+    evf = elem_var(np.concatenate([vf[idx], vf[m + idx]]), g[f"s{k}_var_refined"])
+    emf = elem_mean(np.concatenate([mf[idx], mf[m + idx]]), g[f"s{k}_mean_refined"])
+    print(f"  same factor on the FP64 engine: var elementwise {evf:.2e}, mean elementwise {emf:.2e}; "
+          f"int8 emulation vs it over the full grid {emu:.2e}")
+    assert emu < GATE   # what the guard controls: the emulation within the gate of the exact products
+    if evf < GATE and emf < GATE:   # the gate is reachable in fp64: the guarded engine meets it
+        assert ev < GATE and em < GATE
+    else:
+        # beyond fp64's reach (noise 1e-4: cond(K_y) ≈ 4e6 on these dense tracks, so an fp64 factor's
+        # own rounding moves the posterior by ~cond·2^-53): the guarded engine within the gate of the
+        # FP64 products of the same factor (above), and no worse than them against the refined one
+        assert ev < evf + GATE and em < 1.01 * emf + GATE
 
 
 def test_unguarded_fails_where_the_guard_acts(guard_case):
-    """Without the guard (49 bits) the (5, 1e-4) setting misses the elementwise gate — the
-    guard is what holds it (the same fixture points, the same fit inputs)."""
+    """Without the guard (49 bits) the (5, 1e-4) setting misses the elementwise gate by far more
+    than the FP64 engine does — the guard is what holds it (same fixture points, same inputs)."""
     g, x, y, xg = guard_case
     k = 2
     l, nz = (float(v) for v in g["settings"][k])
@@ -92,7 +113,7 @@ def test_unguarded_fails_where_the_guard_acts(guard_case):
     m, idx = xg.shape[0], g["idx"]
     ev = elem_var(np.concatenate([var[idx], var[m + idx]]), g[f"s{k}_var_refined"])
     print(f"unguarded (5, 1e-4): var elementwise {ev:.2e}")
-    assert ev > GATE
+    assert ev > 5 * GATE
 
 
 def test_guard_keeps_the_headline_at_49_bits(golden):
@@ -102,7 +123,7 @@ def test_guard_keeps_the_headline_at_49_bits(golden):
     gp = E.fit(E.KernelSpec(kind="df", l_df=5.0), np.stack([x1, x2], 1), np.concatenate([u, v]), 0.0025,
                variance="ozaki")
     g = gp.extra["guard"]
-    assert g["engine"] == "ozaki" and g["wbits"] == 49 and gp.extra["ozaki"][2] == 12
+    assert g["engine"] == "ozaki" and (g["wbits"], g["kbits"]) == (49, 45) and gp.extra["ozaki"][2] == 12
     assert 1e-3 < g["vmin_over_kss"] < 1.5e-3 and g["est"] < GATE
 
 
@@ -139,7 +160,8 @@ def test_guard_decision_is_the_same_on_every_path(guard_case):
     E.ozaki_prepare_guarded(d, nz)
     torch.cuda.synchronize()
     for o in (b, c, d):
-        assert o.extra["guard"]["wbits"] == a.extra["guard"]["wbits"] == 56
+        assert (o.extra["guard"]["wbits"], o.extra["guard"]["kbits"]) == (a.extra["guard"]["wbits"],
+                                                                        a.extra["guard"]["kbits"]) == (56, 48)
         assert o.extra["ozaki"][2] == a.extra["ozaki"][2]
         assert torch.equal(o.extra["ozaki"][0], a.extra["ozaki"][0])
         assert torch.equal(o.extra["ozaki"][1], a.extra["ozaki"][1])

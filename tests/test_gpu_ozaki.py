@@ -132,14 +132,14 @@ def test_nmod_apriori_bounds_data_driven(kind, l, noise, jitter):
     x, y = tracks(700, 5)
     ks = E.KernelSpec(kind=kind, l_df=l, l_cf=l * 1.1, ratio=0.5 if kind == "mixed" else 1.0)
     gp = E.fit(ks, x, y, noise=noise, jitter=jitter, variance="ozaki", guard=False)
-    apriori = int(E.N.lib().gp2d_ozaki_nmod_apriori(gp.n, __import__("ctypes").byref(ks.desc()), noise + jitter, 0))
+    apriori = int(E.N.lib().gp2d_ozaki_nmod_apriori(gp.n, __import__("ctypes").byref(ks.desc()), noise + jitter, 0, 0))
     assert gp.extra["ozaki"][2] <= apriori <= gp.extra["ozaki"][2] + 1
     # at every W precision the accuracy guard can pick: the data-driven count (synchronous
     # prepare) never exceeds the a-priori one the engine uses
-    for wb in (49, 53, 57, 60):
-        E.ozaki_prepare(gp, wbits=wb)
-        ap = int(E.N.lib().gp2d_ozaki_nmod_apriori(gp.n, __import__("ctypes").byref(ks.desc()), noise + jitter, wb))
-        assert gp.extra["ozaki"][2] <= ap <= gp.extra["ozaki"][2] + 1, wb
+    for wb, kb in ((49, 45), (53, 45), (57, 48), (60, 50)):
+        E.ozaki_prepare(gp, wbits=wb, kbits=kb)
+        ap = int(E.N.lib().gp2d_ozaki_nmod_apriori(gp.n, __import__("ctypes").byref(ks.desc()), noise + jitter, wb, kb))
+        assert gp.extra["ozaki"][2] <= ap <= gp.extra["ozaki"][2] + 1, (wb, kb)
 
 
 def test_kstar_ahead_too_few_moduli_falls_back_inline():

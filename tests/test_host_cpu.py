@@ -92,13 +92,13 @@ def test_ozaki_rejects_ratio_outside_unit_interval():
     L = N.lib()
     for r in (-0.25, 1.5):
         k = N.vector_kernel_desc(N.KIND_MIXED, 5.0, 5.0, r)
-        assert L.gp2d_ozaki_nmod_apriori(8192, ctypes.byref(k), 0.0025, 0) == -1
+        assert L.gp2d_ozaki_nmod_apriori(8192, ctypes.byref(k), 0.0025, 0, 0) == -1
         nm = ctypes.c_int(0)
         one = ctypes.c_void_p(1)
-        rc = L.gp2d_ozaki_prepare_async(one, 512, 512, ctypes.byref(k), 0.0025, 0, one, one, ctypes.byref(nm), None)
+        rc = L.gp2d_ozaki_prepare_async(one, 512, 512, ctypes.byref(k), 0.0025, 0, 0, one, one, ctypes.byref(nm), None)
         assert rc < 0 and b"ratio" in L.gp2d_last_error()
     k = N.vector_kernel_desc(N.KIND_MIXED, 5.0, 5.0, 0.5)
-    assert L.gp2d_ozaki_nmod_apriori(8192, ctypes.byref(k), 0.0025, 0) > 0
+    assert L.gp2d_ozaki_nmod_apriori(8192, ctypes.byref(k), 0.0025, 0, 0) > 0
 
 
 def test_no_cpu_fallback():
@@ -226,7 +226,7 @@ def test_ozaki_epilogue_reduction_exact():
     [0, 2^32) (K < 2^17), y = v + (v >> 20)·(−(2^20 − 2^20 mod m)) mod 2^32 (v_mad_i32_i24),
     q = hi32(8y · ⌈2^29/m⌉) (v_mul_hi_u32_u24, both operands < 2^24), r = y − q·m gives
     0 ≤ r < m and r ≡ v (mod m)."""
-    moduli = [256, 255, 253, 251, 247, 241, 239, 233, 229, 227, 223, 217, 211, 199, 197, 193]
+    moduli = [256, 255, 253, 251, 247, 241, 239, 233, 229, 227, 223, 217, 211, 199, 197, 193, 191, 181, 179, 173]
     rng = np.random.default_rng(5)
     edges = np.array([0, 1, 2 ** 20 - 1, 2 ** 20, 2 ** 31 - 1, 2 ** 31, 2 ** 32 - 2 ** 15, 2 ** 32 - 1],
                      dtype=np.uint64)
@@ -256,7 +256,7 @@ def test_ozaki_residue_low_bytes_exact():
     (x + 1.5·2^52) − m·q is exact, lies in [2^52, 2^53), and the low byte of its bit pattern is
     the centred residue's two's-complement byte — the byte the int conversion gave
     (csrc/ozaki.hpp's former residue_byte: (int)(x − m·q) & 0xff)."""
-    moduli = [256, 255, 253, 251, 247, 241, 239, 233, 229, 227, 223, 217, 211, 199, 197, 193]
+    moduli = [256, 255, 253, 251, 247, 241, 239, 233, 229, 227, 223, 217, 211, 199, 197, 193, 191, 181, 179, 173]
     rng = np.random.default_rng(7)
     lim = 2.0 ** 51 - 1
     edges = np.array([0.0, 1.0, -1.0, 127.0, -128.0, 128.0, 2.0 ** 45, -2.0 ** 45, 2.0 ** 49 - 1, -(2.0 ** 49),
@@ -354,3 +354,29 @@ def test_fit_batch_rejects_more_than_64_problems():
     with pytest.raises(ValueError, match="at most 64"):
         E.fit_batch([(k, np.zeros((10, 2)), np.zeros(20), 0.01)] * 65)
     assert E.fit_batch([]) == []
+
+
+def test_ozaki_split_residues_of_wide_w_rows_exact():
+    """The W residue kernel above 50 bits (csrc/ozaki.hpp ozaki_w_res_kernel, pw ≤ 60), emulated
+    in fp64: x = xh·2^26 + xl exactly, the centred residues rh, rl by one fma each, and
+    t = rh·(2^26 mod m, centred) + rl reduced once more gives, for every modulus, the residue of
+    x itself (checked against Python's exact integers)."""
+    moduli = [256, 255, 253, 251, 247, 241, 239, 233, 229, 227, 223, 217, 211, 199, 197, 193, 191, 181, 179, 173]
+    rng = np.random.default_rng(11)
+    lim = 2.0 ** 60
+    x = np.concatenate([np.array([0.0, 1.0, -1.0, 2.0 ** 59, -(2.0 ** 59), lim - 2 ** 8, -(lim - 2 ** 8)]),
+                        np.rint(rng.uniform(-lim, lim, 100_000)), np.rint(rng.uniform(-2.0 ** 52, 2.0 ** 52, 20_000))])
+    xh = np.rint(np.ldexp(x, -26))
+    xl = x - np.ldexp(xh, 26)
+    assert np.array_equal(np.ldexp(xh, 26) + xl, x) and np.abs(xl).max() <= 2 ** 25
+    exact = [int(v) for v in x]
+    for m in moduli:
+        c26 = (1 << 26) % m
+        c26 = c26 - m if 2 * c26 > m else c26
+        rh = xh - m * np.rint(xh * (1.0 / m))
+        rl = xl - m * np.rint(xl * (1.0 / m))
+        t = rh * c26 + rl
+        assert np.abs(t).max() <= 128 * 128 + 128
+        r = t - m * np.rint(t * (1.0 / m))       # the final one-part residue: |t| < 2^50
+        ref = np.array([((e % m) + m) % m for e in exact], dtype=np.float64)
+        assert np.array_equal(np.mod(r, m), ref), m

@@ -1,10 +1,12 @@
-"""Ozaki accuracy away from the bench's hyperparameters (dev tool).
+"""Calibration of the ozaki accuracy guard (dev tool).
 
-For each (ℓ, noise) setting at N_train = 4096 (bench tracks, df kernel, full 256² grid):
-the Ozaki engine's variance against the FP64 engine's, elementwise over all 131,072 outputs,
-and the fit statistics a conditioning rule could read (max |W|, the latent variance at the
-training points σ² − σ⁴·(K_y⁻¹)_ii from W's column norms, the moduli count).
-Usage: GP2D_LIB=... python tools/probe_guard.py [l:noise ...]"""
+For each (ℓ, noise) setting at N_train = 4096 (bench tracks, df kernel, full 256² grid) and each
+(W bits, K* bits): the int8 variance against the FP64 engine's on the SAME factor (the training
+points in the ozaki fit's Morton order, so W and α are the same bits) — the emulation error alone,
+elementwise over all 131,072 outputs — beside the guard's statistics and its model
+(gp2d_ozaki_error_model) and decision (gp2d_ozaki_guard_bits).
+Usage: python tools/probe_guard.py [l:noise ...]  (JSON lines on stdout)"""
+import ctypes
 import json
 import os
 import sys
@@ -18,40 +20,35 @@ from gp2d import data as D  # noqa: E402
 from gp2d import engine as E  # noqa: E402
 
 settings = [tuple(float(v) for v in a.split(":")) for a in sys.argv[1:]] or \
-    [(5.0, 0.0025), (12.0, 1e-3), (2.0, 5e-2), (5.0, 1e-4)]
+    [(5.0, 0.0025), (12.0, 1e-3), (2.0, 5e-2), (5.0, 1e-4), (5.0, 5e-4), (8.0, 0.0025), (12.0, 0.0025)]
+BITS = [(49, 45), (46, 45), (52, 45), (56, 45), (49, 48), (49, 50), (53, 48), (56, 48), (60, 50)]
 x1, x2, u, v = D.synthetic_tracks(4096, seed=2016)
 x = torch.tensor(np.stack([x1, x2], 1), device="cuda")
 y = torch.tensor(np.concatenate([u, v]), device="cuda")
 _, _, xg = D.bbox_grid(x1, x2, 256, pad=5.0)
 g = torch.tensor(xg, device="cuda")
-lib = os.path.basename(os.environ.get("GP2D_LIB", "libgp2d.so"))
+L = E.N.lib()
 for l, nz in settings:
     ks = E.KernelSpec(kind="df", l_df=l)
     kss = ks.kdiag()
     t0 = time.time()
-    go = E.fit(ks, x, y, nz, variance="ozaki")
-    mo, vo = E.predict(go, g)
-    W = go.W
-    wmax = float(W.abs().max())
-    rowmax = W.abs().amax(1)
-    cinv = (W * W).sum(0)                           # diag K_y⁻¹ (Morton order, padded tail = 1)
-    ntr, npad = go.n_train, go.n_pad
-    ci = torch.cat([cinv[:ntr], cinv[npad:npad + ntr]])
-    vtrain = nz - nz * nz * ci                     # latent posterior variance at the training points
-    nmod = go.extra["ozaki"][2]
-    del go, W
-    gf = E.fit(ks, x, y, nz, variance="f64")
-    mf, vf = E.predict(gf, g)
+    go = E.fit(ks, x, y, nz, variance="ozaki")           # guarded: its statistics and decision
+    dec = {k: go.extra["guard"][k] for k in ("engine", "wbits", "kbits", "vmin_over_kss", "wmax", "est")}
+    p = go.perm
+    gf = E.fit(ks, x[p], torch.cat([y[:4096][p], y[4096:][p]]), nz, variance="f64")
+    assert torch.equal(gf.W, go.W)
+    mf, vf = (t.cpu().numpy() for t in E.predict(gf, g))
     del gf
-    vo, vf, mo, mf = (t.cpu().numpy() for t in (vo, vf, mo, mf))
-    rel = np.abs(vo - vf) / vf
-    j = int(np.argmax(rel))
-    mfl = 1e-2 * np.max(np.abs(mf))
-    rec = dict(lib=lib, l=l, noise=nz, kss=kss, nmod=nmod, var_elem=float(rel.max()),
-               var_elem_p999=float(np.quantile(rel, 0.999)), var_norm=float(np.max(np.abs(vo - vf)) / np.max(vf)),
-               mean_elem=float(np.max(np.abs(mo - mf) / np.maximum(np.abs(mf), mfl))),
-               min_var_over_kss=float(vf.min() / kss), var_over_kss_at_worst=float(vf[j] / kss),
-               wmax=wmax, wmax_sq_kss=wmax * wmax * kss, rowmax_median=float(rowmax.median()),
-               vtrain_min_over_kss=float(vtrain.min()) / kss, cinv_max=float(ci.max()),
-               neg_var=int((vo <= 0).sum()), nan=int(np.isnan(vo).sum()), s=round(time.time() - t0, 1))
-    print(json.dumps(rec), flush=True)
+    vmin = dec["vmin_over_kss"] * kss
+    for wb, kb in BITS:
+        E.ozaki_prepare(go, diag_add=nz, wbits=wb, kbits=kb)
+        mo, vo = (t.cpu().numpy() for t in E.predict(go, g))
+        rel = np.abs(vo - vf) / vf
+        rec = dict(l=l, noise=nz, kss=kss, wbits=wb, kbits=kb, nmod=go.extra["ozaki"][2],
+                   var_elem=float(rel.max()), var_elem_p999=float(np.quantile(rel, 0.999)),
+                   mean_elem=float(np.max(np.abs(mo - mf) / np.maximum(np.abs(mf), 1e-2 * np.abs(mf).max()))),
+                   model=float(L.gp2d_ozaki_error_model(kss, vmin, wb, kb)), guard=dec,
+                   min_var_over_kss=float(vf.min() / kss), s=round(time.time() - t0, 1))
+        print(json.dumps(rec), flush=True)
+    del go
+    torch.cuda.empty_cache()

@@ -30,13 +30,21 @@ def main():
     key_e = "End_Timestamp" if "End_Timestamp" in rows[0] else "end_timestamp"
     key_n = "Kernel_Name" if "Kernel_Name" in rows[0] else "kernel_name"
     rows.sort(key=lambda r: int(r[key_s]))
+    marks = [int(r[key_s]) for r in rows if "trace_mark_kernel" in r[key_n]]
+    starts = []
     for r in rows:
         if "igemm_nt_mod_kernel" in r[key_n]:
             durs.append((int(r[key_e]) - int(r[key_s])) * 1e-6)
+            starts.append(int(r[key_s]))
     skip_up = warm * per_job
     up_rng = (skip_up, skip_up + up * per_job)
     t_lo = up_rng[1] + warm * per_job
     t_rng = (t_lo, t_lo + b["steps"] * per_job)
+    if len(marks) >= 2:   # bench.py GP2D_TRACE_MARKS=1: the launches that start inside the marks
+        idx = [i for i, t in enumerate(starts) if marks[0] <= t <= marks[1]]
+        if len(idx) != b["steps"] * per_job:
+            print(f"warning: {len(idx)} launches between the marks, expected {b['steps'] * per_job}", file=sys.stderr)
+        t_rng = (idx[0], idx[-1] + 1)
 
     def avg(a, z):
         seg = durs[a:z]

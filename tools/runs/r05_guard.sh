@@ -1,7 +1,7 @@
 #!/bin/bash
-# r05: Ozaki accuracy at (l, noise) settings away from the bench's
-set -eo pipefail
+# r05: calibration data of the ozaki accuracy guard (tools/probe_guard.py), then its GPU tests
+set -o pipefail
 mkdir -p gpurun_out
-for lib in 2d-gp_amd/gp2d/libgp2d.so tools/_p/libgp2d_50_50.so tools/_p/libgp2d_46_45.so; do
-  GP2D_LIB=$lib timeout -k 10 300 python -u tools/probe_guard.py "$@" >> gpurun_out/r05_guard.jsonl
-done
+timeout -k 10 500 python -u tools/probe_guard.py "$@" > gpurun_out/r05_guard_calib.jsonl || exit 1
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_guard.py \
+  tests/test_gpu_order.py tests/test_gpu_ozaki.py > gpurun_out/r05_guard_tests.log 2>&1
