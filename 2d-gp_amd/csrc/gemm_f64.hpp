@@ -365,7 +365,7 @@ inline GemmParams gemm_params() {
 // (k, k+1) stay adjacent.  Every 16×16 tile of C sums its K = 128 in the same order (k = 4ks +
 // lane/16, ks ascending, the first half then the second) whatever R and CB, so all shapes give
 // the same bits.
-// Shapes (measured, tools/microbench/panel_bench.hip): a launch costs ≈ 11 µs even for four
+// Shapes (measured, tools/microbench/panel_bench.hip (git f1195df)): a launch costs ≈ 11 µs even for four
 // workgroups — a workgroup's own 1 Mflop of f64 MFMAs at one wave per SIMD is ≈ 8k cycles — so
 // the column update splits its 128 columns over four workgroups (R = 32, CB = 32; one tile per
 // wave) and the in-place TRSM, whose workgroups must own whole rows, halves the rows (R = 16,

@@ -77,7 +77,7 @@ def side_stream(device=None) -> torch.cuda.Stream:
     broadcast, concurrent settings.  Taken from torch's HIGH-priority pool: HIP maps streams
     onto at most GPU_MAX_HW_QUEUES hardware queues per priority level (4 on the box), and two
     streams that share a queue run in order, so a side stream on the current stream's queue
-    overlaps nothing.  torch's normal-priority pool streams can land there (tools/probe_queues.py:
+    overlaps nothing.  torch's normal-priority pool streams can land there (tools/probe_queues.py (git f1195df):
     pool streams 6 and 10 of 12 did, profiles/r03_queue_aliasing.json); the high-priority pool is
     a different set of queues."""
     return torch.cuda.Stream(device, priority=-1)

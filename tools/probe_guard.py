@@ -21,7 +21,7 @@ from gp2d import engine as E  # noqa: E402
 
 settings = [tuple(float(v) for v in a.split(":")) for a in sys.argv[1:]] or \
     [(5.0, 0.0025), (12.0, 1e-3), (2.0, 5e-2), (5.0, 1e-4), (5.0, 5e-4), (8.0, 0.0025), (12.0, 0.0025)]
-BITS = [(49, 45), (46, 45), (52, 45), (56, 45), (49, 48), (49, 50), (53, 48), (56, 48), (60, 50)]
+BITS = [(49, 45), (50, 45), (52, 45), (56, 45), (49, 48), (49, 50), (53, 48), (56, 48), (60, 50)]
 x1, x2, u, v = D.synthetic_tracks(4096, seed=2016)
 x = torch.tensor(np.stack([x1, x2], 1), device="cuda")
 y = torch.tensor(np.concatenate([u, v]), device="cuda")
