@@ -25,6 +25,9 @@ from . import engine as E
 # GP2D_FORCE_COLLECTIVES=1 (tests only): run the multi-rank code paths (broadcasts, all-gathers,
 # round-robin fits) even at world size 1 — the real RCCL calls on a one-GPU box
 FORCE_COLLECTIVES = os.environ.get("GP2D_FORCE_COLLECTIVES") == "1"
+# GP2D_RECV_UNPACK=1 (measurement only): receivers of a job stream rebuild the full n×n W and
+# prepare from it (the round-4 path) instead of preparing the int8 planes from the packed payload
+RECV_UNPACK = os.environ.get("GP2D_RECV_UNPACK") == "1"
 
 
 def _solo(ws: int) -> bool:
@@ -120,17 +123,23 @@ def broadcast_fit(gp: E.GPFit | None, spec: E.KernelSpec, noise: float, x, devic
         dist.broadcast(X, src)
     if owner_ok:
         out = gp
-    elif planes_only is not None and spec.is_vector and packed.is_cuda:
-        out = E.GPFit(kernel=spec, noise=float(noise), x=X, n_train=ntr, n_pad=npad, W=None, alpha=alpha, device=dev,
-                      n_mat=n)
-        E.ozaki_prepare(out, diag_add=float(planes_only), packed=packed)
+    elif planes_only is not None and spec.is_vector and packed.is_cuda and not RECV_UNPACK:
+        with _timed(comm, "recv_prepare", False, 0, ws, recv=0, device=dev):
+            out = E.GPFit(kernel=spec, noise=float(noise), x=X, n_train=ntr, n_pad=npad, W=None, alpha=alpha,
+                          device=dev, n_mat=n)
+            E.ozaki_prepare(out, diag_add=float(planes_only), packed=packed)
         # the owner's guard statistics arrive in the status block: check() applies the same rule
         out.extra["guard"] = dict(pending=True, diag_add=float(planes_only),
                                   stream=torch.cuda.current_stream(dev))
     else:
-        W = torch.zeros((n, n), dtype=torch.float64, device=dev)   # the strict upper part stays 0
-        _pack_lower(W, n, packed, unpack=True)
-        out = E.GPFit(kernel=spec, noise=float(noise), x=X, n_train=ntr, n_pad=npad, W=W, alpha=alpha, device=dev)
+        with _timed(comm, "recv_prepare", False, 0, ws, recv=0, device=dev):
+            W = torch.zeros((n, n), dtype=torch.float64, device=dev)   # the strict upper part stays 0
+            _pack_lower(W, n, packed, unpack=True)
+            out = E.GPFit(kernel=spec, noise=float(noise), x=X, n_train=ntr, n_pad=npad, W=W, alpha=alpha, device=dev)
+            if planes_only is not None and RECV_UNPACK:   # the round-4 receive path (measurement only)
+                E.ozaki_prepare(out, diag_add=float(planes_only))
+                out.extra["guard"] = dict(pending=True, diag_add=float(planes_only),
+                                          stream=torch.cuda.current_stream(dev))
         if wbits is not None and wbits != 0:   # the owner's guard decision, applied as is
             out.extra["guard"] = dict(pending=False, engine="f64" if wbits < 0 else "ozaki",
                                       wbits=None if wbits < 0 else wbits, kbits=None if wbits < 0 else kbits)

@@ -542,6 +542,10 @@ def fit_batch(problems, variance: str = "f64", jitter: float = 0.0, device=None,
         ntr = X.shape[0]
         if ntr < 1:
             raise ValueError("need at least one training point")
+        ny = y.numel() if isinstance(y, torch.Tensor) else np.asarray(y).size
+        if ny != kernel.block_dim * ntr:   # every problem's shape is checked before any GPU work
+            raise ValueError(f"problem {len(prep)}: observation vector has {ny} entries, "
+                             f"expected {kernel.block_dim * ntr}")
         npad, n = fit_layout(kernel, ntr, variance)
         perm = None
         if variance == "ozaki" and ntr > 1:
@@ -1022,21 +1026,28 @@ def auto_fits_ahead(kernel: KernelSpec, n_train: int, m_grid: int, variance: str
 FIT_BATCH_MAX = 8
 FIT_BATCH_MAX_SMALL = 16        # matrix order ≤ FIT_BATCH_SMALL_N: the chain-bound sizes
 FIT_BATCH_SMALL_N = 2048
-FIT_BATCH_MAX_BYTES = 8 << 30
+FIT_BATCH_MAX_BYTES = 16 << 30   # two batches in flight (batch_ahead: g predicted, g+1 fitted)
+
+
+def fit_problem_bytes(n: int) -> int:
+    """Device bytes one problem of a batched fit holds: its n×n matrix (W in place) and its share
+    of the TRTRI workspace ((n/2 + NB)² doubles) — the estimate of auto_fit_batch and
+    hyper.auto_batch."""
+    return 8 * (n * n + (n // 2 + NB) ** 2)
 
 
 def auto_fit_batch(kernel: KernelSpec, n_train: int, variance: str = "ozaki") -> int:
     """krige_jobs' default batch for back-to-back jobs: up to FIT_BATCH_MAX fits per batched
     factorisation (FIT_BATCH_MAX_SMALL for matrix orders ≤ FIT_BATCH_SMALL_N, whose fit is the
-    diagonal chain's latency) while the batch's matrices stay below FIT_BATCH_MAX_BYTES.
+    diagonal chain's latency) while TWO batches' matrices (batch_ahead keeps the predicted batch
+    and the next one alive) stay below FIT_BATCH_MAX_BYTES.
     Measured (profiles/r04_fit_batch.jsonl): N_train = 1024, 1/2/4/8 fits in 2.27 / 2.56 / 3.20 /
     4.67 ms (2.28 ms each alone); 4096: 8 fits in 64 ms (13.4 each).  Config B's job stream
     (N_train = 1024, profiles/r04_bfit16_ab.jsonl): 8.33–8.38e6 points/s with 8 fits per batch,
     9.39–9.46e6 with 16, 9.24–9.27e6 with 32."""
     _, n = fit_layout(kernel, max(1, int(n_train)), variance)
-    per = 8 * (n * n + (n // 2 + NB) ** 2)
     cap = FIT_BATCH_MAX_SMALL if n <= FIT_BATCH_SMALL_N else FIT_BATCH_MAX
-    return max(1, min(cap, FIT_BATCH_MAX_BYTES // max(per, 1)))
+    return max(1, min(cap, FIT_BATCH_MAX_BYTES // (2 * fit_problem_bytes(n))))
 
 
 def _job_groups(jobs, b, variance):

@@ -282,8 +282,7 @@ def auto_batch(kernel: E.KernelSpec, x, n_settings: int, concurrent=None) -> int
     if concurrent is not None or n_settings < 2:
         return 1
     npad, n = E.fit_layout(kernel, E._point_count(x, kernel.input_dim))
-    per = 8 * (n * n + (n // 2 + 128) ** 2)
-    return max(1, min(BATCH_MAX, n_settings, BATCH_MAX_BYTES // max(per, 1)))
+    return max(1, min(BATCH_MAX, n_settings, BATCH_MAX_BYTES // E.fit_problem_bytes(n)))
 
 
 def _sweep_batched(kernel, x, y, settings, base, mine, jitter, device, eval_gradient, bsz, vals, grads):

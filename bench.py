@@ -608,9 +608,10 @@ def main():
     comm_out = None
     if cfg["mode"] == "rr" and comm is not None:
         # every rank receives (or sends) every job's factor: bytes and HIP-event ms per job
-        comm_out = comm_block(comm, ("bcast",), args.steps, ws, dev)
+        comm_out = comm_block(comm, ("bcast", "recv_prepare"), args.steps, ws, dev)
         comm_out["what"] = ("per timed job, MAX over ranks: the job's factor broadcast from its fitting rank (packed "
-                            "W + alpha + X_train + the status block), RCCL on the comm stream under the predict")
+                            "W + alpha + X_train + the status block), RCCL on the comm stream under the predict; "
+                            "recv_prepare: a receiving rank's int8 planes from the packed payload (no bytes)")
 
     # one job alone (unpipelined, its grid sharded over the ranks; at N > 1 fitted on rank 0 and
     # broadcast): the single-job reading beside the job-stream value

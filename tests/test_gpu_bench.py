@@ -79,6 +79,9 @@ def test_bench_two_ranks_default_contract():
     n = 2 * 256   # padded matrix order at N_train = 256 (ozaki layout)
     # each rank fits (and sends) every other job's factor and receives the rest
     assert cb["bytes_recv_per_job_max"] + cb["bytes_sent_per_job_max"] >= 8 * n * n // 2
+    # a rank prepares the int8 planes of the jobs it receives (every other one) from the payload
+    rp = d["comm"]["recv_prepare"]
+    assert rp["calls_per_job"] == 0.5 and rp["ms_per_job_max_over_ranks"] > 0 and rp["bytes_recv_per_job_max"] == 0
     dc = sj["distributed_fit"]["comm"]
     assert dc["panel_bcast"]["calls_per_job"] >= 1 and dc["w_allgather"]["calls_per_job"] == 1
 

@@ -23,7 +23,7 @@ for r in sorted(inside, key=lambda r: int(r[ks])):
     a = agg.setdefault(n, [0, 0])
     a[0] += 1
     a[1] += int(r[ke]) - int(r[ks])
-foreign = {n: c for n, (c, _) in agg.items() if not (n.split()[-1].startswith("gp2d::") or "__amd_rocclr" in n)}
+foreign = {n: c for n, (c, _) in agg.items() if not ("gp2d::" in n or "__amd_rocclr" in n)}
 out = {"window_ms": (t1 - t0) / 1e6, "kernels": {n: {"calls": c, "busy_ms": d / 1e6} for n, (c, d) in agg.items()},
        "non_engine_kernels": foreign}
 print(json.dumps(out, indent=1))
