@@ -26,6 +26,16 @@
 #pragma once
 #include "ozaki.hpp"
 
+// Schedule variants (tools/microbench/igemm_bench.hip builds them; the product uses the defaults):
+//   IGPP_DMA   0: 2 DMA pieces in each read interval; 1: 1 in M1 (beside its 8 reads), 3 in M2
+//   IGPP_PRIO  0: none; 1: s_setprio 1 around each MFMA cluster; 2: s_setprio 1 for G1 throughout
+#ifndef IGPP_DMA
+#define IGPP_DMA 0
+#endif
+#ifndef IGPP_PRIO
+#define IGPP_PRIO 0
+#endif
+
 namespace gp2d {
 
 __global__ __launch_bounds__(512, 1) void igemm_pp_kernel(const int8_t* __restrict__ A, const int8_t* __restrict__ B,
@@ -74,11 +84,12 @@ __global__ __launch_bounds__(512, 1) void igemm_pp_kernel(const int8_t* __restri
     for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = i4v{bias, bias, bias, bias};
 
   const int drow = lane >> 2, dchunk = lane & 3;
-  auto issue_a = [&](int ks, int st) {   // this wave's 2 A pieces (rows 32·wid .. +31) of slab ks
+  // this wave's A pieces h0 .. h1−1 (rows 32·wid + 16h .. +15) of slab ks
+  auto issue_a = [&](int ks, int st, int h0 = 0, int h1 = 2) {
     const int8_t* Ag = Ap + (int64_t)ks * I_OP;
     int8_t* As = smem + st * STG;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = h0; h < h1; ++h) {
       const int row = (wid * 2 + h) * 16 + drow;
       __builtin_amdgcn_global_load_lds((const void*)(Ag + row * IBK + 16 * swz16(row, dchunk)),
                                        (lds_ptr_t)(As + (wid * 2 + h) * 16 * IBK), 16, 0, 0);
@@ -151,12 +162,14 @@ __global__ __launch_bounds__(512, 1) void igemm_pp_kernel(const int8_t* __restri
     // G1 runs the same body one interval behind G0: its first barrier pairs with the end of
     // G0's first read interval, and G0 makes up the count after the loop
     if (wr == 1) PP_BAR();
+    if (IGPP_PRIO == 2 && wr == 1) __builtin_amdgcn_s_setprio(1);
     PP_SB();
     i4v a0[4], a1[4], bE[4], bO[4];
     auto cycle = [&](int s, i4v (&b)[4]) {
       const int k3 = slab(s + 3), st3 = (s + 3) % NST, st = s % NST;
       // M1: DMA A(s+3); read B(s), A0(s)
-      issue_a(k3, st3);
+      if (IGPP_DMA == 0) issue_a(k3, st3);
+      else issue_a(k3, st3, 0, 1);
       readb(st, b);
       reada(st, 0, a0);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -164,11 +177,14 @@ __global__ __launch_bounds__(512, 1) void igemm_pp_kernel(const int8_t* __restri
       PP_BAR();
       PP_SB();
       // C0
+      if (IGPP_PRIO == 1) __builtin_amdgcn_s_setprio(1);
       mfmas(0, a0, b);
+      if (IGPP_PRIO == 1) __builtin_amdgcn_s_setprio(0);
       PP_SB();
       PP_BAR();
       PP_SB();
       // M2: DMA B(s+3); read A1(s); this wave's pieces of slab s+1 landed (s+2's and s+3's 8 younger)
+      if (IGPP_DMA != 0) issue_a(k3, st3, 1, 2);
       issue_b(k3, st3);
       reada(st, 1, a1);
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_waitcnt vmcnt(8)" ::: "memory");
@@ -176,7 +192,9 @@ __global__ __launch_bounds__(512, 1) void igemm_pp_kernel(const int8_t* __restri
       PP_BAR();
       PP_SB();
       // C1
+      if (IGPP_PRIO == 1) __builtin_amdgcn_s_setprio(1);
       mfmas(1, a1, b);
+      if (IGPP_PRIO == 1) __builtin_amdgcn_s_setprio(0);
       PP_SB();
       PP_BAR();
       PP_SB();

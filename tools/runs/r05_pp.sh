@@ -1,10 +1,11 @@
 #!/bin/bash
-# r05: the int8 GEMM with its wave groups in ping-pong (csrc/igemm_pp.hpp) vs the product kernel,
-# microbench on random residues (triangle + 4096 sampled outputs checked), then dense K = 4096
+# r05: the int8 GEMM with its wave groups in ping-pong (csrc/igemm_pp.hpp; schedule variants
+# IGPP_DMA / IGPP_PRIO) vs the product kernel, microbench on random residues (triangle + 4096
+# sampled outputs checked), then dense K = 4096
 set -o pipefail
 mkdir -p gpurun_out/r05_pp
 cd tools/microbench
-for b in igemm_FULL igemm_PP; do
+for b in ${PP_BINS:-igemm_FULL igemm_PP igemm_PP_D1 igemm_PP_P1 igemm_PP_P2 igemm_PP_D1P2}; do
   timeout -k 10 90 ./$b > ../../gpurun_out/r05_pp/$b.txt 2>&1 || exit 1
   IGEMM_K=4096 timeout -k 10 90 ./$b >> ../../gpurun_out/r05_pp/$b.txt 2>&1 || exit 1
 done
