@@ -9,7 +9,6 @@
 #include "factor.hpp"
 #include "predict.hpp"
 #include "ozaki.hpp"
-#include "igemm_pp.hpp"
 #include "lml.hpp"
 #include "dfact.hpp"
 #include "order.hpp"
@@ -1267,16 +1266,6 @@ int gp2d_ozaki_guard_bits(double kss, double vmin, double target, int* wbits, in
   return 0;   // beyond the int8 engine's precision range: the FP64 engine
 }
 
-// ---- the int8 GEMM's schedule: lockstep (igemm_nt_mod_kernel) or the wave groups in ping-pong
-// (igemm_pp_kernel); GP2D_IGEMM=pp / lockstep overrides (measurement only)
-static bool igemm_pingpong() {
-  static const int v = [] {
-    const char* e = std::getenv("GP2D_IGEMM");
-    return (e && std::string(e) == "pp") ? 1 : 0;
-  }();
-  return v != 0;
-}
-
 // ---- zero-slab skipping: K* block flags → per-B-tile slab lists (ozaki_slab_list_kernel)
 static int g_oz_skip = 1;
 // block flags of one chunk: [cp/64 grid blocks][npad/64 training blocks] bytes
@@ -1376,15 +1365,10 @@ static int predict_ozaki_impl(const int8_t* wres, const double* rowscale, int nm
         const int8_t* Al = wres + (size_t)l0 * n * n;
         const int8_t* Bl = B + (size_t)l0 * bplane;
         uint8_t* Cl = cres + (size_t)l0 * n * ncols;
-        if (igemm_pingpong())
-          igemm_pp_kernel<<<ggrid, 512, 0, s>>>(Al, Bl, Cl, n, (int)n, (int)ncols, (int)n, 1, oc.m[l0],
-                                                (int)(cp / IBN), (int)(ntr_pad / IBK), use_skip ? slist : nullptr,
-                                                use_skip ? scnt : nullptr, zb);
-        else
-          igemm_nt_mod_kernel<256, I_NSTAGE><<<ggrid, 512, 0, s>>>(Al, Bl, Cl, n, (int)n, (int)ncols, (int)n, 1,
-                                                                   oc.m[l0], (int)(cp / IBN), (int)(ntr_pad / IBK),
-                                                                   use_skip ? slist : nullptr,
-                                                                   use_skip ? scnt : nullptr, zb);
+        igemm_nt_mod_kernel<256, I_NSTAGE><<<ggrid, 512, 0, s>>>(Al, Bl, Cl, n, (int)n, (int)ncols, (int)n, 1, oc.m[l0],
+                                                                 (int)(cp / IBN), (int)(ntr_pad / IBK),
+                                                                 use_skip ? slist : nullptr, use_skip ? scnt : nullptr,
+                                                                 zb);
         GP2D_CHECK(check_launch("igemm_nt_mod_kernel"));
       }
       if (e0) {

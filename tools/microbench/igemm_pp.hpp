@@ -1,6 +1,7 @@
-// INT8 NT GEMM mod m with the two wave groups of a workgroup in ping-pong (DESIGN.md §6 "int8
-// GEMM, ping-pong"): the same product, tile, operand layout, ring and epilogue as
-// igemm_nt_mod_kernel (ozaki.hpp), a different schedule.
+// DEV VARIANT (tools/microbench only; measured in round 5 and not kept — DESIGN.md §6 "int8 GEMM,
+// ping-pong"; profiles/r05_igemm_pp_ab.txt, r05_ppbench_ab.txt): INT8 NT GEMM mod m with the two
+// wave groups of a workgroup in ping-pong — the same product, tile, operand layout, ring and
+// epilogue as igemm_nt_mod_kernel (2d-gp_amd/csrc/ozaki.hpp), a different schedule.
 //
 // igemm_nt_mod_kernel runs its 8 waves in lockstep — every wave issues its DMA pieces and
 // fragment reads, then its MFMAs, then meets the others at the per-slab barrier — so both
@@ -24,7 +25,7 @@
 // end of the list the pieces reload the last slab into the free stage (never read), so the
 // counts stay those of the steady state.
 #pragma once
-#include "ozaki.hpp"
+#include "../../2d-gp_amd/csrc/ozaki.hpp"
 
 // Schedule variants (tools/microbench/igemm_bench.hip builds them; the product uses the defaults):
 //   IGPP_DMA   0: 2 DMA pieces in each read interval; 1: 1 in M1 (beside its 8 reads), 3 in M2
