@@ -47,9 +47,9 @@ def test_fit_batch_settings_bit_identical(ntr, kind, variance):
         g1 = E.fit(k, x, y, nz, variance=variance)
         assert same(gb.W, g1.W) and same(gb.alpha, g1.alpha)
         if variance == "ozaki":
-            _, rb, mb = gb.extra["ozaki"]   # (the residue buffers' tiles above the diagonal are never written)
-            _, r1, m1 = g1.extra["ozaki"]
-            assert mb == m1 and same(rb, r1)
+            _, rb, mb, kb = gb.extra["ozaki"]   # (the residue buffers' tiles above the diagonal are never written)
+            _, r1, m1, k1 = g1.extra["ozaki"]
+            assert mb == m1 and kb == k1 and same(rb, r1)
             xg = np.stack([np.linspace(-5, 65, 300), np.linspace(-5, 50, 300)], 1)
             mu_b, var_b = E.predict(gb, xg)
             mu_1, var_1 = E.predict(g1, xg)

@@ -84,11 +84,11 @@ def test_ozaki_too_few_moduli_poisons_instead_of_wrapping():
     rng = np.random.default_rng(4)
     xg = np.stack([rng.uniform(0, 60, 500), rng.uniform(0, 45, 500)], 1)
     gp = E.fit(E.KernelSpec(kind="df", l_df=5.0), x, y, noise=0.0025, variance="ozaki")
-    wres, rowscale, nmod = gp.extra["ozaki"]
+    wres, rowscale, nmod, kbits = gp.extra["ozaki"]
     assert nmod >= 12
     mu_ok, var_ok = E.predict(gp, xg)
     assert np.isfinite(var_ok.cpu().numpy()).all()
-    gp.extra["ozaki"] = (wres, rowscale, 6)   # ≈ 47 bits of CRT range for ≈ 94-bit products
+    gp.extra["ozaki"] = (wres, rowscale, 6, kbits)   # ≈ 47 bits of CRT range for ≈ 94-bit products
     mu, var = E.predict(gp, xg)
     v = var.cpu().numpy()
     assert np.isnan(v).mean() > 0.5

@@ -3,4 +3,4 @@
 set -o pipefail
 mkdir -p gpurun_out
 out=${OUT:-gpurun_out/r05_gpu_tests.log}
-timeout -k 10 1000 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu "${@:-tests}" > "$out" 2>&1
+timeout -k 10 1000 python -u -m pytest ${PYTEST_X--x} -v --timeout 300 --timeout-method thread -m gpu "${@:-tests}" > "$out" 2>&1
