@@ -170,8 +170,11 @@ def test_guard_decision_is_the_same_on_every_path(guard_case):
     for o in (b, c, d):
         assert (o.extra["guard"]["wbits"], o.extra["guard"]["kbits"]) == (a.extra["guard"]["wbits"],
                                                                         a.extra["guard"]["kbits"]) == (56, 49)
-        nm = a.extra["ozaki"][2]
-        assert o.extra["ozaki"][2] == nm and o.extra["ozaki"][3] == a.extra["ozaki"][3]
-        nb = nm * a.n * a.n   # the planes in use (the buffer holds room for the most moduli)
-        assert torch.equal(o.extra["ozaki"][0][:nb], a.extra["ozaki"][0][:nb])
-        assert torch.equal(o.extra["ozaki"][1], a.extra["ozaki"][1])
+        assert o.extra["ozaki"][2] == a.extra["ozaki"][2] and o.extra["ozaki"][3] == a.extra["ozaki"][3]
+        assert torch.equal(o.extra["ozaki"][1], a.extra["ozaki"][1])   # the W row scales
+    # the residue buffers hold unwritten tiles above the diagonal (and room for more moduli), so
+    # the planes are compared through what they compute: every path's predict, bit for bit
+    mu_a, var_a = E.Predictor(a, 8192)(xg)
+    for o in (b, c, d):
+        mu_o, var_o = E.Predictor(o, 8192)(xg)
+        assert torch.equal(mu_o, mu_a) and torch.equal(var_o, var_a)
