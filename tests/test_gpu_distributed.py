@@ -121,7 +121,8 @@ def test_gp2d_bcast_native_rccl():
         rccl.ncclCommDestroy(comm)
 
 
-def _jobs():
+def _jobs(noises=None):
+    """Five small jobs; noises (optional): per-job noise overrides (the accuracy guard's range)."""
     from gp2d import engine as E
     out = []
     for seed, n, G, kind in [(11, 700, 40, "df"), (12, 700, 44, "mixed"), (13, 900, 40, "df"), (14, 700, 36, "cf"),
@@ -132,11 +133,15 @@ def _jobs():
         GX, GY = np.meshgrid(np.linspace(-5, 65, G), np.linspace(-5, 50, G + 5))
         xg = np.stack([GX.reshape(-1), GY.reshape(-1)], 1)
         spec = E.KernelSpec(kind=kind, l_df=4.0 + seed % 3, l_cf=3.0, ratio=0.5 if kind == "mixed" else 1.0)
-        out.append((spec, x, y, 0.0025, xg))
+        out.append((spec, x, y, 0.0025 if noises is None else noises[len(out)], xg))
     return out
 
 
-def _rr_worker(rank, world, port, out_dir, variance, bad):
+# the guard's three outcomes across the job stream: default bits, more bits, the FP64 engine
+GUARD_NOISES = (0.0025, 2e-5, 0.0025, 0.01, 1e-8)
+
+
+def _rr_worker(rank, world, port, out_dir, variance, bad, noises=None):
     for p in (ROOT, PKG):
         if p not in sys.path:
             sys.path.insert(0, p)
@@ -145,7 +150,7 @@ def _rr_worker(rank, world, port, out_dir, variance, bad):
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from gp2d import distributed as GD
-    jobs = _jobs()
+    jobs = _jobs(noises)
     if bad is not None:   # a non-SPD job (negative noise) owned by rank bad % world
         s, x, y, _, xg = jobs[bad]
         jobs[bad] = (s, x, y, -100.0, xg)
@@ -193,6 +198,32 @@ def test_round_robin_jobs_two_ranks_bit_identical(tmp_path, variance):
         shards_v = [(int(r[i][f"lo{j}"]), int(r[i][f"hi{j}"]), r[i][f"var{j}"]) for i in range(world)]
         assert np.array_equal(GD.assemble_from_shards(m, 2, shards_m), mu), j
         assert np.array_equal(GD.assemble_from_shards(m, 2, shards_v), var), j
+
+
+def test_round_robin_guard_decisions_two_ranks_bit_identical(tmp_path):
+    """The accuracy guard across ranks: jobs whose statistics ask for more W / K* bits (noise
+    2e-5) or for the FP64 engine (1e-8) — the receiving rank applies the owner's status block to
+    the packed payload (re-prepared planes, or W unpacked) — still equal one process bit for bit."""
+    from gp2d import distributed as GD
+    from gp2d import engine as E
+    world = 2
+    _spawn(_rr_worker, world, str(tmp_path), "ozaki", None, GUARD_NOISES)
+    r = [np.load(os.path.join(tmp_path, f"rr{i}.npz")) for i in range(world)]
+    engines = []
+    for j, (spec, x, y, noise, xg) in enumerate(_jobs(GUARD_NOISES)):
+        gp = E.fit(spec, x, y, noise, variance="ozaki")
+        g = gp.extra["guard"]
+        engines.append((g["engine"], g["wbits"], g["kbits"]))
+        mu, var = (t.cpu().numpy() for t in E.Predictor(gp, 1024)(xg))
+        m = xg.shape[0]
+        shards_m = [(int(r[i][f"lo{j}"]), int(r[i][f"hi{j}"]), r[i][f"mean{j}"]) for i in range(world)]
+        shards_v = [(int(r[i][f"lo{j}"]), int(r[i][f"hi{j}"]), r[i][f"var{j}"]) for i in range(world)]
+        assert np.array_equal(GD.assemble_from_shards(m, 2, shards_m), mu), j
+        assert np.array_equal(GD.assemble_from_shards(m, 2, shards_v), var), j
+    print("guard decisions:", engines)
+    # all three outcomes: default bits, more bits, the FP64 engine
+    assert engines[0] == ("ozaki", 49, 45) and engines[4][0] == "f64"
+    assert engines[1][0] == "ozaki" and (engines[1][1], engines[1][2]) != (49, 45)
 
 
 def test_round_robin_jobs_non_spd_raises_on_every_rank(tmp_path):
