@@ -22,7 +22,8 @@ import torch  # noqa: E402
 from gp2d import data as D  # noqa: E402
 from gp2d import engine as E  # noqa: E402
 
-settings = [tuple(float(v) for v in a.split(":")) for a in sys.argv[1:]] or \
+# a setting: l:noise (div-free) or kind:l:noise (kind df | cf | mixed; mixed: l_cf = l, ratio 0.5)
+settings = [tuple(a.split(":")) for a in sys.argv[1:]] or \
     [(5.0, 0.0025), (12.0, 1e-3), (2.0, 5e-2), (5.0, 1e-4), (5.0, 5e-4), (8.0, 0.0025), (12.0, 0.0025), (3.0, 1e-3),
      (2.0, 1e-4)]
 BITS = [(49, 45), (50, 45), (52, 45), (56, 45), (49, 47), (49, 48), (51, 46), (53, 47), (53, 48), (56, 48), (58, 50)]
@@ -32,8 +33,10 @@ y = torch.tensor(np.concatenate([u, v]), device="cuda")
 _, _, xg = D.bbox_grid(x1, x2, 256, pad=5.0)
 g = torch.tensor(xg, device="cuda")
 L = E.N.lib()
-for l, nz in settings:
-    ks = E.KernelSpec(kind="df", l_df=l)
+for st in settings:
+    kind, l, nz = ("df", *st) if len(st) == 2 else st
+    l, nz = float(l), float(nz)
+    ks = E.KernelSpec(kind=kind, l_df=l, l_cf=l, ratio=0.5 if kind == "mixed" else 1.0)
     kss = ks.kdiag()
     t0 = time.time()
     go = E.fit(ks, x, y, nz, variance="ozaki")           # guarded: its statistics and decision
@@ -47,13 +50,13 @@ for l, nz in settings:
     E.ozaki_prepare(go, diag_add=nz, wbits=60, kbits=50)
     mx, vx = (t.cpu().numpy() for t in E.predict(go, g))
     fl = np.abs(vx - vf) / vf
-    print(json.dumps(dict(l=l, noise=nz, kss=kss, wbits=60, kbits=50, ref="f64", var_elem=float(fl.max()),
+    print(json.dumps(dict(kind=kind, l=l, noise=nz, kss=kss, wbits=60, kbits=50, ref="f64", var_elem=float(fl.max()),
                           model=float(L.gp2d_ozaki_error_model(kss, vmin, 60, 50)), guard=dec)), flush=True)
     for wb, kb in BITS:
         E.ozaki_prepare(go, diag_add=nz, wbits=wb, kbits=kb)
         mo, vo = (t.cpu().numpy() for t in E.predict(go, g))
         rel = np.abs(vo - vx) / vx
-        rec = dict(l=l, noise=nz, kss=kss, wbits=wb, kbits=kb, nmod=go.extra["ozaki"][2], ref="max",
+        rec = dict(kind=kind, l=l, noise=nz, kss=kss, wbits=wb, kbits=kb, nmod=go.extra["ozaki"][2], ref="max",
                    var_elem=float(rel.max()), var_elem_p999=float(np.quantile(rel, 0.999)),
                    var_elem_f64=float(np.max(np.abs(vo - vf) / vf)),
                    mean_elem=float(np.max(np.abs(mo - mf) / np.maximum(np.abs(mf), 1e-2 * np.abs(mf).max()))),
