@@ -1279,14 +1279,22 @@ static size_t oz_list_bytes(int64_t n, int64_t chunk) {
   return sizeof(int) * (size_t)(nbj * ks + nbj * (ks / 4 + 1));
 }
 
-size_t gp2d_predict_ozaki_workspace(int64_t n, int64_t chunk) {
-  const int nm = ozaki_nmod_for(n);
-  if (nm <= 0) return 0;
+// workspace of gp2d_predict_ozaki for a fit with nmod moduli (the layout follows nmod)
+static size_t predict_ozaki_ws(int64_t n, int64_t chunk, int nm) {
+  if (nm <= 0 || n <= 0) return 0;
   const int64_t cp = round_up(chunk < 1 ? 1 : chunk, IBN);
   const int64_t ncols = 2 * cp;
   return 2 * (size_t)nm * (size_t)n * (size_t)ncols                        // Bres + Cres planes
          + sizeof(double) * ((size_t)(n / 2 / OZ_KS_T + 1) + (size_t)(n / OZ_CRT_ROWS + 1)) * ncols
          + oz_flag_bytes(n, chunk) + oz_list_bytes(n, chunk);
+}
+static size_t predict_ozaki_planes_ws(int64_t n, int64_t chunk, int nm);
+
+size_t gp2d_predict_ozaki_workspace(int64_t n, int64_t chunk) { return predict_ozaki_ws(n, chunk, ozaki_nmod_for(n)); }
+
+size_t gp2d_predict_ozaki_workspace_nmod(int64_t n, int64_t chunk, int nmod) {
+  if (nmod <= 0 || nmod > ozaki_nmod_for(n)) return 0;
+  return std::max(predict_ozaki_ws(n, chunk, nmod), predict_ozaki_planes_ws(n, chunk, nmod));
 }
 
 void gp2d_ozaki_set_skip(int on) { g_oz_skip = on ? 1 : 0; }
@@ -1403,10 +1411,10 @@ int gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int nmod, int
   GP2D_CHECK(validate_ozaki_kernel(k));
   GP2D_REQUIRE(n == 2 * ntr_pad && n % IBM == 0, "ozaki: n must equal 2·ntr_pad and be a multiple of 256");
   GP2D_REQUIRE(chunk > 0 && chunk % (IBN / 2) == 0, "ozaki: chunk must be a positive multiple of 128");
-  GP2D_REQUIRE(work != nullptr && work_bytes >= gp2d_predict_ozaki_workspace(n, chunk), "ozaki: workspace too small");
   GP2D_REQUIRE(var_mode >= 0 && var_mode <= 2, "predict: bad var_mode");
   if (m <= 0) return 0;
-  GP2D_REQUIRE(nmod > 0 && nmod <= ozaki_nmod_for(n), "ozaki: nmod exceeds the worst-case count the workspace is sized for");
+  GP2D_REQUIRE(nmod > 0 && nmod <= ozaki_nmod_for(n), "ozaki: nmod exceeds the moduli table");
+  GP2D_REQUIRE(work != nullptr && work_bytes >= predict_ozaki_ws(n, chunk, nmod), "ozaki: workspace too small");
   GP2D_CHECK(valid_bits(0, kbits));
   const int nm = nmod;
   const int64_t ncols_max = 2 * round_up(chunk, IBN);
@@ -1479,12 +1487,15 @@ int gp2d_ozaki_kstar(const double* xtr, int64_t ntr, int64_t ntr_pad, const doub
   return 0;
 }
 
-size_t gp2d_predict_ozaki_planes_workspace(int64_t n, int64_t chunk) {
-  const int nm = ozaki_nmod_for(n);
+static size_t predict_ozaki_planes_ws(int64_t n, int64_t chunk, int nm) {
   if (nm <= 0 || n <= 0) return 0;
   const int64_t ncols = 2 * round_up(chunk < 1 ? 1 : chunk, IBN);
   return (size_t)nm * (size_t)n * (size_t)ncols + sizeof(double) * ozaki_partials(n) * (size_t)ncols +
          oz_list_bytes(n, chunk);
+}
+
+size_t gp2d_predict_ozaki_planes_workspace(int64_t n, int64_t chunk) {
+  return predict_ozaki_planes_ws(n, chunk, ozaki_nmod_for(n));
 }
 
 int gp2d_predict_ozaki_planes(const int8_t* wres, const double* rowscale, int nmod, int kbits, int64_t n,
@@ -1495,12 +1506,11 @@ int gp2d_predict_ozaki_planes(const int8_t* wres, const double* rowscale, int nm
   GP2D_CHECK(validate_ozaki_kernel(k));
   GP2D_REQUIRE(n == 2 * ntr_pad && n % IBM == 0, "ozaki: n must equal 2·ntr_pad and be a multiple of 256");
   GP2D_REQUIRE(chunk > 0 && chunk % (IBN / 2) == 0, "ozaki: chunk must be a positive multiple of 128");
-  GP2D_REQUIRE(work != nullptr && work_bytes >= gp2d_predict_ozaki_planes_workspace(n, chunk),
-               "ozaki: workspace too small");
   GP2D_REQUIRE(var_mode >= 0 && var_mode <= 2, "predict: bad var_mode");
   GP2D_REQUIRE(alpha != nullptr && bres != nullptr, "ozaki_planes: alpha and the K* planes are required");
   if (m <= 0) return 0;
-  GP2D_REQUIRE(nmod > 0 && nmod <= ozaki_nmod_for(n), "ozaki: nmod exceeds the worst-case count");
+  GP2D_REQUIRE(nmod > 0 && nmod <= ozaki_nmod_for(n), "ozaki: nmod exceeds the moduli table");
+  GP2D_REQUIRE(work != nullptr && work_bytes >= predict_ozaki_planes_ws(n, chunk, nmod), "ozaki: workspace too small");
   GP2D_CHECK(valid_bits(0, kbits));
   if (nmod > nmod_b || ozaki_kbits(kbits) != ozaki_kbits(kbits_b)) {
     set_error("ozaki_planes: the fit needs more moduli, or another K* precision, than the planes carry");

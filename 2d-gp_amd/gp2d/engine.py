@@ -626,9 +626,14 @@ def ozaki_prepare(gp: GPFit, diag_add: float | None = None, packed: torch.Tensor
     choice, apply_guard).  gp.extra['ozaki'] = (residue planes, row scales, moduli count, kbits)."""
     L = N.lib()
     n = gp.n
-    wres = torch.empty(int(L.gp2d_ozaki_wres_bytes(n)), dtype=torch.int8, device=gp.device)
-    rowscale = torch.empty(n, dtype=torch.float64, device=gp.device)
     desc = gp.kernel.desc()
+    # the planes this fit will use: the a-priori count is known before the call (the async and
+    # packed preparations use exactly it); the data-driven one only after (the worst case)
+    nm = int(L.gp2d_ozaki_nmod_apriori(n, ctypes.byref(desc), float(diag_add), int(wbits), int(kbits))) \
+        if diag_add is not None else 0
+    wbytes = nm * n * n if nm > 0 else int(L.gp2d_ozaki_wres_bytes(n))
+    wres = torch.empty(wbytes, dtype=torch.int8, device=gp.device)
+    rowscale = torch.empty(n, dtype=torch.float64, device=gp.device)
     nmod = ctypes.c_int(0)
     if packed is not None:
         if diag_add is None:
@@ -750,12 +755,27 @@ class Predictor:
         self.ozaki = "ozaki" in gp.extra
         unit = 128 if (bd == 1 or self.ozaki) else 64
         self.chunk = max(unit, (int(chunk) + unit - 1) // unit * unit)
+        self.wnmod = 0   # the moduli count the ozaki workspace is sized for (grows on demand)
         if self.ozaki:
-            self.wbytes = int(N.lib().gp2d_predict_ozaki_workspace(gp.n, self.chunk))
+            self._ozaki_workspace(gp.extra["ozaki"][2])
         else:
             self.wbytes = int(N.lib().gp2d_predict_workspace(gp.n, self.chunk, bd))
-        self.work = torch.empty(self.wbytes // 8 + 1, dtype=torch.float64, device=gp.device)
+            self.work = torch.empty(self.wbytes // 8 + 1, dtype=torch.float64, device=gp.device)
         self._grid = None   # (the caller's grid tensor, its version, Morton order, the grid in that order)
+
+    def _ozaki_workspace(self, nmod: int):
+        """Size the ozaki workspace for a fit with `nmod` moduli (its layout follows nmod): the
+        accuracy guard may give later fits more, and a worst-case buffer would hold 1.5× the bytes
+        at n = 32,768 for nothing."""
+        if nmod > self.wnmod:
+            self.wbytes = int(N.lib().gp2d_predict_ozaki_workspace_nmod(self.gp.n, self.chunk, int(nmod)))
+            if self.wbytes <= 0:
+                raise N.GP2DError(f"no ozaki workspace for {nmod} moduli at n = {self.gp.n}")
+            if self.wnmod:   # a grown workspace: the old one may still be read by queued predicts
+                torch.cuda.synchronize(self.gp.device)
+            self.work = None
+            self.work = torch.empty(self.wbytes // 8 + 1, dtype=torch.float64, device=self.gp.device)
+            self.wnmod = int(nmod)
 
     def _grid_order(self, xg, G: torch.Tensor, reuse: bool):
         """Morton order of the grid and the grid in that order.  reuse=True (a job stream predicting
@@ -798,6 +818,7 @@ class Predictor:
         desc = gp.kernel.desc()
         if self.ozaki and "ozaki" in gp.extra:
             wres, rowscale, nmod, kbits = gp.extra["ozaki"]
+            self._ozaki_workspace(nmod)
             use_planes = planes is not None and compute_var
             if use_planes and (planes.m != m or planes.n != gp.n or planes.chunk != self.chunk):
                 raise ValueError("K* planes were made for another grid, fit layout or chunk size")

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define GP2D_ABI_VERSION 9
+#define GP2D_ABI_VERSION 10
 
 /* kernel families */
 #define GP2D_FAMILY_VECTOR2D 0   /* 2×2 matrix-valued SE kernels on (x1, x2)          */
@@ -216,6 +216,14 @@ int    gp2d_ozaki_guard(const double* W, int64_t n, int64_t ldw, int64_t ntr, in
 double gp2d_ozaki_error_model(double kss, double vmin, int wbits, int kbits);
 int    gp2d_ozaki_guard_bits(double kss, double vmin, double target, int* wbits, int* kbits);
 size_t gp2d_predict_ozaki_workspace(int64_t n, int64_t chunk);
+/* gp2d_predict_ozaki_workspace(n, chunk) and gp2d_predict_ozaki_planes_workspace(n, chunk) are
+ * the worst case (the most moduli any W / K* precision can need at this n);
+ * gp2d_predict_ozaki_workspace_nmod(n, chunk, nmod) is what either predict entry needs for a fit
+ * prepared with nmod moduli (the entries check against that; 0 if nmod is out of range) — at
+ * config D's n = 32,768 the worst case is 1.5× the 13 moduli the guard takes there.  Likewise the
+ * residue planes of a fit take nmod·n² bytes of the gp2d_ozaki_wres_bytes(n) worst case (the
+ * async preparations' nmod is gp2d_ozaki_nmod_apriori's, known before the call).          */
+size_t gp2d_predict_ozaki_workspace_nmod(int64_t n, int64_t chunk, int nmod);
 /* The variance GEMMs skip K slabs (64 training components) whose K* tile is exactly zero for
  * a 256-row grid tile — exact, such slabs add nothing.  gp2d_ozaki_set_skip(0) runs them
  * dense (A/B measurement and the bit-identity test); default on.                       */

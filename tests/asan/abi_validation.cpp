@@ -152,7 +152,11 @@ int main() {
   const size_t ow = gp2d_predict_ozaki_workspace(256, 128);
   EXPECT_ERR(gp2d_predict_ozaki(wb, buf, 12, 0, 256, buf, buf, 100, 128, buf, 10, &df, 0, 0.0, 1, buf, buf, nullptr, 100, buf, ow, nullptr)); // chunk
   EXPECT_ERR(gp2d_predict_ozaki(wb, buf, 12, 0, 384, buf, buf, 100, 192, buf, 10, &df, 0, 0.0, 1, buf, buf, nullptr, 128, buf, ow, nullptr)); // n
-  EXPECT_ERR(gp2d_predict_ozaki(wb, buf, 12, 0, 256, buf, buf, 100, 128, buf, 10, &df, 0, 0.0, 1, buf, buf, nullptr, 128, buf, ow - 8, nullptr));
+  const size_t ow12 = gp2d_predict_ozaki_workspace_nmod(256, 128, 12);   // what a 12-moduli fit needs
+  EXPECT(ow12 > 0 && ow12 <= ow && gp2d_predict_ozaki_workspace_nmod(256, 128, 0) == 0 &&
+         gp2d_predict_ozaki_workspace_nmod(256, 128, 99) == 0 &&
+         gp2d_predict_ozaki_workspace_nmod(256, 128, 11) < ow12);
+  EXPECT_ERR(gp2d_predict_ozaki(wb, buf, 12, 0, 256, buf, buf, 100, 128, buf, 10, &df, 0, 0.0, 1, buf, buf, nullptr, 128, buf, ow12 - 8, nullptr));
   EXPECT_ERR(gp2d_predict_ozaki(wb, buf, 0, 0, 256, buf, buf, 100, 128, buf, 10, &df, 0, 0.0, 1, buf, buf, nullptr, 128, buf, ow, nullptr)); // nmod
   EXPECT_ERR(gp2d_predict_ozaki(wb, buf, 17, 0, 256, buf, buf, 100, 128, buf, 10, &df, 0, 0.0, 1, buf, buf, nullptr, 128, buf, ow, nullptr));
   EXPECT_ERR(gp2d_ozaki_kstar(buf, 100, 128, buf, 10, &df, 12, 0, 100, wb, 1 << 20, nullptr));     // chunk
