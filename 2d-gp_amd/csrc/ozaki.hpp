@@ -446,6 +446,12 @@ constexpr int IBM = 256, IBN = 256, IBK = 64;
 constexpr int I_OP = IBM * IBK;        // bytes per operand per stage (16 KB) = one layout tile
 constexpr int I_STAGE = 2 * I_OP;      // A then B
 constexpr int I_NSTAGE = 4;        // ring stages of the 256-wide shape (I_NSTAGE − 1 slabs in flight)
+#ifndef GP2D_IGEMM_BUFLDS
+#define GP2D_IGEMM_BUFLDS 0        // 1: the LDS-DMA through buffer descriptors (measurement variant)
+#endif
+#ifndef GP2D_IGEMM_V2
+#define GP2D_IGEMM_V2 0            // 1: wave-uniform wave index, offset-field fragment reads (measurement variant)
+#endif
 
 typedef int i4v __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -520,7 +526,11 @@ __global__ __launch_bounds__(TBN * 2, (TBN == 256) ? 1 : 2) void igemm_nt_mod_ke
   const int i0 = bi * IBM, j0 = bj * TBN;
   const int jb = j0 / IBN, jr = j0 % IBN;             // 256-row B layout block, row offset in it
   const int ke = a_lower ? min(K, i0 + IBM) : K;
+#if GP2D_IGEMM_V2
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+#else
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+#endif
   const int wr = wid / WC, wc = wid % WC;
   const int l16 = lane & 15, lq = lane >> 4;
   const int64_t kslabs = K / IBK;
@@ -549,6 +559,38 @@ __global__ __launch_bounds__(TBN * 2, (TBN == 256) ? 1 : 2) void igemm_nt_mod_ke
 
   // wave w moves A rows [16·AP·w, +16·AP) and B rows [32w, 32w+32): contiguous 1 KB pieces
   const int drow = lane >> 2, dchunk = lane & 3;
+#if GP2D_IGEMM_BUFLDS && defined(__HIP_DEVICE_COMPILE__)   // (the host pass only needs the launch stub)
+  // LDS-DMA through buffer descriptors: the lane's 32-bit offset inside a slab tile is the same
+  // for every slab, the slab's offset goes in the scalar soffset — no per-piece 64-bit address
+  const int rec = (int)(kslabs * I_OP);
+  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)Ap, (short)0, rec, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rBp = __builtin_amdgcn_make_buffer_rsrc((void*)Bp, (short)0, rec, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rBq = __builtin_amdgcn_make_buffer_rsrc((void*)Bq, (short)0, rec, 0x00020000);
+  int voA[AP], voB[BPW];
+#pragma unroll
+  for (int h = 0; h < AP; ++h) {
+    const int row = (wid * AP + h) * 16 + drow;
+    voA[h] = row * IBK + 16 * swz16(row, dchunk);
+  }
+#pragma unroll
+  for (int h = 0; h < BPW; ++h) {
+    const int row = (wid * BPW + h) * 16 + drow;
+    voB[h] = row * IBK + 16 * swz16(jr + row, dchunk);
+  }
+  auto issue = [&](int ks, int st) {
+    int8_t* As = smem + st * STG;
+    int8_t* Bs = As + I_OP;
+    const int so = ks * I_OP;
+#pragma unroll
+    for (int h = 0; h < AP; ++h)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_ptr_t)(As + (wid * AP + h) * 16 * IBK), 16, voA[h], so, 0, 0);
+    const bool q = alias && ks < alias_ks;
+#pragma unroll
+    for (int h = 0; h < BPW; ++h)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(q ? rBq : rBp, (lds_ptr_t)(Bs + (wid * BPW + h) * 16 * IBK), 16, voB[h],
+                                               so, 0, 0);
+  };
+#else
   // ks: the K slab (already mapped through the list) loaded into ring stage st
   auto issue = [&](int ks, int st) {
     int8_t* As = smem + st * STG;
@@ -568,7 +610,35 @@ __global__ __launch_bounds__(TBN * 2, (TBN == 256) ? 1 : 2) void igemm_nt_mod_ke
                                        (lds_ptr_t)(Bs + (wid * BPW + h) * 16 * IBK), 16, 0, 0);
     }
   };
+#endif
   const uint32_t lds_base = (uint32_t)(size_t)(lds_ptr_t)smem;
+#if GP2D_IGEMM_V2
+  // one base VGPR per read group, the fragment in the offset field: the swizzle depends on
+  // (row >> 2) & 3 = (l16 >> 2) & 3 only (fragment rows are 16-aligned; jr % 16 == 0)
+  const uint32_t lane_a = (uint32_t)((wr * 128 + l16) * IBK + 16 * swz16(l16, lq));
+  const uint32_t lane_b = (uint32_t)(I_OP + (wc * 64 + l16) * IBK + 16 * swz16(jr + l16, lq));
+  auto reada = [&](int st, int half, i4v (&a)[4]) {  // A fragments mi = 4·half .. 4·half+3
+    const uint32_t ad = lds_base + st * STG + lane_a;
+    if (half == 0) {
+      asm volatile("ds_read_b128 %0, %1 offset:0" : "=v"(a[0]) : "v"(ad) : "memory");
+      asm volatile("ds_read_b128 %0, %1 offset:1024" : "=v"(a[1]) : "v"(ad) : "memory");
+      asm volatile("ds_read_b128 %0, %1 offset:2048" : "=v"(a[2]) : "v"(ad) : "memory");
+      asm volatile("ds_read_b128 %0, %1 offset:3072" : "=v"(a[3]) : "v"(ad) : "memory");
+    } else {
+      asm volatile("ds_read_b128 %0, %1 offset:4096" : "=v"(a[0]) : "v"(ad) : "memory");
+      asm volatile("ds_read_b128 %0, %1 offset:5120" : "=v"(a[1]) : "v"(ad) : "memory");
+      asm volatile("ds_read_b128 %0, %1 offset:6144" : "=v"(a[2]) : "v"(ad) : "memory");
+      asm volatile("ds_read_b128 %0, %1 offset:7168" : "=v"(a[3]) : "v"(ad) : "memory");
+    }
+  };
+  auto readb = [&](int st, i4v (&b)[4]) {
+    const uint32_t ad = lds_base + st * STG + lane_b;
+    asm volatile("ds_read_b128 %0, %1 offset:0" : "=v"(b[0]) : "v"(ad) : "memory");
+    asm volatile("ds_read_b128 %0, %1 offset:1024" : "=v"(b[1]) : "v"(ad) : "memory");
+    asm volatile("ds_read_b128 %0, %1 offset:2048" : "=v"(b[2]) : "v"(ad) : "memory");
+    asm volatile("ds_read_b128 %0, %1 offset:3072" : "=v"(b[3]) : "v"(ad) : "memory");
+  };
+#else
   auto reada = [&](int st, int half, i4v (&a)[4]) {  // A fragments mi = 4·half .. 4·half+3
     const uint32_t As = lds_base + st * STG;
 #pragma unroll
@@ -587,6 +657,7 @@ __global__ __launch_bounds__(TBN * 2, (TBN == 256) ? 1 : 2) void igemm_nt_mod_ke
       asm volatile("ds_read_b128 %0, %1" : "=v"(b[ni]) : "v"(ad) : "memory");
     }
   };
+#endif
   auto mfmas = [&](int half, const i4v (&a)[4], const i4v (&b)[4]) {
 #pragma unroll
     for (int u = 0; u < 4; ++u)
