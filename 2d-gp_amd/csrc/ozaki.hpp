@@ -434,7 +434,7 @@ __device__ __forceinline__ uint32_t ozaki_mod_u32(uint32_t v, const OzModConsts&
 // 256×256 output tile per 512-thread workgroup: 8 waves as 2×4, two waves per SIMD, each
 // wave 128×64 = 8×4 tiles of v_mfma_i32_16x16x64_i8 (128 accumulators).  While one wave of
 // a SIMD issues its LDS-DMA pieces and fragment reads the other keeps the matrix core busy.
-// K advances in 64-byte slabs loaded global→LDS directly (global_load_lds_dwordx4) into a
+// K advances in 64-byte slabs loaded global→LDS directly (buffer_load_dwordx4 … lds) into a
 // 4-stage ring with three slabs in flight; one barrier per slab, between the slab's two MFMA
 // halves, publishes the next one.
 // Lane l reads A[row l&15][k 16(l>>4)..+15]; a ds_read_b128 lane group covers rows
@@ -446,15 +446,21 @@ constexpr int IBM = 256, IBN = 256, IBK = 64;
 constexpr int I_OP = IBM * IBK;        // bytes per operand per stage (16 KB) = one layout tile
 constexpr int I_STAGE = 2 * I_OP;      // A then B
 constexpr int I_NSTAGE = 4;        // ring stages of the 256-wide shape (I_NSTAGE − 1 slabs in flight)
-#ifndef GP2D_IGEMM_BUFLDS
-#define GP2D_IGEMM_BUFLDS 0        // 1: the LDS-DMA through buffer descriptors (measurement variant)
-#endif
-#ifndef GP2D_IGEMM_V2
-#define GP2D_IGEMM_V2 0            // 1: wave-uniform wave index, offset-field fragment reads (measurement variant)
-#endif
+
 
 typedef int i4v __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+// One 1 KB LDS-DMA piece per wave (buffer_load_dwordx4 … offen lds): 16 B per lane from the
+// descriptor's base + the lane's 32-bit offset + the wave-uniform soffset into LDS at dst (M0).
+// Against global_load_lds with 64-bit lane addresses it needs no per-piece address arithmetic:
+// the lane offsets are the same for every K slab and the slab's offset is scalar (round 5:
+// −4.5 % per unpipelined launch with the offset-field fragment reads, profiles/r05_bufbench_ab.txt).
+__device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t r, lds_ptr_t dst, int voff, int soff) {
+#if defined(__HIP_DEVICE_COMPILE__)   // a gfx950 builtin: the host pass only needs the kernels' launch stubs
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, dst, 16, voff, soff, 0, 0);
+#endif
+}
 
 __device__ __forceinline__ int swz16(int row, int chunk) {
   const int q = (row >> 2) & 3;
@@ -526,11 +532,8 @@ __global__ __launch_bounds__(TBN * 2, (TBN == 256) ? 1 : 2) void igemm_nt_mod_ke
   const int i0 = bi * IBM, j0 = bj * TBN;
   const int jb = j0 / IBN, jr = j0 % IBN;             // 256-row B layout block, row offset in it
   const int ke = a_lower ? min(K, i0 + IBM) : K;
-#if GP2D_IGEMM_V2
+  // the wave index as a scalar: LDS-DMA destinations (M0) and piece offsets without v_readfirstlane
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-#else
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-#endif
   const int wr = wid / WC, wc = wid % WC;
   const int l16 = lane & 15, lq = lane >> 4;
   const int64_t kslabs = K / IBK;
@@ -559,9 +562,8 @@ __global__ __launch_bounds__(TBN * 2, (TBN == 256) ? 1 : 2) void igemm_nt_mod_ke
 
   // wave w moves A rows [16·AP·w, +16·AP) and B rows [32w, 32w+32): contiguous 1 KB pieces
   const int drow = lane >> 2, dchunk = lane & 3;
-#if GP2D_IGEMM_BUFLDS && defined(__HIP_DEVICE_COMPILE__)   // (the host pass only needs the launch stub)
-  // LDS-DMA through buffer descriptors: the lane's 32-bit offset inside a slab tile is the same
-  // for every slab, the slab's offset goes in the scalar soffset — no per-piece 64-bit address
+  // LDS-DMA through buffer descriptors over this row block's slab tiles (A) and the column
+  // block's (B; Bq: the aliased (v,u) tiles): lane offsets fixed, the slab (ks·16 KB) in soffset
   const int rec = (int)(kslabs * I_OP);
   const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)Ap, (short)0, rec, 0x00020000);
   const __amdgpu_buffer_rsrc_t rBp = __builtin_amdgcn_make_buffer_rsrc((void*)Bp, (short)0, rec, 0x00020000);
@@ -582,37 +584,13 @@ __global__ __launch_bounds__(TBN * 2, (TBN == 256) ? 1 : 2) void igemm_nt_mod_ke
     int8_t* Bs = As + I_OP;
     const int so = ks * I_OP;
 #pragma unroll
-    for (int h = 0; h < AP; ++h)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_ptr_t)(As + (wid * AP + h) * 16 * IBK), 16, voA[h], so, 0, 0);
+    for (int h = 0; h < AP; ++h) lds_dma16(rA, (lds_ptr_t)(As + (wid * AP + h) * 16 * IBK), voA[h], so);
     const bool q = alias && ks < alias_ks;
 #pragma unroll
-    for (int h = 0; h < BPW; ++h)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(q ? rBq : rBp, (lds_ptr_t)(Bs + (wid * BPW + h) * 16 * IBK), 16, voB[h],
-                                               so, 0, 0);
+    for (int h = 0; h < BPW; ++h) lds_dma16(q ? rBq : rBp, (lds_ptr_t)(Bs + (wid * BPW + h) * 16 * IBK), voB[h], so);
   };
-#else
-  // ks: the K slab (already mapped through the list) loaded into ring stage st
-  auto issue = [&](int ks, int st) {
-    int8_t* As = smem + st * STG;
-    int8_t* Bs = As + I_OP;
-    const int8_t* Ag = Ap + (int64_t)ks * I_OP;
-    const int8_t* Bg = ((alias && ks < alias_ks) ? Bq : Bp) + (int64_t)ks * I_OP;
-#pragma unroll
-    for (int h = 0; h < AP; ++h) {
-      const int row = (wid * AP + h) * 16 + drow;
-      __builtin_amdgcn_global_load_lds((const void*)(Ag + row * IBK + 16 * swz16(row, dchunk)),
-                                       (lds_ptr_t)(As + (wid * AP + h) * 16 * IBK), 16, 0, 0);
-    }
-#pragma unroll
-    for (int h = 0; h < BPW; ++h) {
-      const int row = (wid * BPW + h) * 16 + drow;   // swizzle by the row within the 256 block
-      __builtin_amdgcn_global_load_lds((const void*)(Bg + row * IBK + 16 * swz16(jr + row, dchunk)),
-                                       (lds_ptr_t)(Bs + (wid * BPW + h) * 16 * IBK), 16, 0, 0);
-    }
-  };
-#endif
+
   const uint32_t lds_base = (uint32_t)(size_t)(lds_ptr_t)smem;
-#if GP2D_IGEMM_V2
   // one base VGPR per read group, the fragment in the offset field: the swizzle depends on
   // (row >> 2) & 3 = (l16 >> 2) & 3 only (fragment rows are 16-aligned; jr % 16 == 0)
   const uint32_t lane_a = (uint32_t)((wr * 128 + l16) * IBK + 16 * swz16(l16, lq));
@@ -638,26 +616,6 @@ __global__ __launch_bounds__(TBN * 2, (TBN == 256) ? 1 : 2) void igemm_nt_mod_ke
     asm volatile("ds_read_b128 %0, %1 offset:2048" : "=v"(b[2]) : "v"(ad) : "memory");
     asm volatile("ds_read_b128 %0, %1 offset:3072" : "=v"(b[3]) : "v"(ad) : "memory");
   };
-#else
-  auto reada = [&](int st, int half, i4v (&a)[4]) {  // A fragments mi = 4·half .. 4·half+3
-    const uint32_t As = lds_base + st * STG;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int row = wr * 128 + (4 * half + u) * 16 + l16;
-      const uint32_t ad = As + row * IBK + 16 * swz16(row, lq);
-      asm volatile("ds_read_b128 %0, %1" : "=v"(a[u]) : "v"(ad) : "memory");
-    }
-  };
-  auto readb = [&](int st, i4v (&b)[4]) {
-    const uint32_t Bs = lds_base + st * STG + I_OP;
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni) {
-      const int row = wc * 64 + ni * 16 + l16;
-      const uint32_t ad = Bs + row * IBK + 16 * swz16(jr + row, lq);
-      asm volatile("ds_read_b128 %0, %1" : "=v"(b[ni]) : "v"(ad) : "memory");
-    }
-  };
-#endif
   auto mfmas = [&](int half, const i4v (&a)[4], const i4v (&b)[4]) {
 #pragma unroll
     for (int u = 0; u < 4; ++u)
