@@ -1369,14 +1369,18 @@ static int predict_ozaki_impl(const int8_t* wres, const double* rowscale, int nm
         const int nz = std::min(zper, nm - l0);
         IgemmZ zb{(int64_t)n * n, (int64_t)bplane, (int64_t)n * ncols, {}};
         for (int u = 0; u < nz; ++u) zb.m[u] = oc.m[l0 + u];
-        const dim3 ggrid((unsigned)(ncols / IBN), (unsigned)(n / IBM), (unsigned)nz);
+#ifndef GP2D_IG_TBN
+#define GP2D_IG_TBN 256   // output columns per workgroup (128: two workgroups per CU, a measurement build)
+#endif
+        constexpr int tbn = GP2D_IG_TBN, nst = (GP2D_IG_TBN == 256) ? I_NSTAGE : 3;
+        const dim3 ggrid((unsigned)(ncols / tbn), (unsigned)(n / IBM), (unsigned)nz);
         const int8_t* Al = wres + (size_t)l0 * n * n;
         const int8_t* Bl = B + (size_t)l0 * bplane;
         uint8_t* Cl = cres + (size_t)l0 * n * ncols;
-        igemm_nt_mod_kernel<256, I_NSTAGE><<<ggrid, 512, 0, s>>>(Al, Bl, Cl, n, (int)n, (int)ncols, (int)n, 1, oc.m[l0],
-                                                                 (int)(cp / IBN), (int)(ntr_pad / IBK),
-                                                                 use_skip ? slist : nullptr, use_skip ? scnt : nullptr,
-                                                                 zb);
+        igemm_nt_mod_kernel<tbn, nst><<<ggrid, 2 * tbn, 0, s>>>(Al, Bl, Cl, n, (int)n, (int)ncols, (int)n, 1, oc.m[l0],
+                                                                (int)(cp / IBN), (int)(ntr_pad / IBK),
+                                                                use_skip ? slist : nullptr, use_skip ? scnt : nullptr,
+                                                                zb);
         GP2D_CHECK(check_launch("igemm_nt_mod_kernel"));
       }
       if (e0) {
