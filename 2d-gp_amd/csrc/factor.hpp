@@ -143,7 +143,10 @@ __device__ __forceinline__ Pivot make_pivot(double d) {
 // the next GP2D_PANEL_RL columns' multipliers straight from lane c's register by v_readlane
 // instead, so the pivot chain K → K+1 carries no LDS round trip: 1, 2 and 4 such columns measured
 // 54.4–54.9 µs per diagonal block against 54.0 µs — the panel wave is issue-bound on its
-// 2·(31 − K) FMAs per pivot, not bound by the broadcast's latency; tools/microbench diag_bench_rl*.)
+// 2·(31 − K) FMAs per pivot, not bound by the broadcast's latency; tools/microbench diag_bench_rl*.
+// Round 5 took the chain itself off the issue stream — uniform-value pivot chain, bulk update one
+// step late, broadcast under the next pivot — bit-identical and −1.2 %: a lone wave's issue of
+// the whole step sets the pivot time; profiles/r05_diag_panel_ab.txt, git 9434024.)
 #ifndef GP2D_PANEL_RL
 #define GP2D_PANEL_RL 0
 #endif
@@ -192,158 +195,13 @@ __device__ __forceinline__ void panel_step(double (&x0)[32], double (&x1)[32], d
     __builtin_amdgcn_wave_barrier();
   }
 }
-#ifndef GP2D_PANEL_LAG
-#define GP2D_PANEL_LAG 1   // 0: panel_step (dev builds, for the A/B)
-#endif
-#ifndef GP2D_DEV_NEWTON1
-#define GP2D_DEV_NEWTON1 0   // 1: dev timing builds only — one Newton step per pivot (≈ 46-bit 1/√d)
-#endif
-#ifndef GP2D_DEV_NOX1
-#define GP2D_DEV_NOX1 0    // 1: dev timing builds only — the first two panels skip their second row set (wrong factor)
-#endif
-
-// lc[c] = colbuf[c] for c in [CMIN, 32), issued by inline asm with the offset in the
-// instruction (one base VGPR, no per-read address registers): the caller waits (lgkmcnt) and
-// pins lc before the first use — the compiler does not count these reads.  Every destination
-// register must be a live lc entry until that wait (a dead half of a 16-byte read would be
-// handed to other values while the read is still in flight), so an odd CMIN starts with one
-// 8-byte read.
-template <int CMIN, int... Is>
-__device__ __forceinline__ void read_lc(std::integer_sequence<int, Is...>, double (&lc)[32], uint32_t cb) {
-  if constexpr (CMIN & 1)
-    asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(lc[CMIN]) : "v"(cb), "n"(8 * CMIN) : "memory");
-  auto one = [&](auto ic) {
-    constexpr int c = ((CMIN + 1) & ~1) + 2 * decltype(ic)::value;
-    d2 v;
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(cb), "n"(8 * c) : "memory");
-    lc[c] = v.x;
-    lc[c + 1] = v.y;
-  };
-  (one(std::integral_constant<int, Is>{}), ...);
-}
-// Pivot K of the panel with the bulk of its rank-1 update one step late (round 5).  In
-// panel_step every pivot waits for its column's LDS broadcast and then for the ≤ 62 FMAs
-// issued in front of the next column's scaling, so pivot time = Newton chain + broadcast
-// round trip + FMA issue (≈ 500 cycles at every K, even for the 32-row last panel).  Here the
-// columns that the next pivots need take their multipliers by v_readlane, and the rest of
-// column K's update runs during step K + 1, behind the pivot chain:
-//   step K: scale column K; column K+1 −= column K · L[K+1][K]  →  pivot K+1 (rsq/Newton);
-//           column K+2: step K−1's update, then step K's; columns ≥ K+3: step K−1's update
-//           (multipliers lc: column K−1 broadcast through LDS at the end of step K−1, so
-//           the round trip runs under the next pivot's first operations).
-// Every element still receives the updates of steps 0, 1, … in order with the same operands,
-// so the factor is bit-identical to panel_step's.
-template <int K, bool X1>
-__device__ __forceinline__ void panel_step_lag(double (&x0)[32], double (&x1)[32], double (&lc)[32], double* colbuf,
-                                               int lane, int& bad, Pivot& pv, double& rn, double& an) {
-  bad = (bad == 0 && !(pv.d > 0.0)) ? K + 1 : bad;
-  if constexpr (K < 31) {
-    // the pivot chain on wave-uniform values: L[K+1][K] = rn / √d_K and d_{K+1} = an − L[K+1][K]²,
-    // where rn = A[K+1][K] and an = A[K+1][K+1] after steps < K (read off the chain at step K−1):
-    // the same operations on the same operands as the per-lane update, so the same bits
-    const double l1 = rn * pv.ird;
-    const double d = fma(-l1, l1, an);
-    double y = __builtin_amdgcn_rsq(d), t = 0.0;
-    const double nhd = d * -0.5;
-    asm volatile("" : "+v"(y));
-    x0[K] = (lane > K) ? x0[K] * pv.ird : ((lane == K) ? pv.rd : x0[K]);
-    if constexpr (X1) x1[K] *= pv.ird;
-    x0[K + 1] = fma(-x0[K], l1, x0[K + 1]);
-    asm volatile("" : "+v"(x0[K + 1]));
-    if constexpr (X1) {
-      x1[K + 1] = fma(-x1[K], l1, x1[K + 1]);
-      asm volatile("" : "+v"(x1[K + 1]));
-    }
-    double l0 = 0.0, l2 = 0.0;   // L[K+2][K−1] and L[K+2][K] by readlane (no LDS wait up front)
-    if constexpr (K + 2 < 32) {
-      if constexpr (K >= 1) l0 = readlane_f64(x0[K - 1], K + 2);
-      l2 = readlane_f64(x0[K], K + 2);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    // the update work: column K+2 (step K−1, then step K), columns ≥ K+3 (step K−1); the
-    // Newton steps of pivot K+1 (make_pivot's operations in its order) spread between them so
-    // that the wave issues FMAs while each waits for its predecessor
-    constexpr int NC2 = (K + 2 < 32) ? ((K >= 1) ? 2 : 1) : 0;
-    constexpr int NBULK = (K >= 1 && K + 3 < 32) ? 32 - (K + 3) : 0;
-    constexpr int NW = NC2 + NBULK;
-    auto item = [&](int i) {
-      if (i < NC2) {
-        const bool lag = (NC2 == 2 && i == 0);
-        const int kk = lag ? K - 1 : K;
-        const double m = lag ? l0 : l2;
-        x0[K + 2] = fma(-x0[kk], m, x0[K + 2]);
-        asm volatile("" : "+v"(x0[K + 2]));
-        if constexpr (X1) {
-          x1[K + 2] = fma(-x1[kk], m, x1[K + 2]);
-          asm volatile("" : "+v"(x1[K + 2]));
-        }
-      } else {
-        const int c = K + 3 + (i - NC2);
-        x0[c] = fma(-x0[K - 1], lc[c], x0[c]);
-        asm volatile("" : "+v"(x0[c]));   // pinned as in panel_step
-        if constexpr (X1) {
-          x1[c] = fma(-x1[K - 1], lc[c], x1[c]);
-          asm volatile("" : "+v"(x1[c]));
-        }
-      }
-    };
-    auto newton = [&](int j) {
-      if (GP2D_DEV_NEWTON1 && j >= 4 && j <= 6) return;
-      switch (j) {
-        case 1: case 4: t = nhd * y; break;
-        case 2: case 5: t = fma(t, y, 1.5); break;
-        case 3: case 6: y = y * t; break;
-        default: t = d * y; break;   // 7: rd
-      }
-      asm volatile("" : "+v"(y), "+v"(t));
-      __builtin_amdgcn_sched_barrier(0);
-    };
-#pragma unroll
-    for (int i = 0; i < NW; ++i) {
-      if (i == NC2) {   // column K−1's multipliers, read at the end of step K−1, have landed
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-        for (int c = K + 3; c < 32; ++c) asm volatile("" : "+v"(lc[c]));
-      }
-      item(i);
-#pragma unroll
-      for (int j = 1; j <= 7; ++j)
-        if ((j * NW) / 8 == i) newton(j);
-    }
-    if constexpr (NW == 0) {
-#pragma unroll
-      for (int j = 1; j <= 7; ++j) newton(j);
-    }
-    if constexpr (K + 2 < 32) {   // the next pivot's operands, long since final
-      rn = readlane_f64(x0[K + 1], K + 2);
-      an = readlane_f64(x0[K + 2], K + 2);
-    }
-    pv = Pivot{d, t, y, 0};
-    if constexpr (K + 4 < 32) {   // column K's multipliers for rows ≥ K+4 (step K+1's bulk)
-      if (lane < 32) colbuf[lane] = x0[K];
-      __builtin_amdgcn_wave_barrier();
-      read_lc<K + 4>(std::make_integer_sequence<int, (32 - ((K + 5) & ~1)) / 2>{}, lc,
-                     (uint32_t)(size_t)(__attribute__((address_space(3))) void*)colbuf);
-    }
-    __builtin_amdgcn_wave_barrier();
-  } else {
-    x0[K] = (lane > K) ? x0[K] * pv.ird : ((lane == K) ? pv.rd : x0[K]);
-    if constexpr (X1) x1[K] *= pv.ird;
-  }
-}
 // Returns the 1-based column of the first non-positive pivot of the panel (0: none).
 template <bool X1, int... Ks>
 __device__ __forceinline__ int panel_steps(std::integer_sequence<int, Ks...>, double (&x0)[32], double (&x1)[32],
                                            double* colbuf, int lane) {
   Pivot pv = make_pivot(readlane_f64(x0[0], 0));
   int bad = 0;
-  if constexpr (GP2D_PANEL_LAG) {
-    double lc[32];
-    double rn = readlane_f64(x0[0], 1), an = readlane_f64(x0[1], 1);
-    (panel_step_lag<Ks, X1>(x0, x1, lc, colbuf, lane, bad, pv, rn, an), ...);
-  } else {
-    (panel_step<Ks, X1>(x0, x1, colbuf, lane, bad, pv), ...);
-  }
+  (panel_step<Ks, X1>(x0, x1, colbuf, lane, bad, pv), ...);
   return bad;
 }
 
@@ -497,7 +355,7 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
       x1[c] = t1.x; x1[c + 1] = t1.y;
     }
     // rows c0+64+lane exist only for the first two panels
-    const int bad = (p < 2 && !GP2D_DEV_NOX1) ? panel_steps<true>(std::make_integer_sequence<int, 32>{}, x0, x1, colbuf, lane)
+    const int bad = (p < 2) ? panel_steps<true>(std::make_integer_sequence<int, 32>{}, x0, x1, colbuf, lane)
                             : panel_steps<false>(std::make_integer_sequence<int, 32>{}, x0, x1, colbuf, lane);
     if (bad && lane == 0 && info) atomicCAS(info, 0, k0 + c0 + bad);
     if (v0) {

@@ -1,5 +1,5 @@
 #!/bin/bash
-# r05: the diagonal-block kernel's panel pivots with the lagged update (GP2D_PANEL_LAG, default)
+# r05: the diagonal-block kernel's panel pivots with the lagged update (GP2D_PANEL_LAG; factor.hpp at git 9434024)
 # vs panel_step (dev build tools/_p/libgp2d_lag0.so): per-call time, fit medians, factor bits;
 # then phase stamps (tools/microbench/diag_stamps.h) of dev builds: lag1, lag0, lag1 without the
 # second row set of panels 0-1 (NOX1: timing only).
