@@ -290,6 +290,52 @@ __device__ __forceinline__ void tile4x4_store(double* __restrict__ S, int r, int
   }
 }
 
+// The same 32×32 block products on the f64 matrix core (round 5): one wave, 2×2 tiles of
+// v_mfma_f64_16x16x4f64, K = 32 in 8 steps of 4.  Operands: a = X[row l&15][k l>>4],
+// b = Y(k l>>4, col l&15); acc[ti][tj][r] is C[16ti + (l>>4) + 4r][16tj + (l&15)].  A tenth of
+// tile4x4's LDS bytes per product (16 vs 128 KB per wave); the sums run in the matrix core's
+// order, so the factor differs from the FMA tiles' in the last bits.
+#ifndef GP2D_DIAG_MFMA
+#define GP2D_DIAG_MFMA 1   // 0: tile4x4 (dev builds, for the A/B)
+#endif
+typedef d4 tileacc_t[2][2];
+template <bool NT>
+__device__ __forceinline__ void tile32_mfma(const double* __restrict__ S, int xr, int xk, int yk, int yc,
+                                            tileacc_t& acc, int l16, int lk) {
+#pragma unroll
+  for (int k0 = 0; k0 < 32; k0 += 4) {
+    double a[2], b[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      a[t] = S[dsw(xr + 16 * t + l16, xk + k0 + lk)];
+      b[t] = NT ? S[dsw(yc + 16 * t + l16, yk + k0 + lk)] : S[dsw(yk + k0 + lk, yc + 16 * t + l16)];
+    }
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+      for (int tj = 0; tj < 2; ++tj) acc[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ti], b[tj], acc[ti][tj], 0, 0, 0);
+  }
+}
+__device__ __forceinline__ void tile32_zero(tileacc_t& acc) {
+#pragma unroll
+  for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+    for (int tj = 0; tj < 2; ++tj) acc[ti][tj] = d4{0.0, 0.0, 0.0, 0.0};
+}
+// S[r0 + …][c0 + …] = sgn·acc + (accumulate ? S : 0), the MFMA output map
+__device__ __forceinline__ void tile32_store(double* __restrict__ S, int r0, int c0, const tileacc_t& acc, double sgn,
+                                             bool accumulate, int l16, int lk) {
+#pragma unroll
+  for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+    for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        double* o = S + dsw(r0 + 16 * ti + lk + 4 * r, c0 + 16 * tj + l16);
+        *o = fma(sgn, acc[ti][tj][r], accumulate ? *o : 0.0);
+      }
+}
+
 // inv_in_place (the fused factor + inverse, gp2d_potrf_inv): A's diagonal block receives
 // W_kk = L_kk⁻¹ instead of L_kk (nothing reads L_kk from A after this kernel: the panel TRSM
 // uses dinv), which is TRTRI's level 0.
@@ -368,11 +414,23 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
     }
   };
   // A(bi, bj) −= L(bi, p) · L(bj, p)ᵀ  (32-block indices), one wave
+  const int m16 = lane & 15, mk = lane >> 4;   // the MFMA operand / output map
+#if GP2D_DIAG_MFMA
+  typedef tileacc_t acc_t;
+#else
+  typedef double acc_t[4][4];
+#endif
   auto update = [&](int p, int bi, int bj) {
-    double acc[4][4];
+    acc_t acc;
+#if GP2D_DIAG_MFMA
+    tile32_zero(acc);
+    tile32_mfma<true>(S, 32 * bi, 32 * p, 32 * p, 32 * bj, acc, m16, mk);
+    tile32_store(S, 32 * bi, 32 * bj, acc, -1.0, true, m16, mk);
+#else
     tile4x4_zero(acc);
     tile4x4<true>(S, 32 * bi + tr4, 32 * p, 32 * p, 32 * bj + tc4, acc);
     tile4x4_store(S, 32 * bi + tr4, 32 * bj + tc4, acc, -1.0, true);
+#endif
   };
   // column block cb of L (all 128 rows, zeros above the diagonal) to A, by threads [t0, t0+nt)
   auto store_colblock = [&](int cb, int t0, int nt) {
@@ -400,12 +458,21 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
     }
   };
   // acc = Σ_{p in [p0, p1]} X(bi, p) · Y(p, bj)  (NN, 32-block indices)
-  auto prod = [&](double (&acc)[4][4], int bi, int bj, int p0, int p1) {
+  auto prod = [&](acc_t& acc, int bi, int bj, int p0, int p1) {
+#if GP2D_DIAG_MFMA
+    tile32_zero(acc);
+    for (int p = p0; p <= p1; ++p) tile32_mfma<false>(S, 32 * bi, 32 * p, 32 * p, 32 * bj, acc, m16, mk);
+#else
     tile4x4_zero(acc);
     for (int p = p0; p <= p1; ++p) tile4x4<false>(S, 32 * bi + tr4, 32 * p, 32 * p, 32 * bj + tc4, acc);
+#endif
   };
-  auto put = [&](int bi, int bj, const double (&acc)[4][4], double sgn) {
+  auto put = [&](int bi, int bj, const acc_t& acc, double sgn) {
+#if GP2D_DIAG_MFMA
+    tile32_store(S, 32 * bi, 32 * bj, acc, sgn, false, m16, mk);
+#else
     tile4x4_store(S, 32 * bi + tr4, 32 * bj + tc4, acc, sgn, false);
+#endif
   };
 
   // P0
@@ -452,7 +519,7 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
     return;
   }
   // B: L column block 3, then W33 (registers) | T10 = L10 W00 → W10 = −W11 T10 | T32 = L32 W22
-  double acc[4][4], acc2[4][4];
+  acc_t acc;
   if (wid == 0) {
     if (storeL) store_colblock(3, 0, 64);
     diag_inverse(3, xd);
@@ -467,22 +534,24 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
   }
   __syncthreads();
   GP2D_STAMP(9);
-  // C: W33 → S, W32 = −W33 T32 | T20 | T21 and T31 | T30   (T kept in registers)
+  // C: W33 → S, W32 = −W33 T32, then T31 | T20 | T21 | T30   (T kept in registers: one
+  // accumulator set per wave — S(3,2) is nobody else's operand here)
   if (wid == 0) {
     put_diag(3, xd);
     prod(acc, 3, 2, 3, 3);
     put(3, 2, acc, -1.0);
+    prod(acc, 3, 1, 1, 1);
   } else if (wid == 1) {
     prod(acc, 2, 0, 0, 1);
   } else if (wid == 2) {
     prod(acc, 2, 1, 1, 1);
-    prod(acc2, 3, 1, 1, 1);
   } else {
     prod(acc, 3, 0, 0, 1);
   }
   __syncthreads();
+  if (wid == 0) put(3, 1, acc, 1.0);
   if (wid == 1) put(2, 0, acc, 1.0);
-  if (wid == 2) { put(2, 1, acc, 1.0); put(3, 1, acc2, 1.0); }
+  if (wid == 2) put(2, 1, acc, 1.0);
   if (wid == 3) put(3, 0, acc, 1.0);
   __syncthreads();
   GP2D_STAMP(10);
