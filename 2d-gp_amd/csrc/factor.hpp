@@ -336,6 +336,26 @@ __device__ __forceinline__ void tile32_store(double* __restrict__ S, int r0, int
       }
 }
 
+// Column step K of the forward substitution of a 16×16 block at rows/cols rb0 (lane ↔ column
+// j = lane & 15 of its half's block; rk = 1 / L_KK of that block): as inv_step, 16 wide.
+template <int K>
+__device__ __forceinline__ void inv16_step(double (&x)[16], const double* S, int rb0, double rk) {
+  double lk[16];
+#pragma unroll
+  for (int i = K + 1; i < 16; ++i) lk[i] = S[dsw(rb0 + i, rb0 + K)];
+  x[K] = x[K] * rk;
+#pragma unroll
+  for (int i = K + 1; i < 16; ++i) {
+    x[i] = fma(-lk[i], x[K], x[i]);
+    asm volatile("" : "+v"(x[i]));
+  }
+}
+template <int... Ks>
+__device__ __forceinline__ void inv16_steps(std::integer_sequence<int, Ks...>, double (&x)[16], const double* S, int rb0,
+                                            double rl, int h) {
+  (inv16_step<Ks>(x, S, rb0, h ? readlane_f64(rl, 16 + Ks) : readlane_f64(rl, Ks)), ...);
+}
+
 // inv_in_place (the fused factor + inverse, gp2d_potrf_inv): A's diagonal block receives
 // W_kk = L_kk⁻¹ instead of L_kk (nothing reads L_kk from A after this kernel: the panel TRSM
 // uses dinv), which is TRTRI's level 0.
@@ -450,6 +470,44 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
     for (int i = 0; i < 32; ++i) x[i] = (i == j) ? 1.0 : 0.0;
     inv_steps(std::make_integer_sequence<int, 32>{}, x, S, b0, rl);
   };
+  // W(q,q) = L(q,q)⁻¹ in place in S, one wave (round 5, GP2D_DIAG_MFMA): the two 16×16
+  // diagonal blocks by forward substitution at once (lanes 0–15 the upper, 16–31 the lower one:
+  // 16 serial steps instead of 32), then W21 = −W22·(L21·W11) as two 16×16×16 products on the
+  // matrix core (T stored over L21, then W21 over T).
+  auto inv_diag_mfma = [&](int q) {
+    const int b0 = 32 * q, h = (lane >> 4) & 1, j = lane & 15, rb0 = b0 + 16 * h;
+    const double rl = 1.0 / S[dsw(b0 + (lane & 31), b0 + (lane & 31))];   // lane i < 32: 1 / L_ii
+    double x[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) x[i] = (i == j) ? 1.0 : 0.0;
+    inv16_steps(std::make_integer_sequence<int, 16>{}, x, S, rb0, rl, h);
+    if (lane < 32) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) S[dsw(rb0 + i, rb0 + j)] = x[i];   // x[i] = 0 above the diagonal
+      if (h == 0) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) S[dsw(b0 + i, b0 + 16 + j)] = 0.0;   // W's upper right quarter
+      }
+    }
+    asm volatile("" ::: "memory");
+    d4 t = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int k0 = 0; k0 < 16; k0 += 4)
+      t = __builtin_amdgcn_mfma_f64_16x16x4f64(S[dsw(b0 + 16 + m16, b0 + k0 + mk)], S[dsw(b0 + k0 + mk, b0 + m16)], t,
+                                               0, 0, 0);
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int r = 0; r < 4; ++r) S[dsw(b0 + 16 + mk + 4 * r, b0 + m16)] = t[r];   // T over L21
+    asm volatile("" ::: "memory");
+    d4 w = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int k0 = 0; k0 < 16; k0 += 4)
+      w = __builtin_amdgcn_mfma_f64_16x16x4f64(S[dsw(b0 + 16 + m16, b0 + 16 + k0 + mk)],
+                                               S[dsw(b0 + 16 + k0 + mk, b0 + m16)], w, 0, 0, 0);
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int r = 0; r < 4; ++r) S[dsw(b0 + 16 + mk + 4 * r, b0 + m16)] = -w[r];   // W21 over T
+  };
   auto put_diag = [&](int q, const double (&x)[32]) {   // x (lanes 0–31) → S's diagonal block q
     const int b0 = 32 * q, j = lane & 31;
     if (lane < 32) {
@@ -502,13 +560,19 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
   __syncthreads();
   GP2D_STAMP(7);
   // P3 | W00, W11 | L column block 2, then W22
+#if !GP2D_DIAG_MFMA
   double xd[32];
+#endif
   if (wid == 0) {
     panel(3);
   } else if (inv) {
     if (wid == 3 && storeL) store_colblock(2, 192, 64);
+#if GP2D_DIAG_MFMA
+    inv_diag_mfma(wid - 1);
+#else
     diag_inverse(wid - 1, xd);
     put_diag(wid - 1, xd);
+#endif
   } else if (storeL) {
     store_colblock(2, 64, 192);
   }
@@ -522,7 +586,11 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
   acc_t acc;
   if (wid == 0) {
     if (storeL) store_colblock(3, 0, 64);
+#if GP2D_DIAG_MFMA
+    inv_diag_mfma(3);   // S(3,3) is nobody else's operand in B
+#else
     diag_inverse(3, xd);
+#endif
   } else if (wid == 1) {
     prod(acc, 1, 0, 0, 0);
     put(1, 0, acc, 1.0);
@@ -537,7 +605,9 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
   // C: W33 → S, W32 = −W33 T32, then T31 | T20 | T21 | T30   (T kept in registers: one
   // accumulator set per wave — S(3,2) is nobody else's operand here)
   if (wid == 0) {
+#if !GP2D_DIAG_MFMA
     put_diag(3, xd);
+#endif
     prod(acc, 3, 2, 3, 3);
     put(3, 2, acc, -1.0);
     prod(acc, 3, 1, 1, 1);
