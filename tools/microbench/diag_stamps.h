@@ -1,4 +1,4 @@
-// diag_stamps.h — dev builds only (hipcc ... -include tools/microbench/diag_stamps.h, tools/runs/r05_diagmf.sh):
+// diag_stamps.h — dev builds only (hipcc ... -include tools/microbench/diag_stamps.h, tools/runs/r05_diaginv.sh):
 // GP2D_STAMP(slot) in potrf_diag_kernel records the cycle counter of workgroup 0's first thread
 // per phase; tools/probe_diag.py reads them through gp2d_debug_diag_stamps.
 #pragma once
