@@ -432,6 +432,12 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
 #pragma unroll
       for (int c = 0; c < 32; c += 2) *reinterpret_cast<d2*>(p1 + c) = d2{x1[c], x1[c + 1]};
     }
+    if (p == 3 && storeL && v0) {   // the last diagonal 32×32 block of L straight from registers
+      double* g = Ab + (int64_t)r0 * lda + c0;
+#pragma unroll
+      for (int c = 0; c < 32; c += 2)
+        *reinterpret_cast<d2*>(g + c) = d2{(c0 + c <= r0) ? x0[c] : 0.0, (c0 + c + 1 <= r0) ? x0[c + 1] : 0.0};
+    }
   };
   // A(bi, bj) −= L(bi, p) · L(bj, p)ᵀ  (32-block indices), one wave
   const int m16 = lane & 15, mk = lane >> 4;   // the MFMA operand / output map
@@ -582,10 +588,9 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
     if (storeL) store_colblock(3, 0, 256);
     return;
   }
-  // B: L column block 3, then W33 (registers) | T10 = L10 W00 → W10 = −W11 T10 | T32 = L32 W22
+  // B: W33 | T10 = L10 W00 → W10 = −W11 T10 | T32 = L32 W22 | L column block 3's zeros
   acc_t acc;
   if (wid == 0) {
-    if (storeL) store_colblock(3, 0, 64);
 #if GP2D_DIAG_MFMA
     inv_diag_mfma(3);   // S(3,3) is nobody else's operand in B
 #else
@@ -599,6 +604,11 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
   } else if (wid == 2) {
     prod(acc, 3, 2, 2, 2);
     put(3, 2, acc, 1.0);
+  } else if (storeL) {   // L's column block 3 above its diagonal block (rows 96–127 left panel 3)
+    for (int e = lane; e < 96 * 16; e += 64) {
+      const int r = e >> 4, c = 96 + 2 * (e & 15);
+      *reinterpret_cast<d2*>(Ab + (int64_t)r * lda + c) = d2{0.0, 0.0};
+    }
   }
   __syncthreads();
   GP2D_STAMP(9);
