@@ -643,7 +643,7 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
   __syncthreads();
   GP2D_STAMP(11);
   double* D = dinv + (int64_t)(k0 / NB) * NB * NB;
-#pragma unroll 1
+#pragma unroll 8
   for (int e = 0; e < (NB * NB / 2) / 256; ++e) {
     const int idx = tid + 256 * e, r = idx >> 6, c = 2 * (idx & 63);
     const d2 v = *reinterpret_cast<const d2*>(S + dsw(r, c));
