@@ -165,7 +165,7 @@ __device__ __forceinline__ void panel_step(double (&x0)[32], double (&x1)[32], d
     }
     constexpr int C0 = (K + 1 + RL) & ~1;
     if constexpr (C0 < 32) {
-      if (lane < 32) colbuf[lane] = x0[K];
+      colbuf[lane] = x0[K];   // all 64 lanes (entries 32–63 unread): no EXEC mask around the store
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
       for (int c = C0; c < 32; c += 2) {
@@ -365,7 +365,7 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
                                                          double* __restrict__ dinv, int* info, int inv_in_place,
                                                          int64_t sA = 0, int64_t sD = 0) {
   __shared__ __attribute__((aligned(16))) double S[DS_DOUBLES];
-  __shared__ __attribute__((aligned(16))) double colbuf[32];
+  __shared__ __attribute__((aligned(16))) double colbuf[64];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   A += blockIdx.x * sA;
   if (dinv) dinv += blockIdx.x * sD;
