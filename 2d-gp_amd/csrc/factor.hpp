@@ -155,7 +155,7 @@ __device__ __forceinline__ void panel_step(double (&x0)[32], double (&x1)[32], d
                                            Pivot& pv) {
   constexpr int RL = GP2D_PANEL_RL;
   bad = (bad == 0 && !(pv.d > 0.0)) ? K + 1 : bad;  // no branch: keeps the pivot chain schedulable
-  x0[K] = (lane > K) ? x0[K] * pv.ird : ((lane == K) ? pv.rd : x0[K]);
+  x0[K] = (lane >= K) ? x0[K] * pv.ird : x0[K];   // lane K: x0[K] = d, so d·(1/√d) = rd exactly
   if constexpr (X1) x1[K] *= pv.ird;
   if constexpr (K < 31) {
     double lc[32];
