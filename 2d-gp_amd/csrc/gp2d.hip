@@ -18,6 +18,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 #include <cmath>
 #include <atomic>
 #include <memory>
@@ -1760,52 +1761,196 @@ int gp2d_transpose(const double* A, int64_t n, int64_t lda, double* At, void* st
   return check_launch("transpose_kernel");
 }
 
-// ------------------------------------------------------------- RCCL broadcast
-// ncclBroadcast of the caller's communicator, resolved at first use from the RCCL the process
-// already has loaded (dlsym(RTLD_DEFAULT), then an RTLD_NOLOAD librccl.so.1: the library that
-// created `comm`), else librccl.so.1 from the ROCm install — no link-time dependency, so the
-// engine loads where RCCL is absent.  `comm` must come from that same RCCL instance.
+// ------------------------------------------------------------- RCCL (the library's communicator)
+// The multi-GPU data path — a job's packed factor, the distributed factor's panels, its W column
+// all-gather, the status all-reduce — runs on an RCCL communicator the library itself creates
+// (gp2d_comm_init from an ncclUniqueId the caller exchanges over any host channel; the Python
+// layer uses torch.distributed's TCP store) and drives on the caller's HIP stream.  RCCL is
+// resolved at first use from the copy the process already has loaded (dlsym(RTLD_DEFAULT), then an
+// RTLD_NOLOAD librccl.so.1 — torch's bundled RCCL carries that soname), else librccl.so.1 from the
+// ROCm install: no link-time dependency, so the engine loads where RCCL is absent.  A communicator
+// must be used with the RCCL instance that made it (gp2d_bcast with a foreign ncclComm_t: the
+// same rule).
 }  // extern "C"
 namespace {
+struct RcclUniqueId { char internal[128]; };   // ncclUniqueId (NCCL_UNIQUE_ID_BYTES)
 typedef int (*rccl_bcast_fn)(const void*, void*, size_t, int, int, void*, hipStream_t);
+typedef int (*rccl_allgather_fn)(const void*, void*, size_t, int, void*, hipStream_t);
+typedef int (*rccl_allreduce_fn)(const void*, void*, size_t, int, int, void*, hipStream_t);
+typedef int (*rccl_p2p_fn)(const void*, size_t, int, int, void*, hipStream_t);   // ncclSend / ncclRecv
+typedef int (*rccl_void_fn)(void);                                             // ncclGroupStart / End
+typedef int (*rccl_uid_fn)(RcclUniqueId*);
+typedef int (*rccl_init_fn)(void**, int, RcclUniqueId, int);
+typedef int (*rccl_comm_fn)(void*);
+typedef int (*rccl_count_fn)(void*, int*);
 typedef const char* (*rccl_errstr_fn)(int);
 struct RcclSyms {
   rccl_bcast_fn bcast = nullptr;
+  rccl_allgather_fn allgather = nullptr;
+  rccl_allreduce_fn allreduce = nullptr;
+  rccl_p2p_fn send = nullptr, recv = nullptr;
+  rccl_void_fn group_start = nullptr, group_end = nullptr;
+  rccl_uid_fn unique_id = nullptr;
+  rccl_init_fn init_rank = nullptr;
+  rccl_comm_fn destroy = nullptr;
+  rccl_count_fn count = nullptr, user_rank = nullptr;
   rccl_errstr_fn errstr = nullptr;
 };
+template <class F> void rccl_sym(void* h, const char* name, F& out) {
+  out = reinterpret_cast<F>(h ? dlsym(h, name) : dlsym(RTLD_DEFAULT, name));
+}
 const RcclSyms& rccl_syms() {
   static const RcclSyms r = [] {
-    RcclSyms x;
-    // 1. whatever RCCL the process already resolves globally (the one that made `comm`, under
-    //    any file name); 2. an already loaded librccl.so.1; 3. the ROCm install's copy
-    x.bcast = reinterpret_cast<rccl_bcast_fn>(dlsym(RTLD_DEFAULT, "ncclBroadcast"));
-    x.errstr = reinterpret_cast<rccl_errstr_fn>(dlsym(RTLD_DEFAULT, "ncclGetErrorString"));
-    if (x.bcast) return x;
-    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
-    if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
-    if (h) {
-      x.bcast = reinterpret_cast<rccl_bcast_fn>(dlsym(h, "ncclBroadcast"));
-      x.errstr = reinterpret_cast<rccl_errstr_fn>(dlsym(h, "ncclGetErrorString"));
+    // 1. whatever RCCL the process already resolves globally; 2. an already loaded librccl.so.1
+    //    (torch's); 3. the ROCm install's copy
+    void* h = nullptr;
+    if (!dlsym(RTLD_DEFAULT, "ncclBroadcast")) {
+      h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+      if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
     }
+    RcclSyms x;
+    if (!h && !dlsym(RTLD_DEFAULT, "ncclBroadcast")) return x;
+    rccl_sym(h, "ncclBroadcast", x.bcast);
+    rccl_sym(h, "ncclAllGather", x.allgather);
+    rccl_sym(h, "ncclAllReduce", x.allreduce);
+    rccl_sym(h, "ncclSend", x.send);
+    rccl_sym(h, "ncclRecv", x.recv);
+    rccl_sym(h, "ncclGroupStart", x.group_start);
+    rccl_sym(h, "ncclGroupEnd", x.group_end);
+    rccl_sym(h, "ncclGetUniqueId", x.unique_id);
+    rccl_sym(h, "ncclCommInitRank", x.init_rank);
+    rccl_sym(h, "ncclCommDestroy", x.destroy);
+    rccl_sym(h, "ncclCommCount", x.count);
+    rccl_sym(h, "ncclCommUserRank", x.user_rank);
+    rccl_sym(h, "ncclGetErrorString", x.errstr);
     return x;
   }();
   return r;
 }
-constexpr int kRcclUint8 = 1;   // ncclUint8
+constexpr int kRcclUint8 = 1, kRcclInt32 = 2, kRcclFloat64 = 8;   // ncclDataType_t
+int rccl_fail(const char* what, int rc) {
+  const RcclSyms& r = rccl_syms();
+  set_error(std::string(what) + " failed: " + (r.errstr ? r.errstr(rc) : "unknown RCCL error"));
+  return -100 - rc;
+}
+#define GP2D_RCCL(sym, what)                                                                   \
+  const RcclSyms& r = rccl_syms();                                                            \
+  GP2D_REQUIRE(r.sym != nullptr, what ": RCCL (librccl.so.1) not found")
 }  // namespace
 extern "C" {
+
+size_t gp2d_comm_id_bytes(void) { return sizeof(RcclUniqueId); }
+
+int gp2d_comm_unique_id(void* id) {
+  GP2D_REQUIRE(id != nullptr, "comm_unique_id: NULL id");
+  GP2D_RCCL(unique_id, "comm_unique_id");
+  const int rc = r.unique_id(static_cast<RcclUniqueId*>(id));
+  return rc ? rccl_fail("ncclGetUniqueId", rc) : 0;
+}
+
+int gp2d_comm_init(void** comm, int nranks, const void* id, int rank, int device) {
+  GP2D_REQUIRE(comm != nullptr && id != nullptr, "comm_init: NULL argument");
+  GP2D_REQUIRE(nranks >= 1 && rank >= 0 && rank < nranks, "comm_init: need 0 <= rank < nranks");
+  GP2D_RCCL(init_rank, "comm_init");
+  if (device >= 0 && hipSetDevice(device) != hipSuccess) { set_error("comm_init: hipSetDevice failed"); return -1; }
+  RcclUniqueId uid;
+  std::memcpy(&uid, id, sizeof(uid));
+  *comm = nullptr;
+  const int rc = r.init_rank(comm, nranks, uid, rank);
+  return rc ? rccl_fail("ncclCommInitRank", rc) : 0;
+}
+
+int gp2d_comm_destroy(void* comm) {
+  if (comm == nullptr) return 0;
+  GP2D_RCCL(destroy, "comm_destroy");
+  const int rc = r.destroy(comm);
+  return rc ? rccl_fail("ncclCommDestroy", rc) : 0;
+}
+
+int gp2d_comm_size(void* comm, int* nranks, int* rank) {
+  GP2D_REQUIRE(comm != nullptr && nranks != nullptr && rank != nullptr, "comm_size: NULL argument");
+  GP2D_RCCL(count, "comm_size");
+  GP2D_REQUIRE(r.user_rank != nullptr, "comm_size: ncclCommUserRank not found");
+  int rc = r.count(comm, nranks);
+  if (rc) return rccl_fail("ncclCommCount", rc);
+  rc = r.user_rank(comm, rank);
+  return rc ? rccl_fail("ncclCommUserRank", rc) : 0;
+}
 
 int gp2d_bcast(void* buf, size_t bytes, int root, void* comm, void* stream) {
   GP2D_REQUIRE(root >= 0, "bcast: root must be >= 0");
   if (bytes == 0) return 0;
   GP2D_REQUIRE(buf != nullptr && comm != nullptr, "bcast: NULL buffer or communicator");
-  const RcclSyms& r = rccl_syms();
-  GP2D_REQUIRE(r.bcast != nullptr, "bcast: RCCL (librccl.so.1, ncclBroadcast) not found");
+  GP2D_RCCL(bcast, "bcast");
   const int rc = r.bcast(buf, buf, bytes, kRcclUint8, root, comm, S(stream));
-  if (rc != 0) {
-    set_error(std::string("bcast: ncclBroadcast failed: ") + (r.errstr ? r.errstr(rc) : "unknown RCCL error"));
-    return -100 - rc;
+  return rc ? rccl_fail("bcast: ncclBroadcast", rc) : 0;
+}
+
+int gp2d_allgather(const void* send, void* recv, size_t bytes_per_rank, void* comm, void* stream) {
+  if (bytes_per_rank == 0) return 0;
+  GP2D_REQUIRE(send != nullptr && recv != nullptr && comm != nullptr, "allgather: NULL argument");
+  GP2D_RCCL(allgather, "allgather");
+  const int rc = r.allgather(send, recv, bytes_per_rank, kRcclUint8, comm, S(stream));
+  return rc ? rccl_fail("allgather: ncclAllGather", rc) : 0;
+}
+
+int gp2d_allreduce(void* buf, size_t count, int dtype, int op, void* comm, void* stream) {
+  GP2D_REQUIRE(dtype == GP2D_COMM_INT32 || dtype == GP2D_COMM_FLOAT64, "allreduce: dtype must be INT32 or FLOAT64");
+  GP2D_REQUIRE(op >= GP2D_COMM_SUM && op <= GP2D_COMM_MIN, "allreduce: op must be SUM, MAX or MIN");
+  if (count == 0) return 0;
+  GP2D_REQUIRE(buf != nullptr && comm != nullptr, "allreduce: NULL argument");
+  GP2D_RCCL(allreduce, "allreduce");
+  const int nccl_op = op == GP2D_COMM_SUM ? 0 : (op == GP2D_COMM_MAX ? 2 : 3);   // ncclSum / ncclMax / ncclMin
+  const int rc = r.allreduce(buf, buf, count, dtype == GP2D_COMM_INT32 ? kRcclInt32 : kRcclFloat64, nccl_op, comm,
+                             S(stream));
+  return rc ? rccl_fail("allreduce: ncclAllReduce", rc) : 0;
+}
+
+int gp2d_sendrecv(const void* send, int send_peer, void* recv, int recv_peer, size_t bytes, void* comm,
+                  void* stream) {
+  if (bytes == 0) return 0;
+  GP2D_REQUIRE(comm != nullptr && (send != nullptr || recv != nullptr), "sendrecv: NULL argument");
+  GP2D_RCCL(send, "sendrecv");
+  GP2D_REQUIRE(r.recv && r.group_start && r.group_end, "sendrecv: ncclRecv / ncclGroupStart not found");
+  int rc = r.group_start();
+  if (rc) return rccl_fail("ncclGroupStart", rc);
+  int rs = 0, rr = 0;
+  if (send != nullptr) rs = r.send(send, bytes, kRcclUint8, send_peer, comm, S(stream));
+  if (recv != nullptr) rr = r.recv(recv, bytes, kRcclUint8, recv_peer, comm, S(stream));
+  rc = r.group_end();
+  if (rs) return rccl_fail("sendrecv: ncclSend", rs);
+  if (rr) return rccl_fail("sendrecv: ncclRecv", rr);
+  return rc ? rccl_fail("ncclGroupEnd", rc) : 0;
+}
+
+int gp2d_stream_create_cumask(int first, int count, void** stream) {
+  // A HIP stream whose kernels may use only the CUs of mask bits [first, first + count).  The
+  // driver deals the mask's bits over the XCDs (bit i → XCD i mod 8), so a range of 8k bits is k
+  // CUs of every XCD.
+  GP2D_REQUIRE(stream != nullptr, "stream_create_cumask: NULL stream");
+  int dev = 0;
+  hipDeviceProp_t prop;
+  if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) {
+    set_error("stream_create_cumask: cannot query the device");
+    return -1;
   }
+  const int ncu = prop.multiProcessorCount;
+  GP2D_REQUIRE(first >= 0 && count >= 1 && first + count <= ncu,
+               "stream_create_cumask: need 0 <= first, 1 <= count, first + count <= CU count");
+  std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+  for (int c = first; c < first + count; ++c) mask[c / 32] |= 1u << (c % 32);
+  hipStream_t s = nullptr;
+  if (hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()) != hipSuccess) {
+    set_error("stream_create_cumask: hipExtStreamCreateWithCUMask failed");
+    return -1;
+  }
+  *stream = s;
+  return 0;
+}
+
+int gp2d_stream_destroy(void* stream) {
+  if (stream == nullptr) return 0;
+  if (hipStreamDestroy(S(stream)) != hipSuccess) { set_error("stream_destroy: hipStreamDestroy failed"); return -1; }
   return 0;
 }
 

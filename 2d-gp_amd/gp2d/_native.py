@@ -12,11 +12,13 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GP2D_LIB", os.path.join(_HERE, "libgp2d.so"))
-ABI_VERSION = 10         # GP2D_ABI_VERSION in include/gp2d.h
+ABI_VERSION = 11         # GP2D_ABI_VERSION in include/gp2d.h
 
 FAMILY_VECTOR2D, FAMILY_ARD_RBF, FAMILY_VECTOR_ST = 0, 1, 2
 KIND_SCALAR, KIND_DIVFREE, KIND_CURLFREE, KIND_MIXED = 0, 1, 2, 3
 VAR_LATENT, VAR_NOISY, VAR_CLIPPED = 0, 1, 2
+COMM_INT32, COMM_FLOAT64 = 2, 8
+COMM_SUM, COMM_MAX, COMM_MIN = 0, 1, 2
 
 # every symbol declared in include/gp2d.h
 EXPORTS = (
@@ -33,7 +35,9 @@ EXPORTS = (
     "gp2d_morton_sort_workspace", "gp2d_morton_sort", "gp2d_gather_rows", "gp2d_obs_pad", "gp2d_lml", "gp2d_lml_grad_count",
     "gp2d_lml_grad_workspace", "gp2d_lml_grad",
     "gp2d_kernel_grad_count", "gp2d_kernel_grad_workspace", "gp2d_kernel_grad",
-    "gp2d_gemm", "gp2d_transpose", "gp2d_bcast", "gp2d_status_flip",
+    "gp2d_gemm", "gp2d_transpose", "gp2d_comm_id_bytes", "gp2d_comm_unique_id", "gp2d_comm_init",
+    "gp2d_comm_destroy", "gp2d_comm_size", "gp2d_bcast", "gp2d_allgather", "gp2d_allreduce", "gp2d_sendrecv",
+    "gp2d_stream_create_cumask", "gp2d_stream_destroy", "gp2d_status_flip",
     "gp2d_dfact_sb", "gp2d_dfact_panel_doubles", "gp2d_dfact_workspace", "gp2d_dfact_panel", "gp2d_dfact_update",
     "gp2d_dfact_invstep", "gp2d_dfact_zpart", "gp2d_dfact_zsum", "gp2d_dfact_alpha_workspace", "gp2d_dfact_alpha_blocks",
     "gp2d_assemble_cols", "gp2d_copy2d", "gp2d_zero_upper", "gp2d_pack_lower_doubles", "gp2d_pack_lower",
@@ -129,7 +133,17 @@ _SIGS = {
     "gp2d_kernel_grad": (_I, [_P, _I64, _P, _I64, _KP, _P, _I64, _P, _P, _SZ, _P]),
     "gp2d_gemm": (_I, [_I, _I64, _I64, _I64, _D, _P, _I64, _P, _I64, _D, _P, _I64, _P]),
     "gp2d_transpose": (_I, [_P, _I64, _I64, _P, _P]),
+    "gp2d_comm_id_bytes": (_SZ, []),
+    "gp2d_comm_unique_id": (_I, [_P]),
+    "gp2d_comm_init": (_I, [ctypes.POINTER(_P), _I, _P, _I, _I]),
+    "gp2d_comm_destroy": (_I, [_P]),
+    "gp2d_comm_size": (_I, [_P, ctypes.POINTER(_I), ctypes.POINTER(_I)]),
     "gp2d_bcast": (_I, [_P, _SZ, _I, _P, _P]),
+    "gp2d_allgather": (_I, [_P, _P, _SZ, _P, _P]),
+    "gp2d_allreduce": (_I, [_P, _SZ, _I, _I, _P, _P]),
+    "gp2d_sendrecv": (_I, [_P, _I, _P, _I, _SZ, _P, _P]),
+    "gp2d_stream_create_cumask": (_I, [_I, _I, ctypes.POINTER(_P)]),
+    "gp2d_stream_destroy": (_I, [_P]),
     "gp2d_status_flip": (_I, [_P, _I, _P]),
     "gp2d_dfact_sb": (_I, []),
     "gp2d_dfact_panel_doubles": (_SZ, [_I64]),

@@ -18,6 +18,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
+from . import comm as C
 from . import data as D
 from . import engine as E
 
@@ -81,7 +82,7 @@ def broadcast_fit(gp: E.GPFit | None, spec: E.KernelSpec, noise: float, x, devic
             meta = torch.tensor(vals, dtype=torch.int64).to(dev)
         else:
             meta = torch.empty(6, dtype=torch.int64, device=dev)
-        dist.broadcast(meta, src)
+        C.broadcast(meta, src)
         n, ntr, npad, st, wbits, kbits = (int(v) for v in meta.tolist())
         if st != 0:
             if rank == src:
@@ -102,7 +103,7 @@ def broadcast_fit(gp: E.GPFit | None, spec: E.KernelSpec, noise: float, x, devic
             status = status.to(dev)
         else:
             status = torch.empty(3, dtype=torch.float64, device=dev)
-        dist.broadcast(status, src)
+        C.broadcast(status, src)
     packed = torch.empty(_packed_len(n), dtype=torch.float64, device=dev)
     owner_ok = rank == src and gp is not None and error is None
     if owner_ok:
@@ -118,9 +119,9 @@ def broadcast_fit(gp: E.GPFit | None, spec: E.KernelSpec, noise: float, x, devic
     # W = L⁻¹ is lower-triangular: only the row blocks' [0, end of their diagonal block)
     # columns travel (≈ half of n² doubles)
     with _timed(comm, "bcast", rank == src, 8 * (packed.numel() + alpha.numel() + X.numel()), ws, device=dev):
-        dist.broadcast(packed, src)
-        dist.broadcast(alpha, src)
-        dist.broadcast(X, src)
+        C.broadcast(packed, src)
+        C.broadcast(alpha, src)
+        C.broadcast(X, src)
     if owner_ok:
         out = gp
     elif planes_only is not None and spec.is_vector and packed.is_cuda and not RECV_UNPACK:
@@ -398,7 +399,7 @@ def fit_distributed(spec: E.KernelSpec, x, y, noise: float, device=None, varianc
             if owner == rank:
                 cstream.wait_event(factored.pop(s))
             with torch.cuda.stream(cstream), _timed(comm, "panel_bcast", owner == rank, 8 * rows * SB, ws, device=dev):
-                dist.broadcast(buf[:rows * SB], owner)
+                C.broadcast(buf[:rows * SB], owner)
             main.wait_stream(cstream)
         elif s in factored:   # one rank: the panel was factored on the chain stream
             main.wait_event(factored.pop(s))
@@ -512,10 +513,7 @@ def _cyclic_order(nsb: int, ws: int, cap: int, dev) -> torch.Tensor:
 
 
 def _all_gather(out: torch.Tensor, t: torch.Tensor, ws: int):
-    if dist.get_backend() == "nccl":
-        dist.all_gather_into_tensor(out, t)
-    else:   # gloo (the CPU / shared-card rehearsals)
-        dist.all_gather(list(out.unbind(0)), t)
+    C.all_gather_into(out, t, ws)
 
 
 def allreduce_first_failure(info: torch.Tensor) -> torch.Tensor:
@@ -534,7 +532,7 @@ def allreduce_first_failure(info: torch.Tensor) -> torch.Tensor:
             info[z] = big
             info[b] = 0
     flip()                                 # 0 ↔ INT32_MAX, so MIN finds the first failure
-    dist.all_reduce(info, op=dist.ReduceOp.MIN)
+    C.all_reduce(info, "min")
     flip()
     return info
 
@@ -556,10 +554,7 @@ def _allgather_w_columns(A: torch.Tensor, n: int, ws: int, rank: int, dev, comm:
         off += rows * SB
     recv = torch.empty(ws * cap, dtype=torch.float64, device=dev)
     with _timed(comm, "w_allgather", True, 8 * sizes[rank], ws, recv=8 * (sum(sizes) - sizes[rank]), device=dev):
-        if dist.get_backend() == "nccl":
-            dist.all_gather_into_tensor(recv, send)
-        else:   # gloo (the CPU / shared-card rehearsals)
-            dist.all_gather(list(recv.view(ws, cap).unbind(0)), send)
+        C.all_gather_into(recv, send, ws)
     for r in range(ws):
         if r == rank:
             continue
@@ -716,8 +711,9 @@ def gather_shards(m: int, bd: int, lo: int, hi: int, mean, var, device, align: i
         k = hi - lo
         for c in range(bd):
             buf[c * maxlen:c * maxlen + k] = t[c * k:(c + 1) * k]
-        parts = [torch.empty_like(buf) for _ in range(ws)]
-        dist.all_gather(parts, buf)
+        allp = torch.empty(ws * buf.numel(), dtype=buf.dtype, device=buf.device)
+        C.all_gather_into(allp, buf, ws)
+        parts = allp.view(ws, -1).unbind(0)
         full = torch.empty(bd * m, dtype=torch.float64, device=device)
         for (a, b), p in zip(ranges, parts):
             k = b - a

@@ -15,6 +15,7 @@ import collections
 import os
 import ctypes
 import itertools
+import math
 import time
 from dataclasses import dataclass, field
 
@@ -81,6 +82,31 @@ def side_stream(device=None) -> torch.cuda.Stream:
     pool streams 6 and 10 of 12 did, profiles/r03_queue_aliasing.json); the high-priority pool is
     a different set of queues."""
     return torch.cuda.Stream(device, priority=-1)
+
+
+class MaskedStream:
+    """A HIP stream restricted to the CUs of mask bits [first, first + count)
+    (gp2d_stream_create_cumask; bit i lies in XCD i mod 8), usable as a torch stream
+    (`.stream`, a torch.cuda.ExternalStream); destroyed with the object."""
+
+    def __init__(self, first: int, count: int, device=None):
+        dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        h = ctypes.c_void_p()
+        with torch.cuda.device(dev):
+            N.check(N.lib().gp2d_stream_create_cumask(int(first), int(count), ctypes.byref(h)),
+                    "gp2d_stream_create_cumask")
+        self.handle = h
+        self.stream = torch.cuda.ExternalStream(h.value, device=dev)
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            try:
+                torch.cuda.synchronize(self.stream.device)
+                N.lib().gp2d_stream_destroy(h)
+            except Exception:   # noqa: BLE001 — interpreter shutdown
+                pass
+            self.handle = None
 
 
 def _as_points(x, dim: int, device) -> torch.Tensor:
@@ -280,8 +306,8 @@ def status_block(device) -> tuple:
     """A fit's device status word: 3 doubles — [0] holds the LAPACK-style info as an int32 in its
     low bytes (gp2d_potrf writes it there through the returned int32 view), [1:3] the accuracy
     guard's statistics (gp2d_ozaki_guard: min latent variance at the observations, max |W|;
-    undefined, and never read, when no guard ran).  One copy to the host (or one broadcast)
-    carries all of it."""
+    NaN when the fit ran no guard — apply_guard then keeps the default precision, so a receiving
+    rank never acts on stale bytes).  One copy to the host (or one broadcast) carries all of it."""
     st = torch.empty(3, dtype=torch.float64, device=device)
     return st, st.view(torch.int32)[0:1]
 
@@ -340,6 +366,12 @@ def apply_guard(gp: GPFit, vmin: float, wmax: float) -> GPFit:
     engine, wbits, kbits, vmin_over_kss, wmax, est."""
     g = gp.extra.get("guard")
     if not g or not g.get("pending"):
+        return gp
+    if math.isnan(vmin):   # the owner's fit ran no guard (status_block's sentinel): default precision
+        g.pop("stream", None)
+        gp.extra.pop("packed", None)
+        g.update(pending=False, engine="ozaki", wbits=OZAKI_DEFAULT_BITS[0], kbits=OZAKI_DEFAULT_BITS[1],
+                 vmin_over_kss=None, wmax=None, est=None)
         return gp
     L = N.lib()
     kss = gp.kernel.kdiag()
@@ -479,6 +511,8 @@ def fit(kernel: KernelSpec, x, y, noise: float, jitter: float = 0.0, device=None
     guard = (GUARD_DEFAULT if guard is None else guard) and variance == "ozaki"
     if guard:   # the guard's statistics from W, into the status word beside info
         _guard_stats(A, n, ntr, npad, noise + jitter, status, dev)
+    else:       # "no guard ran": a receiving rank of the job stream keeps the default precision
+        status[1:].fill_(float("nan"))
     pend = None
     if not check:
         # α (and the ozaki preparation) are enqueued before the status is read (one host sync per
@@ -581,6 +615,8 @@ def fit_batch(problems, variance: str = "f64", jitter: float = 0.0, device=None,
         statuses[b].view(torch.int32)[0:1].copy_(info[b:b + 1])        # a 4-byte device copy
         if guard:
             _guard_stats(A[b], n, ntr, npad, noise + jitter, statuses[b], dev)
+        else:
+            statuses[b, 1:].fill_(float("nan"))
         bd = kernel.block_dim
         Y = _pad_obs(y, ntr, npad, bd, dev, perm)
         alpha = torch.empty(n, dtype=torch.float64, device=dev)
@@ -1114,9 +1150,21 @@ def _krige_jobs_batched(jobs, b, variance, chunk, var_mode, compute_var, jitter,
             for gp in fits:
                 gp.record_stream(main)
         nxt, nfits = None, None
+        # status + accuracy guard of EVERY fit of the batch before the next batch's fit is queued
+        # on `side`: a guard that re-prepares planes then queues that work ahead of the next
+        # batch's factorisation, not behind it (the batch's fits end together, so checking them
+        # all now waits no longer than checking the first); an error raises at its own job
+        errs = []
+        for gp in fits:
+            try:
+                with torch.cuda.stream(side if side is not None else main):
+                    gp.check()
+                errs.append(None)
+            except Exception as e:   # noqa: BLE001 — re-raised when its job is reached
+                errs.append(e)
         for q, (job, gp) in enumerate(zip(group, fits)):
-            with torch.cuda.stream(side if side is not None else main):
-                gp.check()   # status + accuracy guard before the predict (planes re-prepared there)
+            if errs[q] is not None:
+                raise errs[q]
             note_guard(stats, gp)
             if side is not None:
                 gp.ready_on(main)   # only the guard's own work: `side` may carry the next batch's fit

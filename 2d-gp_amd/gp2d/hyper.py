@@ -31,6 +31,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
+from . import comm as C
 from . import engine as E
 
 _BAD = 1e25  # objective for a non-positive-definite K_y (rejected by the line search)
@@ -346,7 +347,7 @@ def allreduce_disjoint(vals: np.ndarray, grads: np.ndarray, device=None):
     v = np.where(bad, 0.0, vals)
     dev = device if (device is not None and torch.cuda.is_available() and dist.get_backend() == "nccl") else "cpu"
     buf = torch.as_tensor(np.concatenate([v, bad.astype(np.float64), grads.reshape(-1)]), device=dev)
-    dist.all_reduce(buf)
+    C.all_reduce(buf, "sum")
     out = buf.cpu().numpy()
     S = vals.size
     v, bad = out[:S], out[S:2 * S] > 0

@@ -79,18 +79,20 @@ class Krig:
     (incl. family='ard' for the sklearn model of krig.scikit_prior).
     var_mode: 'latent' (GP_laser.py:128-131), 'gpy' (+noise, GPy model.predict),
     'sklearn' (+noise, clipped at 0, _gpr.py:473-485).
-    variance: None (default) — the int8 Ozaki-II engine held to the 1e-10 gate by its accuracy
-    guard for the vector kernels (engine.apply_guard: more W bits, or FP64 past its range), the
-    FP64 engine for the ARD family; 'ozaki' / 'f64' force one.
+    variance: 'f64' (default) — the FP64-MFMA engine, FP64 arithmetic throughout as in the
+    reference; 'ozaki' (opt-in, vector kernels) — the int8 Ozaki-II emulation of the same FP64
+    product, held to the 1e-10 gate by its calibrated accuracy guard (engine.apply_guard: more
+    W bits, or FP64 past its range).  The job-stream API (engine.krige_jobs) and bench.py use
+    'ozaki'; the drop-in object keeps the reference's arithmetic unless asked.
     """
 
     def __init__(self, kernel="df", l_df: float = 5.0, l_cf: float = 5.0, ratio: float = None,
                  noise: float = 0.0025, jitter: float = 0.0, var_mode: str = "latent", device=None,
-                 chunk: int = 8192, variance: str | None = None, jitchol: int = 0):
+                 chunk: int = 8192, variance: str = "f64", jitchol: int = 0):
         self.spec = self._make_spec(kernel, l_df, l_cf, ratio)
         self.jitchol = int(jitchol)   # GPy jitchol retries on a non-PD K_y (engine.fit)
-        if variance is None:   # the int8 engine under its accuracy guard where it applies (vector kernels)
-            variance = "ozaki" if self.spec.is_vector else "f64"
+        if variance == "ozaki" and not self.spec.is_vector:
+            raise ValueError("the ozaki variance engine supports the vector kernels only")
         if variance not in E.VARIANCE_ENGINES:
             raise ValueError(f"variance must be one of {E.VARIANCE_ENGINES}")
         self.variance = variance
@@ -232,7 +234,7 @@ class Krig:
             spec = E.KernelSpec(family=fam, kind=str(z["kind"]), l_df=float(z["l_df"]), l_cf=float(z["l_cf"]),
                                 ratio=float(z["ratio"]), **st)
         extra = {}
-        if "variance" in z.files:
+        if "variance" in z.files:   # older checkpoints carry none: they were written by the f64 engine
             extra = dict(variance=str(z["variance"]), chunk=int(z["chunk"]))
         if "jitchol" in z.files:
             extra["jitchol"] = int(z["jitchol"])

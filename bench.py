@@ -186,8 +186,21 @@ def setup_dist(args):
         backend = os.environ.get("GP2D_DIST_BACKEND", "nccl")
         kw = {"device_id": torch.device("cuda", local)} if backend == "nccl" else {}
         dist.init_process_group(backend, **kw)
+        if backend == "nccl":
+            # the library's own RCCL communicator carries the data path (gp2d/comm.py): made here,
+            # before any warmup, from an ncclUniqueId exchanged over torch.distributed's store
+            from gp2d import comm as GC
+            GC.get(torch.device("cuda", local))
         return dist.get_world_size(), dist.get_rank(), torch.device("cuda", local)
     return 1, 0, torch.device("cuda", 0)
+
+
+def finish_dist():
+    from gp2d import comm as GC
+    dist.barrier()
+    torch.cuda.synchronize()
+    GC.shutdown()
+    dist.destroy_process_group()
 
 
 def barrier(ws):
@@ -295,8 +308,7 @@ def run_sweep(args, ws, rank, dev):
         }
         print(json.dumps(out), flush=True)
     if is_multi(ws):
-        dist.barrier()
-        dist.destroy_process_group()
+        finish_dist()
 
 
 def comm_block(comm: dict, keys, per: int, ws: int, dev) -> dict:
@@ -378,23 +390,27 @@ def extra_readings_n1(args, spec, xt, yt, noise, xg, m_all):
         out["f64"] = {"value": m_all * args.f64_steps / dt, "ms_per_step": 1e3 * dt / args.f64_steps,
                       "steps": args.f64_steps, "api": "engine.krige_jobs(variance='f64')"}
     if args.dropin_steps > 0:
-        def one():
-            k = K.Krig(spec.kind, l_df=spec.l_df, l_cf=spec.l_cf, ratio=spec.ratio, noise=noise).fit(xt, yt)
-            mu, var = k.predict_device(xg)
-            return k, mu, var
-        k, _, _ = one()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(args.dropin_steps):
+        # the drop-in object's default (variance='f64', the reference's arithmetic) and its opt-in
+        # guarded int8 engine (variance='ozaki'), one job at a time each
+        for key, variance in (("dropin", "ozaki"), ("dropin_f64", "f64")):
+            def one():
+                k = K.Krig(spec.kind, l_df=spec.l_df, l_cf=spec.l_cf, ratio=spec.ratio, noise=noise,
+                           variance=variance).fit(xt, yt)
+                mu, var = k.predict_device(xg)
+                return k, mu, var
             k, _, _ = one()
-        torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
-        g = k.gp.extra.get("guard") or {}
-        out["dropin"] = {"value": m_all * args.dropin_steps / dt, "ms_per_step": 1e3 * dt / args.dropin_steps,
-                         "steps": args.dropin_steps,
-                         "api": "krig.Krig(kind, l_df, noise).fit(X, obs).predict_device(grid)",
-                         "variance_engine": k.variance if k.variance == "f64" else g.get("engine", "ozaki"),
-                         "guard_bits": [g.get("wbits"), g.get("kbits")]}
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.dropin_steps):
+                k, _, _ = one()
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            g = k.gp.extra.get("guard") or {}
+            out[key] = {"value": m_all * args.dropin_steps / dt, "ms_per_step": 1e3 * dt / args.dropin_steps,
+                        "steps": args.dropin_steps,
+                        "api": f"krig.Krig(kind, l_df, noise, variance='{variance}').fit(X, obs).predict_device(grid)",
+                        "variance_engine": k.variance if k.variance == "f64" else g.get("engine", "ozaki"),
+                        "guard_bits": [g.get("wbits"), g.get("kbits")]}
     return out
 
 
@@ -612,6 +628,11 @@ def main():
         comm_out["what"] = ("per timed job, MAX over ranks: the job's factor broadcast from its fitting rank (packed "
                             "W + alpha + X_train + the status block), RCCL on the comm stream under the predict; "
                             "recv_prepare: a receiving rank's int8 planes from the packed payload (no bytes)")
+        from gp2d import comm as GC
+        lc = GC.get(dev)
+        comm_out["transport"] = ("the library's own RCCL communicator (gp2d_comm_init; gp2d_bcast on the comm stream)"
+                                 if lc is not None else f"torch.distributed ({dist.get_backend()}) rehearsal")
+        comm_out["library_calls"] = dict(lc.calls) if lc is not None else None
 
     # one job alone (unpipelined, its grid sharded over the ranks; at N > 1 fitted on rank 0 and
     # broadcast): the single-job reading beside the job-stream value
@@ -651,8 +672,7 @@ def main():
 
     if rank != 0:
         if is_multi(ws):
-            dist.barrier()
-            dist.destroy_process_group()
+            finish_dist()
         return
 
     achieved = kflops / (kms * 1e-3) / 1e12 if kms > 0 else None
@@ -745,8 +765,7 @@ def main():
         out["cpu_baseline"] = cpu_baseline(x, y, xg_all, args.kind, 5.0, noise, args.cpu_sample_points)
     print(json.dumps(out), flush=True)
     if is_multi(ws):
-        dist.barrier()
-        dist.destroy_process_group()
+        finish_dist()
 
 
 if __name__ == "__main__":

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define GP2D_ABI_VERSION 10
+#define GP2D_ABI_VERSION 11
 
 /* kernel families */
 #define GP2D_FAMILY_VECTOR2D 0   /* 2×2 matrix-valued SE kernels on (x1, x2)          */
@@ -395,16 +395,43 @@ int gp2d_zero_upper(double* A, int64_t n, int64_t lda, void* stream);
 size_t gp2d_pack_lower_doubles(int64_t n);
 int gp2d_pack_lower(double* W, int64_t n, int64_t ldw, double* packed, int unpack, void* stream);
 
-/* ---- multi-GPU: factor broadcast --------------------------------
- * gp2d_bcast: in-place ncclBroadcast of `bytes` bytes of device memory from rank `root` over
- *   the caller's RCCL communicator (`comm` is an ncclComm_t), on `stream`.  The fit of rank 0
- *   (W = L⁻¹ packed, α, the Morton-ordered training points) goes out this way in the bcast
- *   fit mode; a C/C++ host that owns its communicator calls it directly (the Python layer
- *   uses torch.distributed's broadcast on the same RCCL, gp2d/distributed.py).  There is no
- *   reference call it replaces — the reference is single-process.  RCCL is
- *   resolved at first call (no link-time dependency).  Returns −100 − ncclResult_t on an RCCL
- *   failure.                                                                             */
+/* ---- multi-GPU: the library's own RCCL communicator ----------------
+ * The reference is single-process; its parallelism is the job array runKrig.py:7,14-17 and the
+ * per-slice predict krig.py:541-557.  These entries carry the multi-GPU data path over RCCL on
+ * xGMI — a job's packed factor W = L⁻¹ + α + training points (gp2d/distributed.py
+ * broadcast_fit), the distributed factor's panels, its W column all-gather and its status
+ * all-reduce — on a communicator the library creates, driven on the caller's HIP stream.  RCCL
+ * is resolved at first call (no link-time dependency); every entry returns −100 − ncclResult_t
+ * on an RCCL failure.
+ * gp2d_comm_id_bytes / gp2d_comm_unique_id: the ncclUniqueId (128 bytes) rank 0 makes and the
+ *   caller hands to every rank over its own host channel (the Python layer: torch.distributed's
+ *   TCP store).
+ * gp2d_comm_init: ncclCommInitRank on HIP device `device` (−1: the current one); collective over
+ *   the nranks processes.  gp2d_comm_destroy frees it; gp2d_comm_size reads (nranks, rank).
+ * gp2d_bcast: in-place ncclBroadcast of `bytes` bytes from rank `root` (any communicator of the
+ *   resolved RCCL, including the caller's own).
+ * gp2d_allgather: ncclAllGather of bytes_per_rank bytes per rank, rank order.
+ * gp2d_allreduce: in-place ncclAllReduce of `count` INT32 / FLOAT64 values, op SUM / MAX / MIN.
+ * gp2d_sendrecv: one grouped ncclSend (send → send_peer) + ncclRecv (recv ← recv_peer) of
+ *   `bytes` bytes; either pointer may be NULL; a rank may name itself (an RCCL copy kernel).
+ * gp2d_stream_create_cumask: a HIP stream whose kernels use only the CUs of mask bits
+ *   [first, first + count) (hipExtStreamCreateWithCUMask; the driver deals the bits over the
+ *   XCDs, bit i → XCD i mod 8) — e.g. a communication stream on a few CUs of every XCD beside a
+ *   predict stream on the rest; gp2d_stream_destroy.                                        */
+enum { GP2D_COMM_INT32 = 2, GP2D_COMM_FLOAT64 = 8 };
+enum { GP2D_COMM_SUM = 0, GP2D_COMM_MAX = 1, GP2D_COMM_MIN = 2 };
+size_t gp2d_comm_id_bytes(void);
+int gp2d_comm_unique_id(void* id);
+int gp2d_comm_init(void** comm, int nranks, const void* id, int rank, int device);
+int gp2d_comm_destroy(void* comm);
+int gp2d_comm_size(void* comm, int* nranks, int* rank);
 int gp2d_bcast(void* buf, size_t bytes, int root, void* comm, void* stream);
+int gp2d_allgather(const void* send, void* recv, size_t bytes_per_rank, void* comm, void* stream);
+int gp2d_allreduce(void* buf, size_t count, int dtype, int op, void* comm, void* stream);
+int gp2d_sendrecv(const void* send, int send_peer, void* recv, int recv_peer, size_t bytes, void* comm,
+                  void* stream);
+int gp2d_stream_create_cumask(int first, int count, void** stream);
+int gp2d_stream_destroy(void* stream);
 /* gp2d_status_flip: 0 ↔ INT32_MAX on `count` device status words (an involution).  Applied
  *   before and after an all-reduce MIN of LAPACK-style info words (0 = success, k > 0 = first
  *   non-PD minor), it makes the reduction return the FIRST failing minor over the ranks, or 0 —

@@ -41,6 +41,7 @@ def test_bench_json_contract(variance):
     # N = 1 readings beside the headline: the strict FP64 engine and the Krig drop-in surface
     assert d["f64_value"] > 0 and d["f64"]["steps"] == 5
     assert d["dropin"]["value"] > 0 and d["dropin"]["variance_engine"] in ("ozaki", "f64")
+    assert d["dropin_f64"]["value"] > 0 and d["dropin_f64"]["variance_engine"] == "f64"   # Krig's default
     if variance == "ozaki":   # the accuracy guard's decision for the timed jobs
         assert d["guard"]["engine"] in ("ozaki", "f64") and d["guard"]["vmin_over_kss"] > 0
     # the job shape krige_jobs resolved: a batch only back to back, batch_ahead only for a batch
@@ -110,6 +111,9 @@ def test_bench_multi_rank_paths_under_rccl():
     assert d["timed_fits"]["issued_in_window"] == d["timed_fits"]["issued_total"] == 3
     assert d["single_job"]["distributed_fit"]["ms"] > 0
     assert d["comm"]["bcast"]["calls_per_job"] == 1 and d["comm"]["bcast"]["ms_per_job_max_over_ranks"] > 0
+    # the job stream's factor broadcasts went through the library's own RCCL communicator
+    assert d["comm"]["transport"].startswith("the library's own RCCL communicator")
+    assert d["comm"]["library_calls"]["broadcast"] >= 4 * (3 + 1)   # status + packed W + alpha + X per job
 
 
 def test_bench_gpus2_self_launch():

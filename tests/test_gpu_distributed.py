@@ -121,6 +121,82 @@ def test_gp2d_bcast_native_rccl():
         rccl.ncclCommDestroy(comm)
 
 
+def _lib_comm_worker(rank, world, port, out_dir):
+    """One rank on RCCL (the 'nccl' backend) with GP2D_FORCE_COLLECTIVES=1: the library's own
+    communicator (gp2d/comm.py, gp2d_comm_init from a unique id sent through torch's store)
+    carries every collective of the job stream and of the distributed factor."""
+    for p in (ROOT, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GP2D_FORCE_COLLECTIVES="1")
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    from gp2d import comm as C
+    from gp2d import distributed as GD
+    c = C.get(dev)
+    out = {}
+    # the primitives on one rank: broadcast keeps the root's bytes, all-gather copies, the
+    # reductions return the input, a send/receive to itself copies (RCCL's copy kernel)
+    x = torch.arange(1 << 16, dtype=torch.float64, device=dev)
+    y = x.clone()
+    c.broadcast(y, 0)
+    g = torch.empty_like(x)
+    c.all_gather_into(g, x)
+    i = torch.tensor([5, 0, 2147483647], dtype=torch.int32, device=dev)
+    c.all_reduce(i, "min")
+    f = torch.tensor([1.5, -2.0], dtype=torch.float64, device=dev)
+    c.all_reduce(f, "sum")
+    r = torch.empty_like(x)
+    c.sendrecv(x, 0, r, 0)
+    torch.cuda.synchronize()
+    out.update(bcast_ok=torch.equal(y, x), gather_ok=torch.equal(g, x), sendrecv_ok=torch.equal(r, x),
+               imin=i.cpu().numpy(), fsum=f.cpu().numpy())
+    before = dict(c.calls)
+    res = {}
+    for j, (lo, hi, mean, var) in enumerate(GD.krige_jobs_sharded(_jobs(), variance="ozaki", chunk=1024)):
+        res[f"mean{j}"], res[f"var{j}"] = mean.cpu().numpy(), var.cpu().numpy()
+    stream_bcasts = c.calls.get("broadcast", 0) - before.get("broadcast", 0)
+    xd, yd, _ = _dfit_problem(1024)
+    spec = GD.E.KernelSpec(kind="df", l_df=5.0)
+    before = dict(c.calls)
+    gp = GD.fit_distributed(spec, torch.tensor(xd, device=dev), torch.tensor(yd, device=dev), 0.0025, dev)
+    torch.cuda.synchronize()
+    dfit_calls = {k: c.calls.get(k, 0) - before.get(k, 0) for k in c.calls}
+    np.savez(os.path.join(out_dir, "libcomm.npz"), stream_bcasts=stream_bcasts, W_sha=_sha(gp.W),
+             alpha=gp.alpha.cpu().numpy(), dfit_bcast=dfit_calls.get("broadcast", 0),
+             dfit_gather=dfit_calls.get("all_gather", 0), dfit_reduce=dfit_calls.get("all_reduce", 0), **out, **res)
+    torch.cuda.synchronize()
+    dist.barrier()
+    C.shutdown()
+    dist.destroy_process_group()
+
+
+def test_library_rccl_communicator_one_rank(tmp_path):
+    """The multi-GPU data path on the library's own RCCL communicator: the
+    primitives, the job stream's factor broadcasts (4 gp2d_bcast per job: status, packed W, α,
+    X) and the distributed factor's panel broadcasts / all-gathers / status all-reduce, all
+    through gp2d_comm_*; the results equal one process's without any collective, bit for bit."""
+    from gp2d import distributed as GD
+    from gp2d import engine as E
+    _spawn(_lib_comm_worker, 1, str(tmp_path))
+    r = np.load(os.path.join(tmp_path, "libcomm.npz"))
+    assert bool(r["bcast_ok"]) and bool(r["gather_ok"]) and bool(r["sendrecv_ok"])
+    assert r["imin"].tolist() == [5, 0, 2147483647] and r["fsum"].tolist() == [1.5, -2.0]
+    jobs = _jobs()
+    assert int(r["stream_bcasts"]) == 4 * len(jobs)
+    for j, (spec, x, y, noise, xg) in enumerate(jobs):
+        gp = E.fit(spec, x, y, noise, variance="ozaki")
+        mu, var = (t.cpu().numpy() for t in E.Predictor(gp, 1024)(xg))
+        assert np.array_equal(r[f"mean{j}"], mu) and np.array_equal(r[f"var{j}"], var), j
+    xd, yd, _ = _dfit_problem(1024)
+    gp1 = GD.fit_distributed(E.KernelSpec(kind="df", l_df=5.0), xd, yd, 0.0025)   # no process group
+    assert np.array_equal(r["W_sha"], _sha(gp1.W)) and np.array_equal(r["alpha"], gp1.alpha.cpu().numpy())
+    nsb = gp1.W.shape[0] // GD.super_block()
+    assert int(r["dfit_bcast"]) == nsb and int(r["dfit_gather"]) == 3 and int(r["dfit_reduce"]) == 1
+
+
 def _jobs(noises=None):
     """Five small jobs; noises (optional): per-job noise overrides (the accuracy guard's range)."""
     from gp2d import engine as E

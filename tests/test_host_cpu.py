@@ -24,7 +24,7 @@ def test_library_exports_every_header_symbol():
     for s in syms:
         assert hasattr(L, s), s
     assert set(syms) == set(_native.EXPORTS)
-    assert L.gp2d_abi_version() == _native.ABI_VERSION == 10
+    assert L.gp2d_abi_version() == _native.ABI_VERSION == 11
     assert L.gp2d_padded_points(1) == 64 and L.gp2d_padded_points(64) == 64 and L.gp2d_padded_points(65) == 128
 
 
@@ -58,6 +58,19 @@ def test_argument_errors_are_reported():
     assert L.gp2d_bcast(None, 0, 0, None, None) == 0            # nothing to send
     rc = L.gp2d_bcast(one, 8, 0, None, None)
     assert rc < 0 and b"communicator" in L.gp2d_last_error()
+    # the library's own communicator: argument checks before RCCL is touched
+    assert L.gp2d_comm_id_bytes() == 128                          # ncclUniqueId
+    cm = ctypes.c_void_p()
+    rc = L.gp2d_comm_init(ctypes.byref(cm), 2, one, 2, -1)
+    assert rc < 0 and b"rank < nranks" in L.gp2d_last_error()
+    rc = L.gp2d_allreduce(one, 4, 1, N.COMM_MIN, one, None)       # ncclUint8 is not a reduction type here
+    assert rc < 0 and b"dtype" in L.gp2d_last_error()
+    rc = L.gp2d_allreduce(one, 4, N.COMM_INT32, 7, one, None)
+    assert rc < 0 and b"op" in L.gp2d_last_error()
+    assert L.gp2d_allgather(None, None, 0, None, None) == 0       # nothing to gather
+    rc = L.gp2d_sendrecv(None, 0, None, 0, 8, one, None)
+    assert rc < 0 and b"NULL" in L.gp2d_last_error()
+    assert L.gp2d_comm_destroy(None) == 0 and L.gp2d_stream_destroy(None) == 0
     rc = L.gp2d_bcast(one, 8, -1, one, None)
     assert rc < 0 and b"root" in L.gp2d_last_error()
     # distributed factor (one job over several GPUs): argument checks before any device work
