@@ -55,6 +55,12 @@ nbytes = int(a.mb * 1e6) // 16 * 16
 src = torch.ones(nbytes // 8, dtype=torch.float64, device=dev)
 dst = torch.empty_like(src)
 masks = [int(r) for r in a.mask.split(",") if r]
+# every variant uses the SAME streams: the job stream's fit side stream (krige_jobs draws one from
+# torch's high-priority pool per call, and which pool stream it gets moves its hardware queue —
+# tools/probe_stream_pick.py) and the copy's stream are drawn once here
+copy_side = E.side_stream(dev)
+fit_side = E.side_stream(dev)
+E.side_stream = lambda device=None, _s=fit_side: _s
 
 
 def run(variant, jobs):
@@ -73,7 +79,7 @@ def run(variant, jobs):
         keep.append(cs)
         cstream = cs.stream
     else:
-        cstream = E.side_stream(dev)
+        cstream = copy_side
     evs = []
     with torch.cuda.stream(pstream):
         for _ in E.krige_jobs(itertools.repeat(job, 2), variance="ozaki"):   # warm
