@@ -135,23 +135,54 @@ __device__ __forceinline__ double ard_value(const ArdParams& p, const double* a,
 // Block: 64 (column points) × 4 thread rows; each thread does ROWS_PER_THREAD
 // row points so that the column point's coordinates are loaded once.
 constexpr int ASM_ROWS = 16;
+constexpr int ASM_LOWER = 2;   // `symmetric` mode: K_y's lower block triangle only (gp2d_assemble)
 
 // j_off / col_comp (gp2d_assemble_cols): column points start at j_off and only the columns of
 // component col_comp (0: u, 1: v; −1: both) are written — the same per-element arithmetic.
+//
+// The workgroup's 64 column points are staged once through LDS (wave 0 loads the tile with one
+// coalesced 1–1.5 KB read, every wave reads it back); the row point of a wave is wave-uniform
+// (readfirstlane'd index: scalar loads).  symmetric = ASM_LOWER writes only the entries (R, C)
+// of the n × n matrix (n = 2·na_pad, component-major) with C < 128·(R/128 + 1) — the lower block
+// triangle including the 128 × 128 diagonal blocks, which is all gp2d_potrf reads (it zeroes
+// the rest at its end) — i.e. K_uu's and K_vv's lower halves and all of K_vu: half the stores
+// (GP_scripts.py:80-88 likewise fills one triangle of compute_K and mirrors it).  A wave's 64
+// columns lie on one side of every 128 boundary (64-aligned), so whole row segments drop.
 __global__ __launch_bounds__(256) void assemble_vec_kernel(
     const double* __restrict__ xa, int64_t na, int64_t na_pad,
     const double* __restrict__ xb, int64_t nb, int64_t nb_pad,
     VecParams p, double diag_add, int symmetric, double* __restrict__ out, int64_t ld, int64_t j_off = 0,
     int col_comp = -1) {
-  const int64_t j = j_off + (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
-  const int ty = threadIdx.x >> 6;
+  __shared__ double colpts[3 * 64];
+  const int64_t jt = j_off + (int64_t)blockIdx.x * 64;   // the tile's first column point
+  const int lane = threadIdx.x & 63;
+  const int ty = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t j = jt + lane;
   const bool jv = j < nb;
+  const bool lower = symmetric == ASM_LOWER;
+  if (ty == 0) {
+    for (int e = lane; e < p.pdim * 64; e += 64) {   // the tile's points, coalesced
+      const int64_t g = jt * p.pdim + e;
+      colpts[e] = (g < nb * p.pdim) ? xb[g] : 0.0;
+    }
+  }
+  __syncthreads();
   double b0 = 0.0, b1 = 0.0, b2 = 0.0;
-  if (jv) vec_point(p, xb, j, b0, b1, b2);
+  if (p.pdim == 3) {
+    b0 = colpts[3 * lane]; b1 = colpts[3 * lane + 1]; b2 = colpts[3 * lane + 2];
+  } else {
+    b1 = colpts[2 * lane]; b2 = colpts[2 * lane + 1];
+  }
+  // lower-block limits: column C is kept in matrix row R iff C < 128·(R/128 + 1)
+  const int64_t cu = jt, cv = nb_pad + jt;   // the wave's first matrix column in each component
 #pragma unroll 1
   for (int q = 0; q < ASM_ROWS / 4; ++q) {
-    const int64_t i = (int64_t)blockIdx.y * ASM_ROWS + ty + 4 * q;
+    const int64_t i = (int64_t)blockIdx.y * ASM_ROWS + ty + 4 * q;   // wave-uniform
     if (i >= na_pad) break;
+    const int64_t lim0 = (i / 128 + 1) * 128, lim1 = ((na_pad + i) / 128 + 1) * 128;
+    const bool w_uu = !lower || cu < lim0, w_uv = !lower || cv < lim0;
+    const bool w_vu = !lower || cu < lim1, w_vv = !lower || cv < lim1;
+    if (!(w_uu || w_uv || w_vu || w_vv)) continue;
     double k11, k12, k22;
     if (jv && i < na) {
       double a0, a1, a2;
@@ -165,12 +196,12 @@ __global__ __launch_bounds__(256) void assemble_vec_kernel(
     double* r0 = out + i * ld;
     double* r1 = out + (na_pad + i) * ld;
     if (col_comp != 1) {
-      r0[j] = k11;
-      r1[j] = k12;
+      if (w_uu) r0[j] = k11;
+      if (w_vu) r1[j] = k12;
     }
     if (col_comp != 0) {
-      r0[nb_pad + j] = k12;
-      r1[nb_pad + j] = k22;
+      if (w_uv) r0[nb_pad + j] = k12;
+      if (w_vv) r1[nb_pad + j] = k22;
     }
   }
 }

@@ -5,6 +5,16 @@
 #include <cstdio>
 #include <string>
 
+// The product library is compiled with -DGP2D_RELEASE=1 (__graft_entry__.build_lib).  A few
+// tuning constants of the headers can be overridden by -DGP2D_<NAME> in measurement builds
+// (tools/microbench compiles the headers into its own benches); in a release compile any such
+// override is an error, so no measurement switch reaches a shipped libgp2d.so.
+#if defined(GP2D_RELEASE) &&                                                                   \
+    (defined(GP2D_STAMP) || defined(GP2D_OZ_P) || defined(GP2D_OZ_PW) || defined(GP2D_OZ_PB) || \
+     defined(GP2D_KS_OCC) || defined(GP2D_KS_PPL) || defined(GP2D_CRT_RPL) || defined(GP2D_CRT_OCC))
+#error "gp2d: measurement overrides (-DGP2D_<NAME>) are not allowed in a GP2D_RELEASE build"
+#endif
+
 namespace gp2d {
 
 typedef double d4 __attribute__((ext_vector_type(4)));

@@ -139,38 +139,30 @@ __device__ __forceinline__ Pivot make_pivot(double d) {
 // One pivot of the single-wave panel factorisation (K is a compile-time column index so
 // that x0/x1 stay in registers).  Column K+1 is updated first and pivot K+1 is formed
 // right after it, so its rsq/Newton chain overlaps the remaining FMAs of step K.
-// The multipliers L[c][K] come through one LDS broadcast of the column.  (Dev builds can take
-// the next GP2D_PANEL_RL columns' multipliers straight from lane c's register by v_readlane
-// instead, so the pivot chain K → K+1 carries no LDS round trip: 1, 2 and 4 such columns measured
+// The multipliers L[c][K] come through one LDS broadcast of the column.  (Taking the next 1, 2
+// or 4 columns' multipliers straight from lane c's register by v_readlane instead, so the pivot
+// chain K → K+1 carries no LDS round trip (git 00ed20f, GP2D_PANEL_RL), measured
 // 54.4–54.9 µs per diagonal block against 54.0 µs — the panel wave is issue-bound on its
 // 2·(31 − K) FMAs per pivot, not bound by the broadcast's latency; tools/microbench diag_bench_rl*.
 // Round 5 took the chain itself off the issue stream — uniform-value pivot chain, bulk update one
 // step late, broadcast under the next pivot — bit-identical and −1.2 %: a lone wave's issue of
 // the whole step sets the pivot time; profiles/r05_diag_panel_ab.txt, git 9434024.)
-#ifndef GP2D_PANEL_RL
-#define GP2D_PANEL_RL 0
-#endif
 template <int K, bool X1>
 __device__ __forceinline__ void panel_step(double (&x0)[32], double (&x1)[32], double* colbuf, int lane, int& bad,
                                            Pivot& pv) {
-  constexpr int RL = GP2D_PANEL_RL;
   bad = (bad == 0 && !(pv.d > 0.0)) ? K + 1 : bad;  // no branch: keeps the pivot chain schedulable
   x0[K] = (lane >= K) ? x0[K] * pv.ird : x0[K];   // lane K: x0[K] = d, so d·(1/√d) = rd exactly
   if constexpr (X1) x1[K] *= pv.ird;
   if constexpr (K < 31) {
     double lc[32];
-    if constexpr (RL > 0) {
-#pragma unroll
-      for (int c = K + 1; c < 32 && c <= K + RL; ++c) lc[c] = readlane_f64(x0[K], c);
-    }
-    constexpr int C0 = (K + 1 + RL) & ~1;
+    constexpr int C0 = (K + 1) & ~1;
     if constexpr (C0 < 32) {
       colbuf[lane] = x0[K];   // all 64 lanes (entries 32–63 unread): no EXEC mask around the store
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
       for (int c = C0; c < 32; c += 2) {
         const d2 t = *reinterpret_cast<const d2*>(colbuf + c);
-        if (c > K + RL) lc[c] = t.x;
+        if (c > K) lc[c] = t.x;
         lc[c + 1] = t.y;
       }
     }
@@ -205,99 +197,11 @@ __device__ __forceinline__ int panel_steps(std::integer_sequence<int, Ks...>, do
   return bad;
 }
 
-// Column step K of the forward substitution L X = I, 32×32 block at b0 (lane ↔ column j
-// of X): finalise x[K] (rl: lane i holds 1 / L_ii), then eliminate it from the rows below
-// (pinned like panel_step).
-template <int K>
-__device__ __forceinline__ void inv_step(double (&x)[32], const double* S, int b0, double rl) {
-  double lk[32];  // column K below the diagonal: all reads issued before the first use
-#pragma unroll
-  for (int i = K + 1; i < 32; ++i) lk[i] = S[dsw(b0 + i, b0 + K)];
-  x[K] = x[K] * readlane_f64(rl, K);
-#pragma unroll
-  for (int i = K + 1; i < 32; ++i) {
-    x[i] = fma(-lk[i], x[K], x[i]);
-    asm volatile("" : "+v"(x[i]));
-  }
-}
-template <int... Ks>
-__device__ __forceinline__ void inv_steps(std::integer_sequence<int, Ks...>, double (&x)[32], const double* S, int b0,
-                                          double rl) {
-  (inv_step<Ks>(x, S, b0, rl), ...);
-}
-
-// 4×4 register tile of a 32×32 block product, one wave per block (lane → rows
-// xr..xr+3, columns yc..yc+3):  acc[a][b] += Σ_{k<32} X[xr+a][xk+k] · Y(k, yc+b), with
-// Y(k, c) = S[yk+k][c] (NT = false) or S[c][yk+k] (NT = true, i.e. Y = the transpose of
-// rows yc..yc+3).  Fully unrolled so every LDS read is issued ahead of its FMAs; 16
-// independent accumulator chains.
-template <bool NT>
-__device__ __forceinline__ void tile4x4(const double* __restrict__ S, int xr, int xk, int yk, int yc,
-                                        double (&acc)[4][4]) {
-#pragma unroll
-  for (int k = 0; k < 32; k += 2) {
-    d2 x[4], y[4];
-#pragma unroll
-    for (int a = 0; a < 4; ++a) x[a] = *reinterpret_cast<const d2*>(S + dsw(xr + a, xk + k));
-    if constexpr (NT) {
-#pragma unroll
-      for (int b = 0; b < 4; ++b) y[b] = *reinterpret_cast<const d2*>(S + dsw(yc + b, yk + k));
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-          acc[a][b] = fma(x[a].x, y[b].x, acc[a][b]);
-          acc[a][b] = fma(x[a].y, y[b].y, acc[a][b]);
-        }
-    } else {
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        y[2 * u] = *reinterpret_cast<const d2*>(S + dsw(yk + k + u, yc));
-        y[2 * u + 1] = *reinterpret_cast<const d2*>(S + dsw(yk + k + u, yc + 2));
-      }
-#pragma unroll
-      for (int a = 0; a < 4; ++a) {
-        acc[a][0] = fma(x[a].x, y[0].x, acc[a][0]);
-        acc[a][1] = fma(x[a].x, y[0].y, acc[a][1]);
-        acc[a][2] = fma(x[a].x, y[1].x, acc[a][2]);
-        acc[a][3] = fma(x[a].x, y[1].y, acc[a][3]);
-        acc[a][0] = fma(x[a].y, y[2].x, acc[a][0]);
-        acc[a][1] = fma(x[a].y, y[2].y, acc[a][1]);
-        acc[a][2] = fma(x[a].y, y[3].x, acc[a][2]);
-        acc[a][3] = fma(x[a].y, y[3].y, acc[a][3]);
-      }
-    }
-  }
-}
-
-__device__ __forceinline__ void tile4x4_zero(double (&acc)[4][4]) {
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = 0.0;
-}
-
-// S[r+a][c..c+3] = sgn·acc[a][..] + (accumulate ? S[r+a][c..c+3] : 0)
-__device__ __forceinline__ void tile4x4_store(double* __restrict__ S, int r, int c, const double (&acc)[4][4],
-                                              double sgn, bool accumulate) {
-#pragma unroll
-  for (int a = 0; a < 4; ++a) {
-    d2* o0 = reinterpret_cast<d2*>(S + dsw(r + a, c));
-    d2* o1 = reinterpret_cast<d2*>(S + dsw(r + a, c + 2));
-    const d2 b0 = accumulate ? *o0 : d2{0.0, 0.0}, b1 = accumulate ? *o1 : d2{0.0, 0.0};
-    *o0 = d2{fma(sgn, acc[a][0], b0.x), fma(sgn, acc[a][1], b0.y)};
-    *o1 = d2{fma(sgn, acc[a][2], b1.x), fma(sgn, acc[a][3], b1.y)};
-  }
-}
-
-// The same 32×32 block products on the f64 matrix core (round 5): one wave, 2×2 tiles of
-// v_mfma_f64_16x16x4f64, K = 32 in 8 steps of 4.  Operands: a = X[row l&15][k l>>4],
+// 32×32 block products of the diagonal kernel on the f64 matrix core (round 5): one wave, 2×2
+// tiles of v_mfma_f64_16x16x4f64, K = 32 in 8 steps of 4.  Operands: a = X[row l&15][k l>>4],
 // b = Y(k l>>4, col l&15); acc[ti][tj][r] is C[16ti + (l>>4) + 4r][16tj + (l&15)].  A tenth of
-// tile4x4's LDS bytes per product (16 vs 128 KB per wave); the sums run in the matrix core's
-// order, so the factor differs from the FMA tiles' in the last bits.
-#ifndef GP2D_DIAG_MFMA
-#define GP2D_DIAG_MFMA 1   // 0: tile4x4 (dev builds, for the A/B)
-#endif
+// the LDS bytes per product of the FMA register tiles it replaced (16 vs 128 KB per wave; those
+// are at git 00ed20f).
 typedef d4 tileacc_t[2][2];
 template <bool NT>
 __device__ __forceinline__ void tile32_mfma(const double* __restrict__ S, int xr, int xk, int yk, int yc,
@@ -400,9 +304,8 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
   //   W_pp = L_pp⁻¹;  W10 = −W11 (L10 W00),  W32 = −W33 (L32 W22);
   //   T = L21·W11 (64-blocks: T20 = L20 W00 + L21 W10, T21 = L21 W11, T30, T31 alike), stored
   //   over L21;  W20 = −W22 T20, W21 = −W22 T21, W30 = −(W32 T20 + W33 T30), W31 likewise.
-  // Each 32×32 product is one wave's 4×4-per-lane register tile (tile4x4).
+  // Each 32×32 product is one wave's matrix-core tile (tile32_mfma).
   // row mapping inside the per-wave 32×32 tiles: 8 rows per wave, 4 consecutive columns per lane
-  const int tr4 = 4 * (lane >> 3), tc4 = 4 * (lane & 7);
   const bool storeL = !inv_in_place;
   const bool inv = dinv != nullptr;
   auto panel = [&](int p) {   // wave 0
@@ -441,22 +344,12 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
   };
   // A(bi, bj) −= L(bi, p) · L(bj, p)ᵀ  (32-block indices), one wave
   const int m16 = lane & 15, mk = lane >> 4;   // the MFMA operand / output map
-#if GP2D_DIAG_MFMA
   typedef tileacc_t acc_t;
-#else
-  typedef double acc_t[4][4];
-#endif
   auto update = [&](int p, int bi, int bj) {
     acc_t acc;
-#if GP2D_DIAG_MFMA
     tile32_zero(acc);
     tile32_mfma<true>(S, 32 * bi, 32 * p, 32 * p, 32 * bj, acc, m16, mk);
     tile32_store(S, 32 * bi, 32 * bj, acc, -1.0, true, m16, mk);
-#else
-    tile4x4_zero(acc);
-    tile4x4<true>(S, 32 * bi + tr4, 32 * p, 32 * p, 32 * bj + tc4, acc);
-    tile4x4_store(S, 32 * bi + tr4, 32 * bj + tc4, acc, -1.0, true);
-#endif
   };
   // column block cb of L (all 128 rows, zeros above the diagonal) to A, by threads [t0, t0+nt)
   auto store_colblock = [&](int cb, int t0, int nt) {
@@ -468,15 +361,7 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
       *reinterpret_cast<d2*>(Ab + (int64_t)r * lda + c) = d2{(c <= r) ? v.x : 0.0, (c + 1 <= r) ? v.y : 0.0};
     }
   };
-  // W(q,q) = L(q,q)⁻¹ by forward substitution (lane j ↔ column j), into x; one wave
-  auto diag_inverse = [&](int q, double (&x)[32]) {
-    const int b0 = 32 * q, j = lane & 31;
-    const double rl = 1.0 / S[dsw(b0 + j, b0 + j)];   // lane i: 1 / L_ii
-#pragma unroll
-    for (int i = 0; i < 32; ++i) x[i] = (i == j) ? 1.0 : 0.0;
-    inv_steps(std::make_integer_sequence<int, 32>{}, x, S, b0, rl);
-  };
-  // W(q,q) = L(q,q)⁻¹ in place in S, one wave (round 5, GP2D_DIAG_MFMA): the two 16×16
+  // W(q,q) = L(q,q)⁻¹ in place in S, one wave (round 5): the two 16×16
   // diagonal blocks by forward substitution at once (lanes 0–15 the upper, 16–31 the lower one:
   // 16 serial steps instead of 32), then W21 = −W22·(L21·W11) as two 16×16×16 products on the
   // matrix core (T stored over L21, then W21 over T).
@@ -514,29 +399,13 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
 #pragma unroll
     for (int r = 0; r < 4; ++r) S[dsw(b0 + 16 + mk + 4 * r, b0 + m16)] = -w[r];   // W21 over T
   };
-  auto put_diag = [&](int q, const double (&x)[32]) {   // x (lanes 0–31) → S's diagonal block q
-    const int b0 = 32 * q, j = lane & 31;
-    if (lane < 32) {
-#pragma unroll
-      for (int i = 0; i < 32; ++i) S[dsw(b0 + i, b0 + j)] = x[i];   // x[i] = 0 above the diagonal
-    }
-  };
   // acc = Σ_{p in [p0, p1]} X(bi, p) · Y(p, bj)  (NN, 32-block indices)
   auto prod = [&](acc_t& acc, int bi, int bj, int p0, int p1) {
-#if GP2D_DIAG_MFMA
     tile32_zero(acc);
     for (int p = p0; p <= p1; ++p) tile32_mfma<false>(S, 32 * bi, 32 * p, 32 * p, 32 * bj, acc, m16, mk);
-#else
-    tile4x4_zero(acc);
-    for (int p = p0; p <= p1; ++p) tile4x4<false>(S, 32 * bi + tr4, 32 * p, 32 * p, 32 * bj + tc4, acc);
-#endif
   };
   auto put = [&](int bi, int bj, const acc_t& acc, double sgn) {
-#if GP2D_DIAG_MFMA
     tile32_store(S, 32 * bi, 32 * bj, acc, sgn, false, m16, mk);
-#else
-    tile4x4_store(S, 32 * bi + tr4, 32 * bj + tc4, acc, sgn, false);
-#endif
   };
 
   // P0
@@ -566,19 +435,11 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
   __syncthreads();
   GP2D_STAMP(7);
   // P3 | W00, W11 | L column block 2, then W22
-#if !GP2D_DIAG_MFMA
-  double xd[32];
-#endif
   if (wid == 0) {
     panel(3);
   } else if (inv) {
     if (wid == 3 && storeL) store_colblock(2, 192, 64);
-#if GP2D_DIAG_MFMA
     inv_diag_mfma(wid - 1);
-#else
-    diag_inverse(wid - 1, xd);
-    put_diag(wid - 1, xd);
-#endif
   } else if (storeL) {
     store_colblock(2, 64, 192);
   }
@@ -591,11 +452,7 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
   // B: W33 | T10 = L10 W00 → W10 = −W11 T10 | T32 = L32 W22 | L column block 3's zeros
   acc_t acc;
   if (wid == 0) {
-#if GP2D_DIAG_MFMA
     inv_diag_mfma(3);   // S(3,3) is nobody else's operand in B
-#else
-    diag_inverse(3, xd);
-#endif
   } else if (wid == 1) {
     prod(acc, 1, 0, 0, 0);
     put(1, 0, acc, 1.0);
@@ -615,9 +472,6 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
   // C: W33 → S, W32 = −W33 T32, then T31 | T20 | T21 | T30   (T kept in registers: one
   // accumulator set per wave — S(3,2) is nobody else's operand here)
   if (wid == 0) {
-#if !GP2D_DIAG_MFMA
-    put_diag(3, xd);
-#endif
     prod(acc, 3, 2, 3, 3);
     put(3, 2, acc, -1.0);
     prod(acc, 3, 1, 1, 1);

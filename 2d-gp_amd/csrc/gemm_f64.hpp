@@ -210,9 +210,9 @@ __global__ __launch_bounds__(256, 2) void gemm_f64_kernel(GemmParams p) {
     const bool diag_tile = (p.c_lower && bi == bj) || (p.cyc_lower && bi + p.mask_off == jt);
     const bool has_beta = p.beta != 0.0;
     // per 16-row group mi: 16 C loads, then the updates and stores (element-wise load → use →
-    // store chains leave one HBM round trip per element).  GP2D_EPI_PIPE (the default) issues
-    // group mi+1's loads before group mi's updates, so a tile's C read costs one exposed round
-    // trip instead of four; the per-element arithmetic is the same.
+    // store chains leave one HBM round trip per element).  With β ≠ 0 group mi+1's loads are
+    // issued before group mi's updates, so a tile's C read costs one exposed round trip instead
+    // of four; the per-element arithmetic is the same (round 3, profiles/r03_syrk_epilogue_ab.txt).
     auto cload = [&](int mi, double (&old)[4][4]) {
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni)
@@ -235,10 +235,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f64_kernel(GemmParams p) {
           if (!(diag_tile && col - j0 > row - i0)) C[(int64_t)row * ldc + col] = v;
         }
     };
-#ifndef GP2D_EPI_PIPE
-#define GP2D_EPI_PIPE 1
-#endif
-    if (GP2D_EPI_PIPE && has_beta) {
+    if (has_beta) {
       double o0[4][4], o1[4][4];
       cload(0, o0);
       cload(1, o1);
@@ -249,12 +246,9 @@ __global__ __launch_bounds__(256, 2) void gemm_f64_kernel(GemmParams p) {
       cstore(2, o0);
       cstore(3, o1);
     } else {
+      const double none[4][4] = {};
 #pragma unroll
-      for (int mi = 0; mi < 4; ++mi) {
-        double old[4][4];
-        if (has_beta) cload(mi, old);
-        cstore(mi, old);
-      }
+      for (int mi = 0; mi < 4; ++mi) cstore(mi, none);
     }
   } else {
     // column sums of squares of this 128-row slab of V, combined in a fixed order:

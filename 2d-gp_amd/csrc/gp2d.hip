@@ -4,6 +4,9 @@
 // factor.hpp / predict.hpp.  All work is enqueued on the caller's HIP stream;
 // nothing here synchronises except gp2d_timing_read().
 #include "common.hpp"
+#ifndef GP2D_RELEASE
+#error "libgp2d.so is built with -DGP2D_RELEASE=1 (python __graft_entry__.py build)"
+#endif
 #include "assemble.hpp"
 #include "gemm_f64.hpp"
 #include "factor.hpp"
@@ -98,6 +101,9 @@ static int assemble_impl(const double* xa, int64_t na, int64_t na_pad, const dou
   if (na_pad == 0 || nb_pad == 0) return 0;
   const int bd = is_vector_family(k) ? 2 : 1;
   GP2D_REQUIRE(ld >= bd * nb_pad, "ld too small");
+  GP2D_REQUIRE(symmetric >= 0 && symmetric <= ASM_LOWER, "symmetric must be 0, 1 or 2");
+  GP2D_REQUIRE(symmetric != ASM_LOWER || (bd == 2 && xa == xb && na == nb && na_pad == nb_pad),
+               "symmetric = 2 (lower block triangle) needs a vector kernel and xa == xb");
   dim3 grid(nb_pad / 64, (na_pad + ASM_ROWS - 1) / ASM_ROWS);
   if (bd == 2) {
     assemble_vec_kernel<<<grid, 256, 0, s>>>(xa, na, na_pad, xb, nb, nb_pad, make_vec_params(k), diag_add,
@@ -110,13 +116,6 @@ static int assemble_impl(const double* xa, int64_t na, int64_t na_pad, const dou
 }
 
 
-// Dev knob for attribution A/Bs (tools/runs/r05_attrib.sh), never set in the product build:
-// bit 0 skips the POTRF trailing SYRKs, bit 1 the TRTRI products — the factor is then wrong, but
-// the fit's chain and its launch pattern stay, so a job stream shows what its predict pays for the
-// fit's FP64 GEMM arithmetic versus for its chain.
-#ifndef GP2D_DEV_SKIP
-#define GP2D_DEV_SKIP 0
-#endif
 
 // ------------------------------------------------------------- Ozaki constants
 // pairwise coprime, largest first (the count a product needs takes the first nmod); the last four
@@ -208,6 +207,12 @@ using namespace gp2d;
 extern "C" {
 
 int gp2d_abi_version(void) { return GP2D_ABI_VERSION; }
+const char* gp2d_build_info(void) {
+  static const std::string info = "release gfx950 abi=" + std::to_string(GP2D_ABI_VERSION) +
+                                  " oz_pw=" + std::to_string(OZ_PW) + " oz_pb=" + std::to_string(OZ_PB) +
+                                  " ks_ppl=" + std::to_string(OZ_KS_PPL) + " crt_rpl=" + std::to_string(OZ_CRT_RPL);
+  return info.c_str();
+}
 int64_t gp2d_padded_points(int64_t n) { return round_up(n < 1 ? 1 : n, PT_TILE); }
 int gp2d_block_dim(const gp2d_kernel_t* k) { return (k && k->family == GP2D_FAMILY_ARD_RBF) ? 1 : 2; }
 
@@ -624,7 +629,7 @@ static int potrf_impl(double* A, int64_t n, int64_t lda, double* dinv, int* info
             q.C = A + f0 * lda + f0;
             q.M = (int)(n - f0); q.N = hw * NB;
             q.cyc_lower = 1; q.mask_off = 0;
-            if (!(GP2D_DEV_SKIP & 1)) GP2D_CHECK((launch_gemm<true, EPI_STORE>(q, 1, sb, nprob)));
+            GP2D_CHECK((launch_gemm<true, EPI_STORE>(q, 1, sb, nprob)));
             GP2D_EV(hipEventRecord(e_head, sb));
             q.cyc_lower = 0;
           }
@@ -634,7 +639,7 @@ static int potrf_impl(double* A, int64_t n, int64_t lda, double* dinv, int* info
             q.B = q.A;
             q.C = A + f1 * lda + f1;
             q.M = (int)(n - f1); q.N = q.M; q.c_lower = 1;
-            if (!(GP2D_DEV_SKIP & 1)) GP2D_CHECK((launch_gemm<true, EPI_STORE>(q, 1, sb, nprob)));
+            GP2D_CHECK((launch_gemm<true, EPI_STORE>(q, 1, sb, nprob)));
           }
           if (hw == 0) GP2D_EV(hipEventRecord(e_head, sb));
         } else {
@@ -754,7 +759,6 @@ int gp2d_trtri(double* A, int64_t n, int64_t lda, const double* dinv, void* work
   }
   put_diag_blocks_kernel<<<dim3(NB * NB / 256, nb), 256, 0, s>>>(A, lda, dinv);
   GP2D_CHECK(check_launch("put_diag_blocks_kernel"));
-  if (GP2D_DEV_SKIP & 2) return 0;
   return trtri_levels(A, lda, nb, T, dwork + (size_t)nb * NB * NB, s);
 }
 
@@ -1370,10 +1374,9 @@ static int predict_ozaki_impl(const int8_t* wres, const double* rowscale, int nm
         const int nz = std::min(zper, nm - l0);
         IgemmZ zb{(int64_t)n * n, (int64_t)bplane, (int64_t)n * ncols, {}};
         for (int u = 0; u < nz; ++u) zb.m[u] = oc.m[l0 + u];
-#ifndef GP2D_IG_TBN
-#define GP2D_IG_TBN 256   // output columns per workgroup (128: two workgroups per CU, a measurement build)
-#endif
-        constexpr int tbn = GP2D_IG_TBN, nst = (GP2D_IG_TBN == 256) ? I_NSTAGE : 3;
+        // 256 output columns per workgroup, one workgroup per CU (the 128-wide shape with two
+        // workgroups per CU measured −5 %: tools/microbench/igemm_bench.hip)
+        constexpr int tbn = 256, nst = I_NSTAGE;
         const dim3 ggrid((unsigned)(ncols / tbn), (unsigned)(n / IBM), (unsigned)nz);
         const int8_t* Al = wres + (size_t)l0 * n * n;
         const int8_t* Bl = B + (size_t)l0 * bplane;

@@ -442,9 +442,6 @@ __device__ __forceinline__ uint32_t ozaki_mod_u32(uint32_t v, const OzModConsts&
 // chunk ^ g((row>>2)&3) with g = [0,2,3,1], which spreads every group over 16 distinct
 // 4-bank slots.  The DMA writes LDS lane-linearly; the swizzle is applied on the global
 // source address (an involution, so the same formula maps both ways).
-#ifndef GP2D_IG_NTSTORE
-#define GP2D_IG_NTSTORE 1   // residue-plane stores non-temporal (0: plain stores, for the A/B)
-#endif
 constexpr int IBM = 256, IBN = 256, IBK = 64;
 constexpr int I_OP = IBM * IBK;        // bytes per operand per stage (16 KB) = one layout tile
 constexpr int I_STAGE = 2 * I_OP;      // A then B
@@ -734,13 +731,9 @@ __global__ __launch_bounds__(TBN * 2, (TBN == 256) ? 1 : 2) void igemm_nt_mod_ke
   for (int p = 0; p < (IBM * TBN / 16) / (TBN * 2); ++p) {
     const int id = tid + TBN * 2 * p;
     const int cloc = id >> 4, ch = id & 15;
-#if GP2D_IG_NTSTORE   // non-temporal: the planes are read once, by the CRT, past L2 (r05 A/B)
+    // non-temporal: the planes are read once, by the CRT, past L2 (+0.3–0.5 %, profiles/r05_ntstore_ab.txt)
     const i4v v = *reinterpret_cast<const i4v*>(T + cloc * TP + 16 * ch);
     __builtin_nontemporal_store(v, reinterpret_cast<i4v*>(C + (int64_t)(j0 + cloc) * ldc + i0 + 16 * ch));
-#else
-    const uint4 v = *reinterpret_cast<const uint4*>(T + cloc * TP + 16 * ch);
-    *reinterpret_cast<uint4*>(C + (int64_t)(j0 + cloc) * ldc + i0 + 16 * ch) = v;
-#endif
   }
 }
 

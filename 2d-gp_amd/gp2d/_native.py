@@ -22,7 +22,7 @@ COMM_SUM, COMM_MAX, COMM_MIN = 0, 1, 2
 
 # every symbol declared in include/gp2d.h
 EXPORTS = (
-    "gp2d_abi_version", "gp2d_padded_points", "gp2d_block_dim", "gp2d_kernel_diag",
+    "gp2d_abi_version", "gp2d_build_info", "gp2d_padded_points", "gp2d_block_dim", "gp2d_kernel_diag",
     "gp2d_assemble", "gp2d_factor_sets", "gp2d_factor_set_of", "gp2d_factor_join", "gp2d_potrf_workspace", "gp2d_potrf", "gp2d_trtri_workspace", "gp2d_trtri",
     "gp2d_potrf_inv_workspace", "gp2d_potrf_inv", "gp2d_potrf_batched", "gp2d_trtri_batched_workspace",
     "gp2d_trtri_batched",
@@ -79,6 +79,7 @@ _KP = ctypes.POINTER(KernelDesc)
 
 _SIGS = {
     "gp2d_abi_version": (_I, []),
+    "gp2d_build_info": (ctypes.c_char_p, []),
     "gp2d_padded_points": (_I64, [_I64]),
     "gp2d_block_dim": (_I, [_KP]),
     "gp2d_kernel_diag": (_D, [_KP]),
@@ -188,6 +189,8 @@ def lib():
             fn.argtypes = args
         if L.gp2d_abi_version() != ABI_VERSION:
             raise NativeLibraryError("libgp2d.so ABI version mismatch")
+        if not L.gp2d_build_info().startswith(b"release "):   # a measurement build never ships
+            raise NativeLibraryError(f"{LIB_PATH} is not a release build: {L.gp2d_build_info()!r}")
         _lib = L
         return _lib
 

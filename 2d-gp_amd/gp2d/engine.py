@@ -274,6 +274,7 @@ def _pad_obs(y, n_train: int, n_pad: int, bd: int, device, perm: torch.Tensor | 
 
 
 VARIANCE_ENGINES = ("f64", "ozaki")
+ASSEMBLE_LOWER = 2   # gp2d_assemble's symmetric mode: K_y's lower block triangle only
 
 # fit: the two-call gp2d_potrf + gp2d_trtri sequence, or gp2d_potrf_inv (the left half of the
 # inverse and the top-level T = L21·W11 issued under the second half of the factorisation).
@@ -488,8 +489,9 @@ def fit(kernel: KernelSpec, x, y, noise: float, jitter: float = 0.0, device=None
     s = _stream_handle(dev)
     desc = kernel.desc()
     A = torch.empty((n, n), dtype=torch.float64, device=dev)
-    N.check(L.gp2d_assemble(_ptr(X), ntr, npad, _ptr(X), ntr, npad, ctypes.byref(desc), float(noise + jitter), 1,
-                            _ptr(A), n, s), "gp2d_assemble")
+    # the vector families: K_y's lower block triangle only (symmetric = 2), all gp2d_potrf reads
+    N.check(L.gp2d_assemble(_ptr(X), ntr, npad, _ptr(X), ntr, npad, ctypes.byref(desc), float(noise + jitter),
+                            ASSEMBLE_LOWER if kernel.is_vector else 1, _ptr(A), n, s), "gp2d_assemble")
     dinv = torch.empty((n // NB, NB, NB), dtype=torch.float64, device=dev)
     status, info = status_block(dev)   # gp2d_potrf resets info
     prev_join = L.gp2d_factor_join(1 if (check if join is None else join) else 0)
@@ -594,7 +596,8 @@ def fit_batch(problems, variance: str = "f64", jitter: float = 0.0, device=None,
     A = torch.empty((B, n, n), dtype=torch.float64, device=dev)
     for b, (kernel, X, _, noise, ntr, npad, _, _) in enumerate(prep):
         N.check(L.gp2d_assemble(_ptr(X), ntr, npad, _ptr(X), ntr, npad, ctypes.byref(kernel.desc()),
-                                float(noise + jitter), 1, _ptr(A[b]), n, s), "gp2d_assemble")
+                                float(noise + jitter), ASSEMBLE_LOWER if kernel.is_vector else 1, _ptr(A[b]), n, s),
+                "gp2d_assemble")
     dinv = torch.empty((B, n // NB, NB, NB), dtype=torch.float64, device=dev)
     info = torch.empty(B, dtype=torch.int32, device=dev)   # gp2d_potrf_batched resets them
     prev_join = L.gp2d_factor_join(1 if (check if join is None else join) else 0)

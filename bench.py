@@ -59,11 +59,11 @@ def parse():
     ap.add_argument("--grid-global", type=int, default=0,
                     help="strong scaling: ONE fixed G x G grid sharded over the ranks (0 = weak scaling, "
                          "--grid x --grid points per rank)")
-    ap.add_argument("--config", default=None, choices=["B", "C", "D", "E"],
+    ap.add_argument("--config", default=None, choices=["B", "C", "D", "E", "E-noise"],
                     help="BASELINE.json config preset: B = df N=1024 128^2, C = mixed N=4096 256^2, "
                          "D = mixed N=16384, one 512^2 grid sharded over the ranks (strong scaling), "
-                         "E = 64-setting (l_df, noise) sweep of LML + gradient at N=4096, settings dealt over "
-                         "the ranks (hyper.sweep)")
+                         "E = SURVEY's 64-setting (l_df, l_cf) sweep of LML + gradient at N=4096 (mixed), "
+                         "settings dealt over the ranks (hyper.sweep); E-noise = the (l_df, noise) div-free sweep")
     ap.add_argument("--chunk", type=int, default=8192)
     ap.add_argument("--scaling", default="auto", choices=["auto", "weak", "strong"],
                     help="N>1: strong = the --grid x --grid job grid sharded over the ranks (auto's choice: "
@@ -124,7 +124,7 @@ def parse():
         a.kind, a.ntrain, a.grid_global = "mixed", 16384, 512
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     if a.steps is None:   # config D: every rank owns at least two of the timed jobs' fits
-        a.steps = {"D": max(4, 2 * ws), "E": 2}.get(a.config, 100)
+        a.steps = {"D": max(4, 2 * ws), "E": 2, "E-noise": 2}.get(a.config, 100)
     if a.grid_global == 0 and is_multi(ws) and a.scaling in ("auto", "strong"):
         a.grid_global = a.grid   # N>1 default: one job grid sharded over the ranks
     if a.fit_mode is None:
@@ -243,9 +243,14 @@ def _pmc_round(path: str, pmc: dict) -> str:
     return "round unknown"
 
 
-def config_e_settings():
-    """BASELINE config E's 64 settings: l_df on 8 log-spaced values in [2, 12] km x noise on 8
-    log-spaced values in [1e-3, 5e-2] (the same grid as the committed config-E fixture)."""
+def config_e_settings(variant: str = "E"):
+    """BASELINE config E's 64 settings.  'E' (SURVEY.md §8(d)): the mixed kernel (α = ½, noise
+    0.0025) at 8 ℓ_df × 8 ℓ_cf log-spaced over [1, 10] km (ℓ_df-major); 'E-noise' (rounds 1-5's
+    variant): the div-free kernel at 8 ℓ_df in [2, 12] km × 8 noise values in [1e-3, 5e-2].  The
+    same grids as the committed fixtures (config_e_survey_share.npz, config_e_share.npz)."""
+    if variant == "E":
+        g = np.geomspace(1.0, 10.0, 8)
+        return [dict(l_df=float(a), l_cf=float(b)) for a in g for b in g]
     return [dict(l_df=float(l), noise=float(nz)) for l in np.geomspace(2.0, 12.0, 8)
             for nz in np.geomspace(1e-3, 5e-2, 8)]
 
@@ -260,8 +265,9 @@ def run_sweep(args, ws, rank, dev):
     x1, x2, u, v = D.synthetic_tracks(args.ntrain, seed=2016)
     xt = torch.tensor(np.stack([x1, x2], 1), device=dev)
     yt = torch.tensor(np.concatenate([u, v]), device=dev)
-    settings = config_e_settings()
-    ks = E.KernelSpec(kind="df", l_df=5.0)
+    settings = config_e_settings(args.config)
+    survey = args.config == "E"
+    ks = E.KernelSpec(kind="mixed", l_df=5.0, l_cf=5.0, ratio=0.5) if survey else E.KernelSpec(kind="df", l_df=5.0)
 
     # None: the library's default (hyper.auto_concurrent)
     conc = args.sweep_concurrent
@@ -287,15 +293,17 @@ def run_sweep(args, ws, rank, dev):
         n = 2 * E.padded_points(args.ntrain)
         # per setting: POTRF n³/3 + TRTRI n³/3 + K_y⁻¹ = WᵀW n³/3 (FP64 MFMA), the rest O(n²)
         per_gpu = len(settings) / ws * n ** 3 * args.steps / elapsed / 1e12
+        grid = ("8 l_df x 8 l_cf log-spaced over [1, 10] km, mixed alpha=0.5, noise 0.0025 (SURVEY.md §8d)"
+                if survey else "8 l_df in [2, 12] km x 8 noise in [1e-3, 5e-2], div-free")
         out = {
             "metric": f"hyperparameter settings/sec (fit + LML + gradient), 64-setting sweep, N_train={args.ntrain}, "
-                      "div-free 2D kernel",
+                      + ("mixed div-free + curl-free 2D kernel" if survey else "div-free 2D kernel"),
             "value": len(settings) * args.steps / elapsed, "unit": "settings/s", "n_gpus": ws, "world_size": ws,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps,
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (seeded drifter field, SURVEY.md §8d)",
-            "config": {"workload": f"BASELINE config E: 64 (l_df, noise) settings x N_train={args.ntrain}, "
-                                   f"div-free, LML + exact gradient per setting, settings dealt over {ws} GPU(s)",
+            "config": {"workload": f"BASELINE config {args.config}: 64 settings ({grid}) x N_train={args.ntrain}, "
+                                   f"LML + exact gradient per setting, settings dealt over {ws} GPU(s)",
                        "n_train": args.ntrain, "settings": len(settings), "parallelism": f"settings round robin x{ws}",
                        "sweep_batch": bsz if bsz is not None else
                        H.auto_batch(ks, xt, len(range(rank, len(settings), ws)), conc),
@@ -440,7 +448,7 @@ def main():
     if rc is not None:
         sys.exit(rc)
     ws, rank, dev = setup_dist(args)
-    if args.config == "E":
+    if args.config in ("E", "E-noise"):
         return run_sweep(args, ws, rank, dev)
     from gp2d import data as D
     from gp2d import distributed as GD

@@ -68,6 +68,7 @@ typedef struct gp2d_kernel {
 
 /* ---- sizes ------------------------------------------------------------------- */
 int     gp2d_abi_version(void);
+const char* gp2d_build_info(void);   /* "release gfx950 abi=… oz_pw=… …": the build's tuning constants */
 int64_t gp2d_padded_points(int64_t n);                 /* round up to the 64-point tile */
 int     gp2d_block_dim(const gp2d_kernel_t* k);        /* 2 for vector2d, 1 for ARD      */
 double  gp2d_kernel_diag(const gp2d_kernel_t* k);      /* k(x,x) per component: myKernel.Kdiag, myKernel.py:55-57 */
@@ -78,7 +79,12 @@ double  gp2d_kernel_diag(const gp2d_kernel_t* k);      /* k(x,x) per component: 
  * 159-176, 255-271).  out is (bd·nb_pad) × (bd·... ) with leading dim ld:
  * rows index xa's components, columns xb's.  diag_add (noise + jitter) is added
  * on the diagonal when xa == xb (GP_laser.py:114-115); padded rows/columns are
- * identity (when diag_add is used) or zero.                                     */
+ * identity (when diag_add is used) or zero.
+ * symmetric: 0 = cross-covariance K(xa, xb) (compute_Ks); 1 = K_y = K(x, x) + diag_add·I
+ * in full (compute_K); 2 = K_y's lower block triangle only (vector families: entries (R, C)
+ * with C < 128·(R/128 + 1), the 128×128 diagonal blocks whole, the rest left unwritten) —
+ * all gp2d_potrf reads, half the stores (the fit's assembly; GP_scripts.py:80-88 also builds
+ * one triangle and mirrors it).                                                   */
 int gp2d_assemble(const double* xa, int64_t na, int64_t na_pad,
                   const double* xb, int64_t nb, int64_t nb_pad,
                   const gp2d_kernel_t* k, double diag_add, int symmetric,

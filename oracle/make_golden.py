@@ -334,6 +334,85 @@ def gen_configs(gs, out):
     np.savez_compressed(os.path.join(out, "configs_N4096.npz"), **d)
 
 
+def gen_configs_full(gs, out):
+    """The headline (div-free, α = 1) and config C (mixed, α = ½) at EVERY point of the 256²
+    grid: the bench's seeded N_train = 4096 tracks (gp2d.data.synthetic_tracks(4096, seed=2016),
+    bbox_grid(…, 256, pad=5)), ℓ_df = ℓ_cf = 5 km, noise 0.0025, through the reference's own
+    GP_laser.py:113-134 recipe — vectorised myKernel (GP_scripts.py:6-46) and np.linalg.inv —
+    with K* taken in 4096-point chunks (one 131,072 × 8192 K* would need 8.6 GB).  Mean and
+    variance of all 2 × 65,536 outputs per case."""
+    x, y, u, v = synthetic_tracks(4096)
+    xa = np.stack([x, y], 1)
+    gx = np.linspace(x.min() - 5, x.max() + 5, 256)      # = gp2d.data.bbox_grid(x, y, 256, pad=5)
+    gy = np.linspace(y.min() - 5, y.max() + 5, 256)
+    GX, GY = np.meshgrid(gx, gy)
+    xg = np.stack([GX.reshape(-1), GY.reshape(-1)], 1)
+    M = xg.shape[0]
+    obs = np.concatenate([u, v])[:, None]
+    d = dict(x_sum=np.array([x.sum(), y.sum()]), u_sum=np.array([u.sum(), v.sum()]), xg_sum=xg.sum(0))
+    c = 4096
+    for name, rate in (("df", 1.0), ("mixed", 0.5)):
+        t0 = time.time()
+        K = gs["myKernel"](xa, xa, 5.0, 5.0, rate)
+        K = K + np.identity(K.shape[0]) * 0.0025         # GP_laser.py:114-115
+        Ki = np.linalg.inv(K)                            # GP_laser.py:118
+        d0 = np.diag(gs["myKernel"](xg[:2], xg[:2], 5.0, 5.0, rate))   # the diagonal is constant (r = 0)
+        assert np.all(d0 == d0[0])
+        mean, var = np.empty(2 * M), np.empty(2 * M)
+        for r0 in range(0, M, c):
+            Ks = gs["myKernel"](xg[r0:r0 + c], xa, 5.0, 5.0, rate)   # rows [u(chunk); v(chunk)]
+            f = np.ravel(gs["getMean"](Ks, Ki, obs))                 # GP_laser.py:134
+            q = d0[0] - np.einsum("ij,ij->i", Ks, Ks @ Ki)            # diag of GP_laser.py:129
+            mean[r0:r0 + c], mean[M + r0:M + r0 + c] = f[:c], f[c:]
+            var[r0:r0 + c], var[M + r0:M + r0 + c] = q[:c], q[c:]
+        print(f"  full grid {name}: N=4096, {M} points, {time.time() - t0:.1f}s, min var {var.min():.2e}")
+        d[f"{name}_rate"] = rate
+        d[f"{name}_mean"] = mean
+        d[f"{name}_var"] = var
+    np.savez_compressed(os.path.join(out, "configs_N4096_full.npz"), **d)
+
+
+GUARD_KIND_SETTINGS = (("mixed", 3.0, 8.0, 0.5, 1e-4), ("cf", 12.0, 12.0, 0.0, 1e-3))   # VERDICT r05 item 4
+
+
+def gen_guard_kinds(gs, out):
+    """The accuracy guard's yardstick on the other two vector kernels: the
+    bench's seeded N_train = 4096 tracks and 256² bbox grid at the 512-point config_subsample,
+    mixed (ℓ_df = 3, ℓ_cf = 8, ratio ½, noise 1e-4) and curl-free (ℓ = 12, noise 1e-3), through
+    the reference's GP_laser.py:113-134 recipe (vectorised myKernel, np.linalg.inv) plus the
+    refined posterior (_refined_posterior)."""
+    x, y, u, v = synthetic_tracks(4096)
+    xa = np.stack([x, y], 1)
+    gx = np.linspace(x.min() - 5, x.max() + 5, 256)
+    gy = np.linspace(y.min() - 5, y.max() + 5, 256)
+    GX, GY = np.meshgrid(gx, gy)
+    xg_all = np.stack([GX.reshape(-1), GY.reshape(-1)], 1)
+    idx = config_subsample(xa, xg_all)
+    xg = xg_all[idx]
+    obs = np.concatenate([u, v])
+    d = dict(x_sum=np.array([x.sum(), y.sum()]), u_sum=np.array([u.sum(), v.sum()]), idx=idx, xg=xg,
+             settings=np.array([[ldf, lcf, r, nz] for _, ldf, lcf, r, nz in GUARD_KIND_SETTINGS]),
+             kinds=np.array([k for k, *_ in GUARD_KIND_SETTINGS]))
+    for k, (kind, ldf, lcf, rate, nz) in enumerate(GUARD_KIND_SETTINGS):
+        t0 = time.time()
+        K = gs["myKernel"](xa, xa, ldf, lcf, rate)
+        K = K + np.identity(K.shape[0]) * nz              # GP_laser.py:114-115
+        Ki = np.linalg.inv(K)                            # GP_laser.py:118
+        Ks = gs["myKernel"](xg, xa, ldf, lcf, rate)      # GP_laser.py:122 (vectorised form)
+        f = np.ravel(gs["getMean"](Ks, Ki, obs[:, None]))   # GP_laser.py:134
+        kss = np.diag(gs["myKernel"](xg, xg, ldf, lcf, rate))
+        var = kss - np.einsum("ij,ij->i", Ks, Ks @ Ki)   # diag of GP_laser.py:129
+        del Ki
+        mr, vr = _refined_posterior(K, Ks, kss, obs)
+        print(f"  guard {kind} l=({ldf},{lcf}) ratio={rate} noise={nz}: {time.time() - t0:.1f}s; inv recipe vs "
+              f"refined: var elementwise {np.max(np.abs(var - vr) / vr):.1e}, normwise "
+              f"{np.max(np.abs(var - vr)) / np.max(vr):.1e}; min var/kss {np.min(vr / kss):.1e}")
+        d[f"s{k}_mean"], d[f"s{k}_var"] = f, var
+        d[f"s{k}_mean_refined"], d[f"s{k}_var_refined"] = mr, vr
+        d[f"s{k}_kss"] = kss
+    np.savez_compressed(os.path.join(out, "guard_kinds_N4096.npz"), **d)
+
+
 GUARD_SETTINGS = ((12.0, 1e-3), (2.0, 5e-2), (5.0, 1e-4))   # (ℓ, noise): VERDICT r04 "next" item 1
 
 
@@ -466,6 +545,117 @@ def gen_config_d(gs, out):
           f"min var/kss {np.min(var / kss):.1e}")
     np.savez_compressed(os.path.join(out, "config_d_rank0.npz"), idx=idx, xg=xg, rate=rate, l=5.0, noise=0.0025,
                         mean=mean, var=var, kss=kss, K_rowsum=rowsum, x_sum=np.array([x.sum(), y.sum()]))
+
+
+def gen_config_d_shards(gs, out):
+    """Config D at EVERY rank's shard: as gen_config_d — mixed (α = ½,
+    ℓ = 5, noise 0.0025), N_train = 16384 (a 32768² K from the reference's myKernel in row
+    chunks), the 512² bbox grid cut into 8 shards (gp2d.data.shard_range) — with 64 points
+    from EACH shard (32 nearest to a training point + 32 seeded, config_subsample), 512 in all.
+    Blocked Cholesky (LAPACK on 4096-wide blocks) and forward substitution as gen_config_d."""
+    import scipy.linalg as sla
+    N, rate, P = 16384, 0.5, 8
+    x, y, u, v = synthetic_tracks(N)
+    xa = np.stack([x, y], 1)
+    gx = np.linspace(x.min() - 5, x.max() + 5, 512)
+    gy = np.linspace(y.min() - 5, y.max() + 5, 512)
+    GX, GY = np.meshgrid(gx, gy)
+    xg_all = np.stack([GX.reshape(-1), GY.reshape(-1)], 1)
+    Mall = xg_all.shape[0]
+    sel = []
+    for r in range(P):                                    # shard_range(262144, 8, r) (align 64)
+        lo, hi = r * Mall // P, (r + 1) * Mall // P
+        sel.append(lo + config_subsample(xa, xg_all[lo:hi], 32, 32, seed=5 + r))
+    gidx = np.concatenate(sel)
+    xg = xg_all[gidx]
+    t0 = time.time()
+    K = np.empty((2 * N, 2 * N))
+    c = 1024
+    for r0 in range(0, N, c):
+        blk = gs["myKernel"](xa[r0:r0 + c], xa, 5.0, 5.0, rate)   # rows [u(r0:r0+c); v(r0:r0+c)]
+        K[r0:r0 + c] = blk[:c]
+        K[N + r0:N + r0 + c] = blk[c:]
+        del blk
+    K[np.diag_indices(2 * N)] += 0.0025
+    Ks = gs["myKernel"](xg, xa, 5.0, 5.0, rate)
+    kss = np.diag(gs["myKernel"](xg, xg, 5.0, 5.0, rate))
+    obs = np.concatenate([u, v])
+    bs = 4096
+    L = K
+    for k0 in range(0, 2 * N, bs):
+        k1 = k0 + bs
+        L[k0:k1, k0:k1] = np.linalg.cholesky(L[k0:k1, k0:k1])
+        if k1 < 2 * N:
+            L[k1:, k0:k1] = sla.solve_triangular(L[k0:k1, k0:k1], L[k1:, k0:k1].T, lower=True,
+                                                 check_finite=False).T
+            for j0 in range(k1, 2 * N, bs):
+                L[j0:, j0:j0 + bs] -= L[j0:, k0:k1] @ L[j0:j0 + bs, k0:k1].T
+    B = np.concatenate([Ks.T, obs[:, None]], 1)
+    Z = np.empty_like(B)
+    for i0 in range(0, 2 * N, bs):
+        r = B[i0:i0 + bs] - L[i0:i0 + bs, :i0] @ Z[:i0]
+        Z[i0:i0 + bs] = sla.solve_triangular(L[i0:i0 + bs, i0:i0 + bs], r, lower=True, check_finite=False)
+    mean = Z[:, :-1].T @ Z[:, -1]
+    var = kss - np.einsum("ij,ij->j", Z[:, :-1], Z[:, :-1])
+    print(f"  config D all shards: N={N}, {xg.shape[0]} points, {time.time() - t0:.1f}s, "
+          f"min var/kss {np.min(var / kss):.1e}")
+    np.savez_compressed(os.path.join(out, "config_d_shards.npz"), gidx=gidx, xg=xg, rate=rate, l=5.0, noise=0.0025,
+                        mean=mean, var=var, kss=kss, x_sum=np.array([x.sum(), y.sum()]))
+
+
+def config_e_survey_settings():
+    """SURVEY.md §8(d)'s config E: 8 ℓ_df × 8 ℓ_cf on a log grid over [1, 10] km, mixed kernel
+    with α = ½, noise 0.0025 (ℓ_df-major order)."""
+    g = np.geomspace(1.0, 10.0, 8)
+    return [dict(l_df=float(a), l_cf=float(b)) for a in g for b in g]
+
+
+def gen_config_e_survey(gs, out):
+    """SURVEY §8(d) config E, rank 0's share of the 64 settings over 8 GPUs
+    (settings 0, 8, …, 56; setting i = (ℓ_df[i // 8], ℓ_cf[i % 8]), so rank 0 holds ℓ_cf = 1 km
+    at every ℓ_df — the grid's short end) at N_train = 4096 (seeded tracks),
+    mixed α = ½, noise 0.0025: the LML of each, with K from the reference's myKernel
+    (GP_scripts.py:6-42) and a Cholesky factor; for two of them the gradient in (ℓ_df, ℓ_cf,
+    ratio) by a 4-point central difference of that LML and ∂/∂noise = ½(αᵀα − tr K_y⁻¹) exactly
+    (the reference's analytic gradient, myKernel.py:59-106, is not a derivative)."""
+    import scipy.linalg as sla
+    x, y, u, v = synthetic_tracks(4096)
+    xa = np.stack([x, y], 1)
+    obs = np.concatenate([u, v])
+    S = config_e_survey_settings()
+    share = list(range(0, 64, 8))
+
+    def lml(p, want=False):
+        K = gs["myKernel"](xa, xa, p[0], p[1], p[2])
+        K[np.diag_indices_from(K)] += p[3]
+        L = np.linalg.cholesky(K)
+        a = sla.cho_solve((L, True), obs)
+        val = -0.5 * obs @ a - np.sum(np.log(np.diag(L))) - 0.5 * obs.size * np.log(2 * np.pi)
+        return (val, L, a) if want else val
+
+    t0 = time.time()
+    vals = np.array([lml([S[i]["l_df"], S[i]["l_cf"], 0.5, 0.0025]) for i in share])
+    grads = []
+    gidx = [share[2], share[5]]
+    for i in gidx:
+        p = [S[i]["l_df"], S[i]["l_cf"], 0.5, 0.0025]
+        g = []
+        for j in range(3):
+            h = 1e-4 * (p[j] if j < 2 else 1.0)
+            f = []
+            for t in (-2, -1, 1, 2):
+                q = list(p)
+                q[j] += t * h
+                f.append(lml(q))
+            g.append((f[0] - 8 * f[1] + 8 * f[2] - f[3]) / (12 * h))
+        _, L, a = lml(p, want=True)
+        Li = sla.solve_triangular(L, np.identity(L.shape[0]), lower=True)
+        g.append(0.5 * (a @ a - np.sum(Li * Li)))
+        grads.append(g)
+    print(f"  config E (SURVEY grid) share: 8 settings x N=4096, {time.time() - t0:.1f}s")
+    np.savez_compressed(os.path.join(out, "config_e_survey_share.npz"), share=np.array(share),
+                        l_df=np.array([S[i]["l_df"] for i in share]), l_cf=np.array([S[i]["l_cf"] for i in share]),
+                        ratio=0.5, noise=0.0025, lml=vals, grad_idx=np.array(gidx), grad=np.array(grads))
 
 
 def config_e_settings():
@@ -802,7 +992,10 @@ def main():
                 prep=lambda: gen_prep(a.out), window=lambda: gen_prior_window(a.out),
                 configs=lambda: gen_configs(gs, a.out), config_b=lambda: gen_config_b(gs, a.out),
                 config_d=lambda: gen_config_d(gs, a.out),
-                config_e=lambda: gen_config_e(gs, a.out), guard=lambda: gen_guard(gs, a.out))
+                config_e=lambda: gen_config_e(gs, a.out), guard=lambda: gen_guard(gs, a.out),
+                configs_full=lambda: gen_configs_full(gs, a.out), guard_kinds=lambda: gen_guard_kinds(gs, a.out),
+                config_d_shards=lambda: gen_config_d_shards(gs, a.out),
+                config_e_survey=lambda: gen_config_e_survey(gs, a.out))
     for name, fn in jobs.items():
         if a.only and name not in a.only.split(","):
             continue

@@ -214,3 +214,97 @@ def test_headline_ozaki_full_grid_elementwise(n4096):
     ev, em = elem_var(vo, vf), elem_mean(mo, mf)
     print(f"headline full grid, Ozaki vs FP64 engine: var elementwise {ev:.2e}, mean elementwise {em:.2e}")
     assert ev < GATE and em < GATE
+
+
+@pytest.mark.parametrize("variance", ["ozaki", "f64"])
+@pytest.mark.parametrize("name", ["df", "mixed"])
+def test_config_n4096_every_grid_point(golden, name, variance):
+    """The headline (df) and config C (mixed) through engine.krige_jobs — the job-stream API the
+    bench times; its default engine is the guarded int8 Ozaki-II one — at ALL 65,536 grid points
+    (both components), normwise per component against the reference's own GP_laser.py:113-134
+    recipe (myKernel + np.linalg.inv, K* in chunks) at every point (configs_N4096_full.npz),
+    VERDICT r05 item 4."""
+    g = golden("configs_N4096_full.npz")
+    x1, x2, u, v = D.synthetic_tracks(4096, seed=2016)
+    assert np.array_equal(g["x_sum"], [x1.sum(), x2.sum()]) and np.array_equal(g["u_sum"], [u.sum(), v.sum()])
+    _, _, xg = D.bbox_grid(x1, x2, 256, pad=5.0)
+    assert np.array_equal(g["xg_sum"], xg.sum(0))
+    rate = float(g[f"{name}_rate"])
+    ks = E.KernelSpec(kind=name, l_df=5.0, l_cf=5.0, ratio=rate)
+    dev = torch.device("cuda")
+    job = (ks, torch.tensor(np.stack([x1, x2], 1), device=dev), torch.tensor(np.concatenate([u, v]), device=dev),
+           0.0025, torch.tensor(xg, device=dev))
+    stats = {}
+    (mu, var), = list(E.krige_jobs([job], variance=variance, stats=stats))
+    mu, var = mu.cpu().numpy(), var.cpu().numpy()
+    m = xg.shape[0]
+    assert var.size == 2 * m and np.all(var > 0)
+    errs = []
+    for c in (slice(0, m), slice(m, 2 * m)):
+        errs += [rel(mu[c], g[f"{name}_mean"][c]), rel(var[c], g[f"{name}_var"][c])]
+    print(f"{name}/{variance} every point: normwise mean u/v, var u/v = " + ", ".join(f"{e:.2e}" for e in errs)
+          + f"; guard {stats.get('guard')}")
+    assert max(errs) < GATE
+
+
+def test_config_d_every_rank_shard(golden):
+    """Config D (mixed, N_train = 16384, 512² grid): the fit on the device (engine.fit, the
+    Ozaki engine with its guard), then EACH of the 8 ranks' shards predicted as that rank would
+    (data.shard_range), checked at 64 fixture points per shard (config_d_shards.npz: the
+    reference's myKernel, a blocked Cholesky)."""
+    g = golden("config_d_shards.npz")
+    x1, x2, u, v = D.synthetic_tracks(16384, seed=2016)
+    assert np.allclose([x1.sum(), x2.sum()], g["x_sum"], rtol=0, atol=0)
+    _, _, xg_all = D.bbox_grid(x1, x2, 512, pad=5.0)
+    assert np.array_equal(xg_all[g["gidx"]], g["xg"])
+    ks = E.KernelSpec(kind="mixed", l_df=5.0, l_cf=5.0, ratio=float(g["rate"]))
+    gp = E.fit(ks, torch.tensor(np.stack([x1, x2], 1), device="cuda"),
+               torch.tensor(np.concatenate([u, v]), device="cuda"), noise=0.0025, variance="ozaki")
+    pred = E.Predictor(gp, 8192)
+    gidx = g["gidx"]
+    P = 8
+    mu_s, var_s = np.empty(2 * gidx.size), np.empty(2 * gidx.size)
+    K = gidx.size
+    for r in range(P):
+        lo, hi = D.shard_range(xg_all.shape[0], P, r)
+        mine = np.nonzero((gidx >= lo) & (gidx < hi))[0]
+        assert mine.size == 64, r
+        mu, var = (t.cpu().numpy() for t in pred(torch.tensor(xg_all[lo:hi], device="cuda")))
+        m = hi - lo
+        loc = gidx[mine] - lo
+        mu_s[mine], mu_s[K + mine] = mu[loc], mu[m + loc]
+        var_s[mine], var_s[K + mine] = var[loc], var[m + loc]
+    del gp, pred
+    torch.cuda.empty_cache()
+    ev = elem_var(var_s, g["var"])
+    print(f"D all shards: mean {rel(mu_s, g['mean']):.2e} var {rel(var_s, g['var']):.2e} var elementwise {ev:.2e}")
+    assert rel(mu_s, g["mean"]) < GATE and rel(var_s, g["var"]) < GATE
+    assert ev < GATE
+    assert elem_mean(mu_s, g["mean"]) < GATE
+
+
+def test_config_e_survey_sweep_share(golden):
+    """SURVEY §8(d) config E (bench.py --config E): rank 0's 8 of the 64 settings (ℓ_df over
+    [1, 10] km at ℓ_cf = 1 km; mixed α = ½, noise 0.0025) at N_train = 4096 through hyper.sweep:
+    the LML of all 8 and the full gradient (ℓ_df, ℓ_cf, ratio, noise) of 2, against the
+    reference-myKernel fixture (config_e_survey_share.npz)."""
+    g = golden("config_e_survey_share.npz")
+    x1, x2, u, v = D.synthetic_tracks(4096, seed=2016)
+    x, y = np.stack([x1, x2], 1), np.concatenate([u, v])
+    settings = [dict(l_df=float(a), l_cf=float(b)) for a, b in zip(g["l_df"], g["l_cf"])]
+    ks = E.KernelSpec(kind="mixed", l_df=5.0, l_cf=5.0, ratio=float(g["ratio"]))
+    vals, grads = H.sweep(ks, x, y, settings, noise=float(g["noise"]), eval_gradient=True)
+    print("LML rel err", np.max(np.abs(vals - g["lml"]) / np.abs(g["lml"])))
+    assert np.max(np.abs(vals - g["lml"]) / np.abs(g["lml"])) < GATE
+    names = list(H.get_params(ks, 0.0025))
+    cols = [names.index(k) for k in ("l_df", "l_cf", "ratio", "noise")]
+    for k, gi in enumerate(g["grad_idx"]):
+        j = list(g["share"]).index(gi)
+        ref = g["grad"][k]
+        got = grads[j, cols]
+        print(f"setting {gi}: grad {got} vs {ref}")
+        # ∂/∂ℓ, ∂/∂ratio: the fixture's central differences are good to ~1e-8 relative (of the
+        # gradient's scale); ∂/∂noise is exact
+        scale = np.max(np.abs(ref[:3]))
+        assert np.all(np.abs(got[:3] - ref[:3]) < 1e-6 * scale)
+        assert abs(got[3] - ref[3]) < 1e-9 * abs(ref[3])

@@ -393,3 +393,23 @@ def test_ozaki_split_residues_of_wide_w_rows_exact():
         r = t - m * np.rint(t * (1.0 / m))       # the final one-part residue: |t| < 2^50
         ref = np.array([((e % m) + m) % m for e in exact], dtype=np.float64)
         assert np.array_equal(np.mod(r, m), ref), m
+
+
+def test_release_build_rejects_measurement_overrides():
+    """The shipped library is a release build (gp2d_build_info, checked by _native.lib() on load),
+    and a GP2D_RELEASE compile with a measurement override (-DGP2D_<NAME>) fails at the
+    preprocessor (csrc/common.hpp), so no dev switch reaches libgp2d.so."""
+    import subprocess
+    from gp2d import _native
+    info = _native.lib().gp2d_build_info().decode()
+    assert info.startswith("release gfx950") and "oz_pw=49" in info and "oz_pb=45" in info
+    src = os.path.join(ROOT, "2d-gp_amd", "csrc", "common.hpp")
+    base = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-x", "hip", "-E", "-o", os.devnull, src]
+    ok = subprocess.run(base + ["-DGP2D_RELEASE=1"], capture_output=True, text=True)
+    assert ok.returncode == 0, ok.stderr[-500:]
+    bad = subprocess.run(base + ["-DGP2D_RELEASE=1", "-DGP2D_OZ_PW=50"], capture_output=True, text=True)
+    assert bad.returncode != 0 and "not allowed in a GP2D_RELEASE build" in bad.stderr
+    lib_src = os.path.join(ROOT, "2d-gp_amd", "csrc", "gp2d.hip")
+    norel = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-E", "-o", os.devnull, lib_src],
+                           capture_output=True, text=True)
+    assert norel.returncode != 0 and "GP2D_RELEASE" in norel.stderr
