@@ -135,19 +135,20 @@ __device__ __forceinline__ double ard_value(const ArdParams& p, const double* a,
 // Block: 64 (column points) × 4 thread rows; each thread does ROWS_PER_THREAD
 // row points so that the column point's coordinates are loaded once.
 constexpr int ASM_ROWS = 16;
-constexpr int ASM_LOWER = 2;   // `symmetric` mode: K_y's lower block triangle only (gp2d_assemble)
+constexpr int ASM_LOWER = 2;   // `symmetric` mode: K_y's lower triangle only (gp2d_assemble)
 
 // j_off / col_comp (gp2d_assemble_cols): column points start at j_off and only the columns of
 // component col_comp (0: u, 1: v; −1: both) are written — the same per-element arithmetic.
 //
 // The workgroup's 64 column points are staged once through LDS (wave 0 loads the tile with one
 // coalesced 1–1.5 KB read, every wave reads it back); the row point of a wave is wave-uniform
-// (readfirstlane'd index: scalar loads).  symmetric = ASM_LOWER writes only the entries (R, C)
-// of the n × n matrix (n = 2·na_pad, component-major) with C < 128·(R/128 + 1) — the lower block
-// triangle including the 128 × 128 diagonal blocks, which is all gp2d_potrf reads (it zeroes
-// the rest at its end) — i.e. K_uu's and K_vv's lower halves and all of K_vu: half the stores
-// (GP_scripts.py:80-88 likewise fills one triangle of compute_K and mirrors it).  A wave's 64
-// columns lie on one side of every 128 boundary (64-aligned), so whole row segments drop.
+// (readfirstlane'd index: scalar loads).  symmetric = ASM_LOWER writes only the lower triangle
+// (C ≤ R) of the n × n matrix (n = 2·na_pad, component-major) — all gp2d_potrf uses (its
+// diagonal kernel loads the 32×32 sub-blocks whole but never uses, nor stores, their upper
+// parts; the rest of the upper triangle it zeroes at its end) — i.e. K_uu's and K_vv's lower
+// halves and all of K_vu: half the stores, n(n+1)/2 doubles (GP_scripts.py:80-88 likewise
+// fills one triangle of compute_K and mirrors it).  Row segments wholly above the diagonal are
+// skipped per wave (no kernel evaluation either when all four blocks' segments are).
 __global__ __launch_bounds__(256) void assemble_vec_kernel(
     const double* __restrict__ xa, int64_t na, int64_t na_pad,
     const double* __restrict__ xb, int64_t nb, int64_t nb_pad,
@@ -173,16 +174,17 @@ __global__ __launch_bounds__(256) void assemble_vec_kernel(
   } else {
     b1 = colpts[2 * lane]; b2 = colpts[2 * lane + 1];
   }
-  // lower-block limits: column C is kept in matrix row R iff C < 128·(R/128 + 1)
-  const int64_t cu = jt, cv = nb_pad + jt;   // the wave's first matrix column in each component
+  // lower mode: matrix column C is kept in matrix row R iff C ≤ R; the wave's segments start at
+  // column cu (u component) and cv (v component)
+  const int64_t cu = jt, cv = nb_pad + jt;
 #pragma unroll 1
   for (int q = 0; q < ASM_ROWS / 4; ++q) {
     const int64_t i = (int64_t)blockIdx.y * ASM_ROWS + ty + 4 * q;   // wave-uniform
     if (i >= na_pad) break;
-    const int64_t lim0 = (i / 128 + 1) * 128, lim1 = ((na_pad + i) / 128 + 1) * 128;
-    const bool w_uu = !lower || cu < lim0, w_uv = !lower || cv < lim0;
-    const bool w_vu = !lower || cu < lim1, w_vv = !lower || cv < lim1;
-    if (!(w_uu || w_uv || w_vu || w_vv)) continue;
+    const int64_t R0 = i, R1 = na_pad + i;   // the pair's rows in the u and v components
+    if (lower && cu > R1) continue;          // every segment of this row pair is above the diagonal
+    const bool w_uu = !lower || cu + lane <= R0, w_uv = !lower || cv + lane <= R0;
+    const bool w_vu = !lower || cu + lane <= R1, w_vv = !lower || cv + lane <= R1;
     double k11, k12, k22;
     if (jv && i < na) {
       double a0, a1, a2;

@@ -81,10 +81,9 @@ double  gp2d_kernel_diag(const gp2d_kernel_t* k);      /* k(x,x) per component: 
  * on the diagonal when xa == xb (GP_laser.py:114-115); padded rows/columns are
  * identity (when diag_add is used) or zero.
  * symmetric: 0 = cross-covariance K(xa, xb) (compute_Ks); 1 = K_y = K(x, x) + diag_add·I
- * in full (compute_K); 2 = K_y's lower block triangle only (vector families: entries (R, C)
- * with C < 128·(R/128 + 1), the 128×128 diagonal blocks whole, the rest left unwritten) —
- * all gp2d_potrf reads, half the stores (the fit's assembly; GP_scripts.py:80-88 also builds
- * one triangle and mirrors it).                                                   */
+ * in full (compute_K); 2 = K_y's lower triangle only (vector families: entries (R, C) with
+ * C ≤ R, the rest left unwritten) — all gp2d_potrf uses, n(n+1)/2 stores instead of n² (the
+ * fit's assembly; GP_scripts.py:80-88 also builds one triangle and mirrors it).    */
 int gp2d_assemble(const double* xa, int64_t na, int64_t na_pad,
                   const double* xb, int64_t nb, int64_t nb_pad,
                   const gp2d_kernel_t* k, double diag_add, int symmetric,

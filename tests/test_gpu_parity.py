@@ -83,10 +83,10 @@ def test_golden_mykernel_N1024(golden):
 @pytest.mark.parametrize("kind,npts", [("df", 4096), ("mixed", 700), ("cf", 96), ("df", 1)])
 def test_assemble_lower_block_triangle(kind, npts):
     """gp2d_assemble(symmetric = 2), the fit's assembly: into a NaN-filled buffer it writes
-    exactly K_y's lower block triangle (entries (R, C) with C < 128·(R/128 + 1)), bit for bit
-    the full assembly's values there, and leaves every other entry unwritten (still NaN: half the
-    stores at n = 8192); gp2d_potrf + gp2d_trtri from that buffer give the bits of the full
-    assembly's factor and inverse, so nothing in the factorisation reads the unwritten part.
+    exactly K_y's lower triangle (entries (R, C) with C ≤ R), bit for bit the full assembly's
+    values there, and leaves every other entry unwritten (still NaN: half the stores at
+    n = 8192); gp2d_potrf + gp2d_trtri from that buffer give the bits of the full assembly's
+    factor and inverse, so nothing in the factorisation uses the unwritten part.
     npts = 700 pads to 11·64 points (the component boundary inside a 128-block); 1 is a
     single block."""
     import ctypes
@@ -107,7 +107,7 @@ def test_assemble_lower_block_triangle(kind, npts):
     N.check(L_.gp2d_assemble(P(X), npts, npad, P(X), npts, npad, ctypes.byref(desc), 0.0025, 2, P(low), ld, s), "a2")
     F, Lo = full.cpu().numpy()[:n, :n], low.cpu().numpy()[:n, :n]
     R, C = np.indices((n, n))
-    keep = C < 128 * (R // 128 + 1)
+    keep = C <= R
     assert np.array_equal(Lo[keep], F[keep]) and np.all(np.isfinite(F))
     assert np.all(np.isnan(Lo[~keep]))
     if n >= 8192:   # the stores: ≤ 270 MB at n = 8192
