@@ -189,7 +189,7 @@ def test_guard_decision_is_the_same_on_every_path(guard_case):
 # the other two vector kernels at hard settings (guard_kinds_N4096.npz):
 # mixed (ℓ_df = 3, ℓ_cf = 8, ratio ½, noise 1e-4) and curl-free (ℓ = 12, noise 1e-3) — the guard's
 # decision (engine, W bits, K* bits) for each, as measured on the box
-KIND_CASES = [(0, "mixed", None), (1, "cf", None)]
+KIND_CASES = [(0, "mixed", ("ozaki", 56, 48)), (1, "cf", ("ozaki", 51, 45))]
 
 
 @pytest.fixture(scope="module")
