@@ -38,7 +38,7 @@ from gp2d import engine as E  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--jobs", type=int, default=48)
 ap.add_argument("--P", default="1,2,4,8")
-ap.add_argument("--ranks", default="first,last")
+ap.add_argument("--ranks", default="first,last", help="first,last or all")
 ap.add_argument("--transport", default="rccl,none")
 a = ap.parse_args()
 
@@ -113,7 +113,7 @@ def run(P, r, transport, jobs):
 
 
 for P in [int(p) for p in a.P.split(",")]:
-    ranks = sorted({0 if w == "first" else P - 1 for w in a.ranks.split(",")})
+    ranks = list(range(P)) if a.ranks == "all" else sorted({0 if w == "first" else P - 1 for w in a.ranks.split(",")})
     for r in ranks:
         for transport in (a.transport.split(",") if P > 1 else ["none"]):
             run(P, r, transport, a.jobs)
