@@ -40,6 +40,7 @@ ap.add_argument("--jobs", type=int, default=48)
 ap.add_argument("--P", default="1,2,4,8")
 ap.add_argument("--ranks", default="first,last", help="first,last or all")
 ap.add_argument("--transport", default="rccl,none")
+ap.add_argument("--warm", type=int, default=0, help="warm jobs before each timed stream (default 2·P)")
 a = ap.parse_args()
 
 dev = torch.device("cuda", 0)
@@ -93,7 +94,7 @@ C.broadcast = fake_broadcast
 
 def run(P, r, transport, jobs):
     state.update(P=P, r=r, transport=transport, bytes=0)
-    for _ in GD.krige_jobs_sharded(itertools.repeat(job, 2 * P), chunk=8192):   # warm: every owner once
+    for _ in GD.krige_jobs_sharded(itertools.repeat(job, max(a.warm, 2 * P)), chunk=8192):   # every owner twice
         pass
     torch.cuda.synchronize()
     stats = {}
@@ -113,7 +114,10 @@ def run(P, r, transport, jobs):
 
 
 for P in [int(p) for p in a.P.split(",")]:
-    ranks = list(range(P)) if a.ranks == "all" else sorted({0 if w == "first" else P - 1 for w in a.ranks.split(",")})
+    if a.ranks == "all":
+        ranks = list(range(P))
+    else:
+        ranks = sorted({(0 if w == "first" else P - 1 if w == "last" else int(w)) % P for w in a.ranks.split(",")})
     for r in ranks:
         for transport in (a.transport.split(",") if P > 1 else ["none"]):
             run(P, r, transport, a.jobs)
