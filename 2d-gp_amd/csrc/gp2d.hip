@@ -296,6 +296,39 @@ struct FactorCtx {
   std::mutex* enqueue;
 };
 
+__global__ void stream_touch_kernel(int) {}
+
+// Sets are created on first use (fewer streams, fewer HW queues shared), and each new stream is
+// used at once by an empty kernel: HIP binds a stream to a hardware queue at its first command
+// (the least-used queue of its priority once GPU_MAX_HW_QUEUES are taken), so touching the set
+// here fixes its queues at creation, not at whatever point of the caller's stream use the first
+// factorisation falls (gp2d_factor_warm, DESIGN.md §6 "bench state").  Caller holds g_fs.mu.
+int ensure_factor_sets(std::vector<std::unique_ptr<FactorSet>>& sets, int count) {
+  while ((int)sets.size() < count) {
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) { lo = 0; hi = 0; }
+    auto f = std::make_unique<FactorSet>();
+    // crit (diagonal kernels, skinny panel GEMMs) and aux at the highest priority, bulk (the
+    // trailing SYRK) and inv (the fused inverse's GEMMs) at the lowest.  Keeping CUs free of
+    // the bulk stream (CU-masked streams) was measured slower (DESIGN.md §3.3).
+    if (hipStreamCreateWithPriority(&f->crit, hipStreamNonBlocking, hi) != hipSuccess ||
+        hipStreamCreateWithPriority(&f->bulk, hipStreamNonBlocking, lo) != hipSuccess ||
+        hipStreamCreateWithPriority(&f->aux, hipStreamNonBlocking, hi) != hipSuccess ||
+        hipStreamCreateWithPriority(&f->inv, hipStreamNonBlocking, lo) != hipSuccess) {
+      set_error("hipStreamCreate failed"); return -1;
+    }
+    for (hipStream_t st : {f->crit, f->bulk, f->aux, f->inv}) {
+      stream_touch_kernel<<<1, 64, 0, st>>>(0);
+      if (check_launch("stream_touch_kernel") != 0) return -1;
+    }
+    f->ev.resize(6);
+    for (auto& e : f->ev)
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) { set_error("hipEventCreate failed"); return -1; }
+    sets.push_back(std::move(f));
+  }
+  return 0;
+}
+
 int factor_streams(FactorCtx& c, int nblk, hipStream_t caller) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) { set_error("hipGetDevice failed"); return -1; }
@@ -320,24 +353,7 @@ int factor_streams(FactorCtx& c, int nblk, hipStream_t caller) {
     for (const auto& pr : own) known = known || pr.first == caller;
     if (!known && own.size() < 256) own.emplace_back(caller, idx);
   }
-  while ((int)sets.size() <= idx) {   // sets are created on first use: fewer streams, fewer HW queues shared
-    int lo = 0, hi = 0;
-    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) { lo = 0; hi = 0; }
-    auto f = std::make_unique<FactorSet>();
-    // crit (diagonal kernels, skinny panel GEMMs) and aux at the highest priority, bulk (the
-    // trailing SYRK) and inv (the fused inverse's GEMMs) at the lowest.  Keeping CUs free of
-    // the bulk stream (CU-masked streams) was measured slower (DESIGN.md §3.6).
-    if (hipStreamCreateWithPriority(&f->crit, hipStreamNonBlocking, hi) != hipSuccess ||
-        hipStreamCreateWithPriority(&f->bulk, hipStreamNonBlocking, lo) != hipSuccess ||
-        hipStreamCreateWithPriority(&f->aux, hipStreamNonBlocking, hi) != hipSuccess ||
-        hipStreamCreateWithPriority(&f->inv, hipStreamNonBlocking, lo) != hipSuccess) {
-      set_error("hipStreamCreate failed"); return -1;
-    }
-    f->ev.resize(6);
-    for (auto& e : f->ev)
-      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) { set_error("hipEventCreate failed"); return -1; }
-    sets.push_back(std::move(f));
-  }
+  if (ensure_factor_sets(sets, idx + 1) != 0) return -1;
   FactorSet& f = *sets[idx];
   while ((int)f.blk.size() < nblk) {
     hipEvent_t e;
@@ -697,6 +713,18 @@ int gp2d_factor_sets(int k) {
       for (auto& own : g_fs.owner) own.clear();
   }
   return prev;
+}
+
+int gp2d_factor_warm(int nsets) {
+  GP2D_REQUIRE(nsets >= 1 && nsets <= GP2D_FACTOR_CTX, "factor_warm: nsets must be 1..4");
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) { set_error("factor_warm: no HIP device"); return -1; }
+  std::lock_guard<std::mutex> lk(g_fs.mu);
+  if ((int)g_fs.sets.size() <= dev) {
+    g_fs.sets.resize(dev + 1);
+    g_fs.owner.resize(dev + 1);
+  }
+  return ensure_factor_sets(g_fs.sets[dev], nsets);
 }
 
 int gp2d_factor_set_of(void* stream) {

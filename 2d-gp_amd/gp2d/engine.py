@@ -40,7 +40,28 @@ def _require_device(device=None) -> torch.device:
         raise N.NativeLibraryError("gp2d needs a HIP device (torch.cuda.is_available() is False); "
                                    "there is no CPU fallback")
     N.lib()
-    return torch.device(device if device is not None else "cuda")
+    dev = torch.device(device if device is not None else "cuda")
+    warm_streams(dev)
+    return dev
+
+
+_WARM = set()
+
+
+def warm_streams(device=None):
+    """Bind the library's internal factorisation streams to their hardware queues now, once per
+    device (gp2d_factor_warm): HIP binds a stream to a queue at its first command, and a job
+    stream whose first factorisation came after its side stream's first use ran 56.5 instead of
+    53.1 ms per headline job (tools/probe_first_fit.py, DESIGN.md §6 "bench state").  Called by
+    every device entry point of the engine (through _require_device) before it touches a stream
+    of its own; a caller that uses its own side streams before any gp2d call can call it first."""
+    dev = torch.device(device if device is not None else "cuda")
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    if idx in _WARM:
+        return
+    with torch.cuda.device(idx):
+        N.check(N.lib().gp2d_factor_warm(1), "gp2d_factor_warm")
+    _WARM.add(idx)
 
 
 def morton_sort(P: torch.Tensor):

@@ -11,7 +11,12 @@ it in the process, 56.5 ms when the first fit of the process comes from krige_jo
   fit_side    — engine.fit(check=False) issued from a side stream (krige_jobs' first fit);
   job         — bench.py's unpipelined job: fit(check=False), check(), Predictor, predict;
   potrf_tiny  — one gp2d_potrf of a 128×128 identity from the current stream (the library's
-                internal factor streams are created there).
+                internal factor streams are created there);
+  pool_then_potrf — a kernel on one of torch's high-priority pool streams first, then the raw
+                gp2d_potrf (no engine call: nothing warms the factor streams before the pool
+                stream's first use).
+The engine's own entry points warm the factor streams first (engine.warm_streams) since round 6,
+so `none` and `fit_side` measure that fix.
 usage: python tools/probe_first_fit.py ACTION [jobs]"""
 import ctypes
 import itertools
@@ -55,6 +60,17 @@ elif ACTION == "job":
     gp.ready_on(torch.cuda.current_stream(dev))
     E.Predictor(gp, 8192)(xg)
 elif ACTION == "potrf_tiny":
+    L = E.N.lib()
+    A = torch.eye(128, dtype=torch.float64, device=dev)
+    dinv = torch.empty((1, 128, 128), dtype=torch.float64, device=dev)
+    info = torch.zeros(1, dtype=torch.int32, device=dev)
+    E.N.check(L.gp2d_potrf(E._ptr(A), 128, 128, E._ptr(dinv), E._ptr(info), None, 0,
+                           E._stream_handle(dev)), "gp2d_potrf")
+elif ACTION == "pool_then_potrf":
+    s = torch.cuda.Stream(dev, priority=-1)
+    with torch.cuda.stream(s):
+        torch.ones(16, device=dev).add_(1)
+    torch.cuda.synchronize()
     L = E.N.lib()
     A = torch.eye(128, dtype=torch.float64, device=dev)
     dinv = torch.empty((1, 128, 128), dtype=torch.float64, device=dev)

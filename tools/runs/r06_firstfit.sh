@@ -1,9 +1,11 @@
 #!/bin/bash
-# r06: which first action of a process gives the job stream its fast state (tools/probe_first_fit.py)
+# r06: which first action of a process gives the job stream its fast state (tools/probe_first_fit.py),
+# with the engine's stream warm-up (engine.warm_streams)
 set -o pipefail
-R=gpurun_out/r06_firstfit
+R=gpurun_out/r06_firstfit2
 mkdir -p $R
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-for a in none fit_nocheck fit_check fit_side job potrf_tiny none; do
+for a in none fit_side pool_then_potrf potrf_tiny none; do
   timeout -k 10 200 python -u tools/probe_first_fit.py $a 40 >> $R/first.jsonl 2>> $R/first.err || exit 1
 done
+timeout -k 10 300 python -u bench.py --f64-steps 0 --dropin-steps 0 --cpu-baseline 0 --steps 48 --unpipelined-steps 0 > $R/u0.json 2> $R/u0.err
