@@ -183,6 +183,10 @@ def setup_dist(args):
         # rehearsing the multi-rank path on a one-GPU box
         local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
+        # the library's factor streams take their hardware queues before RCCL's and torch's
+        # streams are first used (engine.warm_streams; DESIGN.md §6 "bench state")
+        from gp2d import engine as E
+        E.warm_streams(torch.device("cuda", local))
         backend = os.environ.get("GP2D_DIST_BACKEND", "nccl")
         kw = {"device_id": torch.device("cuda", local)} if backend == "nccl" else {}
         dist.init_process_group(backend, **kw)
@@ -192,6 +196,8 @@ def setup_dist(args):
             from gp2d import comm as GC
             GC.get(torch.device("cuda", local))
         return dist.get_world_size(), dist.get_rank(), torch.device("cuda", local)
+    from gp2d import engine as E
+    E.warm_streams(torch.device("cuda", 0))
     return 1, 0, torch.device("cuda", 0)
 
 
