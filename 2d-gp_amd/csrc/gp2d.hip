@@ -715,10 +715,13 @@ int gp2d_factor_sets(int k) {
   return prev;
 }
 
-int gp2d_factor_warm(int nsets) {
+int gp2d_factor_warm(int nsets, void* stream) {
   GP2D_REQUIRE(nsets >= 1 && nsets <= GP2D_FACTOR_CTX, "factor_warm: nsets must be 1..4");
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) { set_error("factor_warm: no HIP device"); return -1; }
+  // the caller's stream first (the predict stream of a job stream): then the factor sets
+  stream_touch_kernel<<<1, 64, 0, S(stream)>>>(0);
+  GP2D_CHECK(check_launch("stream_touch_kernel"));
   std::lock_guard<std::mutex> lk(g_fs.mu);
   if ((int)g_fs.sets.size() <= dev) {
     g_fs.sets.resize(dev + 1);

@@ -85,7 +85,7 @@ _SIGS = {
     "gp2d_kernel_diag": (_D, [_KP]),
     "gp2d_assemble": (_I, [_P, _I64, _I64, _P, _I64, _I64, _KP, _D, _I, _P, _I64, _P]),
     "gp2d_factor_sets": (_I, [_I]),
-    "gp2d_factor_warm": (_I, [_I]),
+    "gp2d_factor_warm": (_I, [_I, _P]),
     "gp2d_factor_set_of": (_I, [_P]),
     "gp2d_factor_join": (_I, [_I]),
     "gp2d_potrf_workspace": (_SZ, [_I64]),

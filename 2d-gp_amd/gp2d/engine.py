@@ -49,18 +49,20 @@ _WARM = set()
 
 
 def warm_streams(device=None):
-    """Bind the library's internal factorisation streams to their hardware queues now, once per
-    device (gp2d_factor_warm): HIP binds a stream to a queue at its first command, and a job
-    stream whose first factorisation came after its side stream's first use ran 56.5 instead of
-    53.1 ms per headline job (tools/probe_first_fit.py, DESIGN.md §6 "bench state").  Called by
-    every device entry point of the engine (through _require_device) before it touches a stream
-    of its own; a caller that uses its own side streams before any gp2d call can call it first."""
+    """Bind the current (predict) stream and then the library's internal factorisation streams
+    to their hardware queues, once per device (gp2d_factor_warm).  HIP binds a stream to a queue
+    at its first command; a job stream ran 53.1–53.9 ms per headline job with the predict stream,
+    the factor streams and the side streams first used in that order, and 56.4–56.7 ms in the
+    other orders measured (tools/probe_first_fit.py, DESIGN.md §6 "bench state").  Every device
+    entry point of the engine calls it (through _require_device) before it touches a stream of
+    its own; a caller that uses its own side streams before any gp2d call should call it first."""
     dev = torch.device(device if device is not None else "cuda")
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
     if idx in _WARM:
         return
     with torch.cuda.device(idx):
-        N.check(N.lib().gp2d_factor_warm(1), "gp2d_factor_warm")
+        N.check(N.lib().gp2d_factor_warm(1, ctypes.c_void_p(torch.cuda.current_stream(idx).cuda_stream)),
+                "gp2d_factor_warm")
     _WARM.add(idx)
 
 

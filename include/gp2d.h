@@ -105,13 +105,14 @@ int gp2d_assemble(const double* xa, int64_t na, int64_t na_pad,
  * A call with k > 1 starts a new batch: the caller-stream → set map is cleared, so the
  * next k caller streams get sets 0..k−1 in order of first use.                       */
 int gp2d_factor_sets(int k);
-/* gp2d_factor_warm(k): create the current device's internal factor stream sets 0..k−1 now and
- *   put one empty kernel on each of their streams.  HIP binds a stream to a hardware queue at its
- *   first command, so a process that calls this before it first uses its own side streams keeps
- *   the factor chain's queues apart from them; engine.krige_jobs / fit call it first thing.  On one
- *   MI355X a job stream whose first factorisation was issued after a side stream's first use ran
- *   56.5 ms per headline job, 53.1 ms otherwise (DESIGN.md §6 "bench state").                  */
-int gp2d_factor_warm(int nsets);
+/* gp2d_factor_warm(k, stream): put one empty kernel on `stream` (the caller's predict stream),
+ *   then create the current device's internal factor stream sets 0..k−1 and put one empty kernel
+ *   on each of their streams.  HIP binds a stream to a hardware queue at its first command; on
+ *   one MI355X a job stream ran 53.1–53.9 ms per headline job when its predict stream, then the
+ *   factor streams, then its side streams were first used in that order, and 56.4–56.7 ms in the
+ *   other orders measured (tools/probe_first_fit.py, DESIGN.md §6 "bench state").
+ *   engine.warm_streams calls it once per device before any engine stream is used.            */
+int gp2d_factor_warm(int nsets, void* stream);
 /* gp2d_factor_set_of: the internal stream set `stream`'s factorisations currently draw
  * (0..k−1), or −1 if the stream has none in use (diagnostics and tests).            */
 int gp2d_factor_set_of(void* stream);

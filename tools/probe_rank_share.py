@@ -45,7 +45,7 @@ a = ap.parse_args()
 
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
-E.warm_streams(dev)   # as bench.py: the factor streams bound before RCCL's first use
+E.warm_streams(dev)   # as bench.py: the predict and factor streams bound before RCCL's first use
 dist.init_process_group("nccl", init_method="tcp://127.0.0.1:29563", rank=0, world_size=1, device_id=dev)
 comm = C.get(dev)
 

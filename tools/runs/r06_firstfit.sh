@@ -3,7 +3,7 @@
 # with the engine's stream warm-up (engine.warm_streams); the bench without its reference phase;
 # the rank-share emulation with the warm-up before RCCL's init
 set -o pipefail
-R=gpurun_out/r06_firstfit2
+R=gpurun_out/r06_firstfit3
 mkdir -p $R
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 for a in none fit_side pool_then_potrf potrf_tiny none; do
