@@ -302,6 +302,32 @@ def test_round_robin_guard_decisions_two_ranks_bit_identical(tmp_path):
     assert engines[1][0] == "ozaki" and (engines[1][1], engines[1][2]) != (49, 45)
 
 
+def _rr_noguard_worker(rank, world, port, out_dir):
+    """The job stream with the accuracy guard off (GP2D_GUARD=0, read at import): the owner's
+    status block carries the NaN "no guard ran" sentinel, so the receiving rank keeps the
+    default precision instead of acting on the block's other bytes."""
+    os.environ["GP2D_GUARD"] = "0"
+    _rr_worker(rank, world, port, out_dir, "ozaki", None, GUARD_NOISES)
+
+
+def test_round_robin_jobs_without_guard_bit_identical(tmp_path):
+    from gp2d import distributed as GD
+    from gp2d import engine as E
+    world = 2
+    _spawn(_rr_noguard_worker, world, str(tmp_path))
+    r = [np.load(os.path.join(tmp_path, f"rr{i}.npz")) for i in range(world)]
+    for j, (spec, x, y, noise, xg) in enumerate(_jobs(GUARD_NOISES)):
+        if noise < 1e-6:
+            continue   # noise 1e-8 without the guard: not a parity case (the guard routes it to FP64)
+        gp = E.fit(spec, x, y, noise, variance="ozaki", guard=False)
+        mu, var = (t.cpu().numpy() for t in E.Predictor(gp, 1024)(xg))
+        m = xg.shape[0]
+        shards_m = [(int(r[i][f"lo{j}"]), int(r[i][f"hi{j}"]), r[i][f"mean{j}"]) for i in range(world)]
+        shards_v = [(int(r[i][f"lo{j}"]), int(r[i][f"hi{j}"]), r[i][f"var{j}"]) for i in range(world)]
+        assert np.array_equal(GD.assemble_from_shards(m, 2, shards_m), mu), j
+        assert np.array_equal(GD.assemble_from_shards(m, 2, shards_v), var), j
+
+
 def test_round_robin_jobs_non_spd_raises_on_every_rank(tmp_path):
     """Job 3 (owned by rank 1) has a non-SPD K_y: both ranks raise LinAlgError after the
     three jobs before it, none hangs."""
