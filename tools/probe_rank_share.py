@@ -41,6 +41,9 @@ ap.add_argument("--P", default="1,2,4,8")
 ap.add_argument("--ranks", default="first,last", help="first,last or all")
 ap.add_argument("--transport", default="rccl,none")
 ap.add_argument("--warm", type=int, default=0, help="warm jobs before each timed stream (default 2·P)")
+ap.add_argument("--copy-repeat", type=int, default=1,
+                help="RCCL copies per received payload (stretches the copy kernel's residency toward an "
+                     "xGMI transfer's duration: 10 ≈ 4 ms per job)")
 a = ap.parse_args()
 
 dev = torch.device("cuda", 0)
@@ -84,7 +87,8 @@ def fake_broadcast(t, src):
     s = payload[(tuple(t.shape), t.dtype)]
     state["bytes"] += t.numel() * t.element_size()
     if state["transport"] == "rccl":
-        comm.sendrecv(s, 0, t, 0)                # RCCL's copy kernel on the current (comm) stream
+        for _ in range(a.copy_repeat if t.numel() > 1 << 20 else 1):
+            comm.sendrecv(s, 0, t, 0)            # RCCL's copy kernel on the current (comm) stream
     else:
         t.copy_(s)                              # a plain device copy (the transport's cost removed)
 
@@ -107,6 +111,7 @@ def run(P, r, transport, jobs):
     dt = time.perf_counter() - t0
     ms = 1e3 * dt / jobs
     out = {"P": P, "rank": r, "transport": transport if P > 1 else "none (one rank)", "jobs": jobs,
+           "copy_repeat": a.copy_repeat,
            "ms_per_job": ms, "implied_points_per_s": m / (ms * 1e-3), "fits_issued": stats.get("fits_issued", 0),
            "received_mb_per_job": state["bytes"] / jobs / 1e6,
            "shard_points": int(np.diff(D.shard_range(m, P, r))[0])}
