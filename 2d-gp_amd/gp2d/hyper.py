@@ -345,7 +345,10 @@ def allreduce_disjoint(vals: np.ndarray, grads: np.ndarray, device=None):
     bit-exact).  -inf entries travel as a separate mask."""
     bad = np.isneginf(vals)
     v = np.where(bad, 0.0, vals)
-    dev = device if (device is not None and torch.cuda.is_available() and dist.get_backend() == "nccl") else "cpu"
+    if torch.cuda.is_available() and dist.get_backend() == "nccl":   # RCCL reduces device tensors only
+        dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    else:
+        dev = "cpu"
     buf = torch.as_tensor(np.concatenate([v, bad.astype(np.float64), grads.reshape(-1)]), device=dev)
     C.all_reduce(buf, "sum")
     out = buf.cpu().numpy()
