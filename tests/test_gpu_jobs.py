@@ -139,3 +139,25 @@ def test_predictor_reuses_the_grid_order_only_for_the_same_grid():
     m3, v3 = pr(xg, reuse_grid=True)
     rm, rv = E.Predictor(gp, 1024)(xg.clone())
     assert torch.equal(m3, rm) and torch.equal(v3, rv)
+
+
+def test_warm_streams_once_per_device_and_argument_checks():
+    """engine.warm_streams binds the predict stream, then the factor streams, to their hardware
+    queues once per device (gp2d_factor_warm; DESIGN.md §6 "stream binding"): idempotent, and the
+    fits after it are the bits of fits without it (the same kernels on the same streams)."""
+    import ctypes
+    from gp2d import _native as N
+    L = N.lib()
+    assert L.gp2d_factor_warm(0, None) < 0 and b"nsets" in L.gp2d_last_error()
+    assert L.gp2d_factor_warm(5, None) < 0
+    E.warm_streams()
+    E.warm_streams(torch.device("cuda", torch.cuda.current_device()))
+    assert torch.cuda.current_device() in E._WARM
+    assert L.gp2d_factor_warm(1, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)) == 0   # sets exist: no-op
+    rng = np.random.default_rng(8)
+    x = np.stack([rng.uniform(0, 30, 300), rng.uniform(0, 30, 300)], 1)
+    y = rng.normal(0, 0.3, 600)
+    spec = E.KernelSpec(kind="df", l_df=4.0)
+    a = E.fit(spec, x, y, 0.01, variance="ozaki")
+    b = E.fit(spec, x, y, 0.01, variance="ozaki")
+    assert torch.equal(a.W, b.W) and torch.equal(a.alpha, b.alpha)
