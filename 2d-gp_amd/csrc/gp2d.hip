@@ -287,7 +287,6 @@ struct FactorSet {
 constexpr int GP2D_FACTOR_CTX = 4;
 FactorStreams g_fs;
 std::atomic<int> g_factor_sets{1};   // sets in use (gp2d_factor_sets); 1: every caller shares one
-std::atomic<int> g_factor_reserve{0};   // CUs reserved for crit + aux in sets made later (gp2d_factor_reserve)
 thread_local int t_factor_join = 0;   // gp2d_factor_join: this thread's factorisations join on the host
 
 struct FactorCtx {
@@ -312,30 +311,10 @@ int ensure_factor_sets(std::vector<std::unique_ptr<FactorSet>>& sets, int count)
     // crit (diagonal kernels, skinny panel GEMMs) and aux at the highest priority, bulk (the
     // trailing SYRK) and inv (the fused inverse's GEMMs) at the lowest.  Keeping CUs free of
     // the bulk stream (CU-masked streams) was measured slower.
-    const int reserve = g_factor_reserve.load();
-    if (reserve > 0) {
-      // crit + aux confined to `reserve` CUs (the top mask bits: reserve / 8 per XCD), bulk + inv
-      // to the rest, so the chain's kernels never share a CU with the trailing SYRK
-      int dev = 0, ncu = 0;
-      hipDeviceProp_t prop;
-      if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) {
-        set_error("factor streams: cannot query the device"); return -1;
-      }
-      ncu = prop.multiProcessorCount;
-      if (reserve >= ncu) { set_error("factor_reserve: reserve must be below the CU count"); return -1; }
-      std::vector<uint32_t> mc((ncu + 31) / 32, 0u), mb((ncu + 31) / 32, 0u);
-      for (int c = 0; c < ncu; ++c) (c >= ncu - reserve ? mc : mb)[c / 32] |= 1u << (c % 32);
-      const uint32_t nw = (uint32_t)mc.size();
-      if (hipExtStreamCreateWithCUMask(&f->crit, nw, mc.data()) != hipSuccess ||
-          hipExtStreamCreateWithCUMask(&f->aux, nw, mc.data()) != hipSuccess ||
-          hipExtStreamCreateWithCUMask(&f->bulk, nw, mb.data()) != hipSuccess ||
-          hipExtStreamCreateWithCUMask(&f->inv, nw, mb.data()) != hipSuccess) {
-        set_error("hipExtStreamCreateWithCUMask failed"); return -1;
-      }
-    } else if (hipStreamCreateWithPriority(&f->crit, hipStreamNonBlocking, hi) != hipSuccess ||
-               hipStreamCreateWithPriority(&f->bulk, hipStreamNonBlocking, lo) != hipSuccess ||
-               hipStreamCreateWithPriority(&f->aux, hipStreamNonBlocking, hi) != hipSuccess ||
-               hipStreamCreateWithPriority(&f->inv, hipStreamNonBlocking, lo) != hipSuccess) {
+    if (hipStreamCreateWithPriority(&f->crit, hipStreamNonBlocking, hi) != hipSuccess ||
+        hipStreamCreateWithPriority(&f->bulk, hipStreamNonBlocking, lo) != hipSuccess ||
+        hipStreamCreateWithPriority(&f->aux, hipStreamNonBlocking, hi) != hipSuccess ||
+        hipStreamCreateWithPriority(&f->inv, hipStreamNonBlocking, lo) != hipSuccess) {
       set_error("hipStreamCreate failed"); return -1;
     }
     for (hipStream_t st : {f->crit, f->bulk, f->aux, f->inv}) {
@@ -734,14 +713,6 @@ int gp2d_factor_sets(int k) {
       for (auto& own : g_fs.owner) own.clear();
   }
   return prev;
-}
-
-int gp2d_factor_reserve(int cus) {
-  GP2D_REQUIRE(cus >= 0 && cus % 8 == 0, "factor_reserve: cus must be a non-negative multiple of 8");
-  std::lock_guard<std::mutex> lk(g_fs.mu);
-  for (const auto& d : g_fs.sets)
-    GP2D_REQUIRE(d.empty(), "factor_reserve: the factor streams already exist (call it before the first fit)");
-  return g_factor_reserve.exchange(cus);
 }
 
 int gp2d_factor_warm(int nsets, void* stream) {

@@ -23,7 +23,7 @@ COMM_SUM, COMM_MAX, COMM_MIN = 0, 1, 2
 # every symbol declared in include/gp2d.h
 EXPORTS = (
     "gp2d_abi_version", "gp2d_build_info", "gp2d_padded_points", "gp2d_block_dim", "gp2d_kernel_diag",
-    "gp2d_assemble", "gp2d_factor_sets", "gp2d_factor_warm", "gp2d_factor_reserve", "gp2d_factor_set_of", "gp2d_factor_join", "gp2d_potrf_workspace", "gp2d_potrf", "gp2d_trtri_workspace", "gp2d_trtri",
+    "gp2d_assemble", "gp2d_factor_sets", "gp2d_factor_warm", "gp2d_factor_set_of", "gp2d_factor_join", "gp2d_potrf_workspace", "gp2d_potrf", "gp2d_trtri_workspace", "gp2d_trtri",
     "gp2d_potrf_inv_workspace", "gp2d_potrf_inv", "gp2d_potrf_batched", "gp2d_trtri_batched_workspace",
     "gp2d_trtri_batched",
     "gp2d_potrs_workspace", "gp2d_potrs_inv", "gp2d_predict_workspace", "gp2d_predict",
@@ -86,7 +86,6 @@ _SIGS = {
     "gp2d_assemble": (_I, [_P, _I64, _I64, _P, _I64, _I64, _KP, _D, _I, _P, _I64, _P]),
     "gp2d_factor_sets": (_I, [_I]),
     "gp2d_factor_warm": (_I, [_I, _P]),
-    "gp2d_factor_reserve": (_I, [_I]),
     "gp2d_factor_set_of": (_I, [_P]),
     "gp2d_factor_join": (_I, [_I]),
     "gp2d_potrf_workspace": (_SZ, [_I64]),

@@ -113,12 +113,6 @@ int gp2d_factor_sets(int k);
  *   other orders measured (tools/probe_first_fit.py, DESIGN.md §6 "bench state").
  *   engine.warm_streams calls it once per device before any engine stream is used.            */
 int gp2d_factor_warm(int nsets, void* stream);
-/* gp2d_factor_reserve(cus): factor stream sets created after this call confine the critical
- *   path (crit, aux: diagonal kernels, panel TRSMs, column updates) to `cus` CUs (a multiple of
- *   8: cus / 8 per XCD) and the trailing SYRK / inverse GEMMs (bulk, inv) to the others, with
- *   hipExtStreamCreateWithCUMask (no stream priorities then).  0 (default): no masks.  Returns
- *   the previous value; −2 once the sets exist.                                              */
-int gp2d_factor_reserve(int cus);
 /* gp2d_factor_set_of: the internal stream set `stream`'s factorisations currently draw
  * (0..k−1), or −1 if the stream has none in use (diagnostics and tests).            */
 int gp2d_factor_set_of(void* stream);
