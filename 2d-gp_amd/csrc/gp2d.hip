@@ -698,8 +698,6 @@ static int potrf_impl(double* A, int64_t n, int64_t lda, double* dinv, int* info
 }
 
 extern "C" {
-struct CrtSide;   // the predict's CRT stream (below, gp2d_ozaki_set_crt_side)
-static int crt_side_get(CrtSide** out);
 size_t gp2d_potrf_workspace(int64_t) { return 0; }
 
 int gp2d_factor_sets(int k) {
@@ -724,16 +722,12 @@ int gp2d_factor_warm(int nsets, void* stream) {
   // the caller's stream first (the predict stream of a job stream): then the factor sets
   stream_touch_kernel<<<1, 64, 0, S(stream)>>>(0);
   GP2D_CHECK(check_launch("stream_touch_kernel"));
-  {
-    std::lock_guard<std::mutex> lk(g_fs.mu);
-    if ((int)g_fs.sets.size() <= dev) {
-      g_fs.sets.resize(dev + 1);
-      g_fs.owner.resize(dev + 1);
-    }
-    GP2D_CHECK(ensure_factor_sets(g_fs.sets[dev], nsets));
+  std::lock_guard<std::mutex> lk(g_fs.mu);
+  if ((int)g_fs.sets.size() <= dev) {
+    g_fs.sets.resize(dev + 1);
+    g_fs.owner.resize(dev + 1);
   }
-  CrtSide* side = nullptr;   // then the predict's CRT stream
-  return crt_side_get(&side);
+  return ensure_factor_sets(g_fs.sets[dev], nsets);
 }
 
 int gp2d_factor_set_of(void* stream) {
@@ -1322,14 +1316,12 @@ static size_t oz_list_bytes(int64_t n, int64_t chunk) {
 }
 
 // workspace of gp2d_predict_ozaki for a fit with nmod moduli (the layout follows nmod)
-// (Bres planes, two Cres plane sets, two sets of mean / variance partials, flags, lists: chunk c
-// uses set c mod 2, so chunk c's CRT can run beside chunk c+1's GEMMs — see crt_side below)
 static size_t predict_ozaki_ws(int64_t n, int64_t chunk, int nm) {
   if (nm <= 0 || n <= 0) return 0;
   const int64_t cp = round_up(chunk < 1 ? 1 : chunk, IBN);
   const int64_t ncols = 2 * cp;
-  return 3 * (size_t)nm * (size_t)n * (size_t)ncols                        // Bres + 2 × Cres planes
-         + 2 * sizeof(double) * ((size_t)(n / 2 / OZ_KS_T + 1) + (size_t)(n / OZ_CRT_ROWS + 1)) * ncols
+  return 2 * (size_t)nm * (size_t)n * (size_t)ncols                        // Bres + Cres planes
+         + sizeof(double) * ((size_t)(n / 2 / OZ_KS_T + 1) + (size_t)(n / OZ_CRT_ROWS + 1)) * ncols
          + oz_flag_bytes(n, chunk) + oz_list_bytes(n, chunk);
 }
 static size_t predict_ozaki_planes_ws(int64_t n, int64_t chunk, int nm);
@@ -1342,52 +1334,6 @@ size_t gp2d_predict_ozaki_workspace_nmod(int64_t n, int64_t chunk, int nmod) {
 }
 
 void gp2d_ozaki_set_skip(int on) { g_oz_skip = on ? 1 : 0; }
-
-// ---- chunk c's CRT + finalize beside chunk c+1's int8 GEMMs
-// The CRT (HBM-read-bound, 1.6 GB per headline chunk) and the GEMMs (MFMA-bound) share the CUs
-// well: side by side the 12 GEMM launches of a chunk and another chunk's CRT take 5.50 ms against
-// 5.88 ms one after the other (tools/microbench/coresid.hip, profiles/r06_coresid.json).  Beside
-// the next chunk's K* kernel instead (both HBM-bound) they were slower than serial (round 4,
-// DESIGN.md §3).  So the CRT of chunk c waits for chunk c+1's K* kernel and slab lists too, and
-// runs on an internal stream per device while the caller's stream runs chunk c+1's GEMMs.
-struct CrtSide {
-  std::mutex mu;                   // held across one predict's enqueue (the two events are reused)
-  hipStream_t st = nullptr;
-  hipEvent_t ev_s = nullptr;       // caller stream → side: chunk c's GEMMs and chunk c+1's K* issued
-  hipEvent_t ev_t = nullptr;       // side → caller stream: chunk c's CRT + finalize done
-};
-static std::mutex g_crt_mu;
-static std::vector<std::unique_ptr<CrtSide>> g_crt;   // per device
-static std::atomic<int> g_crt_side{1};
-
-// the current device's side stream (created at the highest priority and touched once, so it is
-// bound to its hardware queue at creation: gp2d_factor_warm creates it after the factor sets)
-static int crt_side_get(CrtSide** out) {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) { set_error("crt side: no HIP device"); return -1; }
-  std::lock_guard<std::mutex> lk(g_crt_mu);
-  if ((int)g_crt.size() <= dev) g_crt.resize(dev + 1);
-  if (!g_crt[dev]) {
-    auto c = std::make_unique<CrtSide>();
-    int lo = 0, hi = 0;
-    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) { lo = 0; hi = 0; }
-    if (hipStreamCreateWithPriority(&c->st, hipStreamNonBlocking, hi) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_s, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_t, hipEventDisableTiming) != hipSuccess) {
-      set_error("crt side: stream / event creation failed"); return -1;
-    }
-    stream_touch_kernel<<<1, 64, 0, c->st>>>(0);
-    if (check_launch("stream_touch_kernel") != 0) return -1;
-    g_crt[dev] = std::move(c);
-  }
-  *out = g_crt[dev].get();
-  return 0;
-}
-
-int gp2d_ozaki_set_crt_side(int on) {
-  if (on < 0) return g_crt_side.load();
-  return g_crt_side.exchange(on ? 1 : 0);
-}
 
 // ozaki_kstar_kernel with buffer stores whenever a plane (n × 2·cp bytes) is below 2 GiB
 static void launch_kstar(dim3 grid, hipStream_t s, const double* xtr, int64_t ntr, int64_t npad, const double* xg,
@@ -1410,8 +1356,7 @@ static int predict_ozaki_impl(const int8_t* wres, const double* rowscale, int nm
                               int64_t ntr_pad, const double* xg, int64_t m, const gp2d_kernel_t* k, int var_mode,
                               double noise, int compute_var, double* mean, double* var,
                               const int64_t* out_order, int64_t chunk,
-                              int8_t* bres, uint8_t* const cres2[2], double* const pm2[2], double* const P2[2],
-                              uint8_t* flags, int* skip,
+                              int8_t* bres, uint8_t* cres, double* pm, double* P, uint8_t* flags, int* skip,
                               const int8_t* pre, size_t pre_stride, size_t pre_flags, hipStream_t s) {
   OzakiConsts oc;
   GP2D_CHECK(make_ozaki_consts(nmod, k, oc, OZ_PW, ozaki_kbits(kbits)));   // pw is in the row scales already
@@ -1426,47 +1371,11 @@ static int predict_ozaki_impl(const int8_t* wres, const double* rowscale, int nm
   const VecParams vp = make_vec_params(k);
   OzakiConsts oc_mean_only = oc;
   oc_mean_only.nmod = 0;   // mean only: K*·α without the residue planes
-  // chunk c's CRT + finalize on the side stream beside chunk c+1's GEMMs (crt_side): plane and
-  // partial set c mod 2; the caller's stream waits for chunk c−2's CRT before it overwrites them
-  const int64_t nchunks = (m + chunk - 1) / chunk;
-  CrtSide* side = nullptr;
-  if (compute_var && nchunks >= 2 && g_crt_side.load()) GP2D_CHECK(crt_side_get(&side));
-  std::unique_lock<std::mutex> side_lk;
-  if (side) side_lk = std::unique_lock<std::mutex>(side->mu);
-  struct Pending { int64_t cv, cp, c0; int b; } prev{0, 0, 0, -1};
-  auto crt_finalize = [&](const Pending& q, hipStream_t st) -> int {
-    const int64_t ncols = 2 * q.cp;
-    if (compute_var) {
-      const dim3 cgrid((unsigned)((ncols + OZ_CRT_BCOLS - 1) / OZ_CRT_BCOLS), (unsigned)npseg);
-      ozaki_crt_colsq_kernel<<<cgrid, 256, 0, st>>>(cres2[q.b], n, ncols, oc, rowscale, P2[q.b]);
-      GP2D_CHECK(check_launch("ozaki_crt_colsq_kernel"));
-    }
-    predict_finalize_kernel<<<(unsigned)((ncols + 63) / 64), 64, 0, st>>>(
-        pm2[q.b], nmseg, P2[q.b], npseg, ncols, q.cp, q.cv, q.c0, m, kss, add, clip, compute_var, mean, var, out_order);
-    return check_launch("predict_finalize_kernel");
-  };
-  // hand the previous chunk's CRT to the side stream: it starts once everything issued on s so
-  // far (that chunk's GEMMs, this chunk's K* kernel and slab lists) has run
-  auto hand_off = [&]() -> int {
-    if (hipEventRecord(side->ev_s, s) != hipSuccess || hipStreamWaitEvent(side->st, side->ev_s, 0) != hipSuccess) {
-      set_error("crt side: event record / wait failed"); return -1;
-    }
-    GP2D_CHECK(crt_finalize(prev, side->st));
-    if (hipEventRecord(side->ev_t, side->st) != hipSuccess) { set_error("crt side: event record failed"); return -1; }
-    return 0;
-  };
   int64_t ci = 0;
   for (int64_t c0 = 0; c0 < m; c0 += chunk, ++ci) {
     const int64_t cv = std::min<int64_t>(chunk, m - c0);
     const int64_t cp = round_up(cv, IBN);   // whole 256-row tiles per component half (B aliasing)
     const int64_t ncols = 2 * cp;
-    const int b = side ? (int)(ci & 1) : 0;
-    uint8_t* cres = cres2[b];
-    double* pm = pm2[b];
-    // set b was last read by chunk c−2's CRT + finalize (the latest ev_t record)
-    if (side && ci >= 2 && hipStreamWaitEvent(s, side->ev_t, 0) != hipSuccess) {
-      set_error("crt side: event wait failed"); return -1;
-    }
     const int8_t* B = pre ? pre + (size_t)ci * pre_stride : bres;
     const uint8_t* F = pre ? reinterpret_cast<const uint8_t*>(B) + pre_flags : flags;
     const size_t bplane = (size_t)ncols * n;
@@ -1482,7 +1391,6 @@ static int predict_ozaki_impl(const int8_t* wres, const double* rowscale, int nm
       ozaki_slab_list_kernel<<<(unsigned)nbj, 64, 0, s>>>(F, (int)(ntr_pad / OZ_KS_T), nbj, kslabs, slist, scnt);
       GP2D_CHECK(check_launch("ozaki_slab_list_kernel"));
     }
-    if (side && ci >= 1) GP2D_CHECK(hand_off());
     if (compute_var) {
       hipEvent_t e0 = nullptr, e1 = nullptr;
       {
@@ -1517,13 +1425,13 @@ static int predict_ozaki_impl(const int8_t* wres, const double* rowscale, int nm
         const double nv = 2.0 * (double)ntr;
         g_timing.flops.push_back(2.0 * (double)cv * nv * nv);  // FP64-equivalent algorithmic flop
       }
+      const dim3 cgrid((unsigned)((ncols + OZ_CRT_BCOLS - 1) / OZ_CRT_BCOLS), (unsigned)npseg);
+      ozaki_crt_colsq_kernel<<<cgrid, 256, 0, s>>>(cres, n, ncols, oc, rowscale, P);
+      GP2D_CHECK(check_launch("ozaki_crt_colsq_kernel"));
     }
-    prev = Pending{cv, cp, c0, b};
-    if (!side) GP2D_CHECK(crt_finalize(prev, s));
-  }
-  if (side) {   // the last chunk's CRT, and the caller's stream joins the side stream
-    GP2D_CHECK(hand_off());
-    if (hipStreamWaitEvent(s, side->ev_t, 0) != hipSuccess) { set_error("crt side: event wait failed"); return -1; }
+    predict_finalize_kernel<<<(unsigned)((ncols + 63) / 64), 64, 0, s>>>(
+        pm, nmseg, P, npseg, ncols, cp, cv, c0, m, kss, add, clip, compute_var, mean, var, out_order);
+    GP2D_CHECK(check_launch("predict_finalize_kernel"));
   }
   return 0;
 }
@@ -1549,14 +1457,11 @@ int gp2d_predict_ozaki(const int8_t* wres, const double* rowscale, int nmod, int
   GP2D_CHECK(valid_bits(0, kbits));
   const int nm = nmod;
   const int64_t ncols_max = 2 * round_up(chunk, IBN);
-  const size_t planes = (size_t)nm * n * ncols_max;
-  const size_t npm = (size_t)(n / 2 / OZ_KS_T + 1) * ncols_max, nP = (size_t)(n / OZ_CRT_ROWS + 1) * ncols_max;
   int8_t* bres = reinterpret_cast<int8_t*>(work);
-  uint8_t* const cres[2] = {reinterpret_cast<uint8_t*>(bres + planes), reinterpret_cast<uint8_t*>(bres + 2 * planes)};
-  double* const pm[2] = {reinterpret_cast<double*>(bres + 3 * planes),
-                         reinterpret_cast<double*>(bres + 3 * planes) + npm + nP};
-  double* const P[2] = {pm[0] + npm, pm[1] + npm};
-  uint8_t* flags = reinterpret_cast<uint8_t*>(pm[1] + npm + nP);
+  uint8_t* cres = reinterpret_cast<uint8_t*>(bres + (size_t)nm * n * ncols_max);
+  double* pm = reinterpret_cast<double*>(cres + (size_t)nm * n * ncols_max);
+  double* P = pm + (size_t)(n / 2 / OZ_KS_T + 1) * ncols_max;
+  uint8_t* flags = reinterpret_cast<uint8_t*>(P + (size_t)(n / OZ_CRT_ROWS + 1) * ncols_max);
   int* skip = reinterpret_cast<int*>(flags + oz_flag_bytes(n, chunk));
   return predict_ozaki_impl(wres, rowscale, nmod, kbits, n, alpha, xtr, ntr, ntr_pad, xg, m, k, var_mode, noise,
                             compute_var, mean, var, out_order, chunk, bres, cres, pm, P, flags, skip, nullptr, 0, 0,
@@ -1624,8 +1529,8 @@ int gp2d_ozaki_kstar(const double* xtr, int64_t ntr, int64_t ntr_pad, const doub
 static size_t predict_ozaki_planes_ws(int64_t n, int64_t chunk, int nm) {
   if (nm <= 0 || n <= 0) return 0;
   const int64_t ncols = 2 * round_up(chunk < 1 ? 1 : chunk, IBN);
-  return 2 * ((size_t)nm * (size_t)n * (size_t)ncols + sizeof(double) * ozaki_partials(n) * (size_t)ncols) +
-         oz_list_bytes(n, chunk);   // two plane + partial sets (crt_side)
+  return (size_t)nm * (size_t)n * (size_t)ncols + sizeof(double) * ozaki_partials(n) * (size_t)ncols +
+         oz_list_bytes(n, chunk);
 }
 
 size_t gp2d_predict_ozaki_planes_workspace(int64_t n, int64_t chunk) {
@@ -1651,14 +1556,10 @@ int gp2d_predict_ozaki_planes(const int8_t* wres, const double* rowscale, int nm
     return -3;
   }
   const int64_t ncols_max = 2 * round_up(chunk, IBN);
-  const size_t cplanes = (size_t)nmod * n * ncols_max;
-  const size_t npm = (size_t)std::max<int64_t>(n / 2 / OZ_KS_T + 1, n / OZ_CRT_ROWS + 1) * ncols_max;
-  const size_t nP = (size_t)(n / OZ_CRT_ROWS + 1) * ncols_max;
-  uint8_t* const cres[2] = {reinterpret_cast<uint8_t*>(work), reinterpret_cast<uint8_t*>(work) + cplanes};
-  double* const pm[2] = {reinterpret_cast<double*>(cres[1] + cplanes),
-                         reinterpret_cast<double*>(cres[1] + cplanes) + npm + nP};
-  double* const P[2] = {pm[0] + npm, pm[1] + npm};
-  int* skip = reinterpret_cast<int*>(pm[1] + npm + nP);
+  uint8_t* cres = reinterpret_cast<uint8_t*>(work);
+  double* pm = reinterpret_cast<double*>(cres + (size_t)nmod * n * ncols_max);
+  double* P = pm + (size_t)std::max<int64_t>(n / 2 / OZ_KS_T + 1, n / OZ_CRT_ROWS + 1) * ncols_max;
+  int* skip = reinterpret_cast<int*>(P + (size_t)(n / OZ_CRT_ROWS + 1) * ncols_max);
   const size_t planes = (size_t)nmod_b * (size_t)n * (size_t)ncols_max;
   const size_t stride = planes + oz_flag_bytes(n, chunk);
   return predict_ozaki_impl(wres, rowscale, nmod, kbits, n, alpha, xtr, ntr, ntr_pad, xg, m, k, var_mode, noise, 1, mean,

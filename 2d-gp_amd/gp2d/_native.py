@@ -12,7 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GP2D_LIB", os.path.join(_HERE, "libgp2d.so"))
-ABI_VERSION = 12         # GP2D_ABI_VERSION in include/gp2d.h
+ABI_VERSION = 11         # GP2D_ABI_VERSION in include/gp2d.h
 
 FAMILY_VECTOR2D, FAMILY_ARD_RBF, FAMILY_VECTOR_ST = 0, 1, 2
 KIND_SCALAR, KIND_DIVFREE, KIND_CURLFREE, KIND_MIXED = 0, 1, 2, 3
@@ -31,7 +31,7 @@ EXPORTS = (
     "gp2d_ozaki_guard_workspace", "gp2d_ozaki_guard", "gp2d_ozaki_error_model", "gp2d_ozaki_guard_bits",
     "gp2d_predict_ozaki_workspace", "gp2d_predict_ozaki_workspace_nmod",
     "gp2d_predict_ozaki", "gp2d_ozaki_nmod_apriori", "gp2d_ozaki_kstar_bytes", "gp2d_ozaki_kstar",
-    "gp2d_predict_ozaki_planes_workspace", "gp2d_predict_ozaki_planes", "gp2d_ozaki_set_skip", "gp2d_ozaki_set_crt_side", "gp2d_morton_codes",
+    "gp2d_predict_ozaki_planes_workspace", "gp2d_predict_ozaki_planes", "gp2d_ozaki_set_skip", "gp2d_morton_codes",
     "gp2d_morton_sort_workspace", "gp2d_morton_sort", "gp2d_gather_rows", "gp2d_obs_pad", "gp2d_lml", "gp2d_lml_grad_count",
     "gp2d_lml_grad_workspace", "gp2d_lml_grad",
     "gp2d_kernel_grad_count", "gp2d_kernel_grad_workspace", "gp2d_kernel_grad",
@@ -119,7 +119,6 @@ _SIGS = {
     "gp2d_predict_ozaki_workspace": (_SZ, [_I64, _I64]),
     "gp2d_predict_ozaki_workspace_nmod": (_SZ, [_I64, _I64, _I]),
     "gp2d_ozaki_set_skip": (None, [_I]),
-    "gp2d_ozaki_set_crt_side": (_I, [_I]),
     "gp2d_morton_codes": (_I, [_P, _I64, _I, _P, _P, _P]),
     "gp2d_morton_sort_workspace": (_SZ, [_I64]),
     "gp2d_morton_sort": (_I, [_P, _I64, _I, _P, _P, _P, _SZ, _P]),

@@ -83,9 +83,6 @@ def parse():
                          "non-root ranks wait for the factor broadcast (N>1, bcast)")
     ap.add_argument("--oz-skip", type=int, default=1,
                     help="ozaki: skip the all-zero K* slabs in the int8 GEMMs (exact; 0 = dense, for A/B)")
-    ap.add_argument("--crt-side", type=int, default=1,
-                    help="ozaki: each chunk's CRT pass on the library's side stream beside the next chunk's "
-                         "int8 GEMMs (bit-identical; 0 = every chunk in order on the predict stream, for A/B)")
     ap.add_argument("--pipeline", type=int, default=1,
                     help="issue each job's fit on a second stream, so job i+1's fit runs while job i's predict "
                          "does (the steps are independent fit+predict jobs, like the reference's per-time-window "
@@ -463,7 +460,6 @@ def main():
     from gp2d import distributed as GD
     from gp2d import engine as E
     E.N.lib().gp2d_ozaki_set_skip(int(args.oz_skip))
-    E.N.lib().gp2d_ozaki_set_crt_side(int(args.crt_side))
 
     G = args.grid
     x1, x2, u, v = D.synthetic_tracks(args.ntrain, seed=2016)

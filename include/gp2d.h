@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define GP2D_ABI_VERSION 12
+#define GP2D_ABI_VERSION 11
 
 /* kernel families */
 #define GP2D_FAMILY_VECTOR2D 0   /* 2×2 matrix-valued SE kernels on (x1, x2)          */
@@ -106,8 +106,8 @@ int gp2d_assemble(const double* xa, int64_t na, int64_t na_pad,
  * next k caller streams get sets 0..k−1 in order of first use.                       */
 int gp2d_factor_sets(int k);
 /* gp2d_factor_warm(k, stream): put one empty kernel on `stream` (the caller's predict stream),
- *   then create the current device's internal factor stream sets 0..k−1 and the predict's CRT
- *   stream (gp2d_ozaki_set_crt_side) and put one empty kernel on each of their streams.  HIP binds a stream to a hardware queue at its first command; on
+ *   then create the current device's internal factor stream sets 0..k−1 and put one empty kernel
+ *   on each of their streams.  HIP binds a stream to a hardware queue at its first command; on
  *   one MI355X a job stream ran 53.1–53.9 ms per headline job when its predict stream, then the
  *   factor streams, then its side streams were first used in that order, and 56.4–56.7 ms in the
  *   other orders measured (tools/probe_first_fit.py, DESIGN.md §6 "bench state").
@@ -241,14 +241,6 @@ size_t gp2d_predict_ozaki_workspace_nmod(int64_t n, int64_t chunk, int nmod);
  * a 256-row grid tile — exact, such slabs add nothing.  gp2d_ozaki_set_skip(0) runs them
  * dense (A/B measurement and the bit-identity test); default on.                       */
 void   gp2d_ozaki_set_skip(int on);
-/* With two or more chunks, the predict runs chunk c's CRT (the residue planes → Σ V² pass) and
- * output finalisation on an internal stream per device (highest priority, created by
- * gp2d_factor_warm after the factor sets) beside chunk c+1's int8 GEMMs, joined back to `stream`
- * before the call's last work: the memory-bound CRT shares the CUs with the MFMA-bound GEMMs
- * (DESIGN.md §3).  The workspace holds two plane and partial sets for it.  Results are bit-identical
- * either way; gp2d_ozaki_set_crt_side(0) runs every chunk in order on `stream` (A/B and tests).
- * Returns the previous setting (default 1); a negative argument only queries.                  */
-int    gp2d_ozaki_set_crt_side(int on);
 /* Z-order (Morton) codes of n points (dim 2 or 3) in their bounding box, 21 bits per
  * coordinate (bbox: 6 doubles of device scratch).  The ozaki engine sorts training and grid
  * points by these codes so that all-zero K* tiles cluster into skippable slabs.          */

@@ -238,50 +238,6 @@ def test_zero_slab_skip_is_exact(kind, l):
     assert rel(vs[idx], vo) < 1e-10 and rel(ms[idx], mo) < 1e-10
 
 
-def test_crt_side_stream_is_exact():
-    """Chunk c's CRT + finalize on the library's side stream beside chunk c+1's GEMMs
-    (gp2d_ozaki_set_crt_side, the default): bit-identical to every chunk in order on the caller's
-    stream — an odd chunk count with a ragged last chunk, the K*-planes-ahead entry, and two
-    predicts issued at once from two streams (they share the side stream and its two events)."""
-    rng = np.random.default_rng(53)
-    n, m = 900, 4700                      # chunk 512: 10 chunks, the last one 92 points
-    x = np.stack([rng.uniform(0, 80, n), rng.uniform(0, 60, n)], 1)
-    y = np.concatenate([np.sin(x[:, 1] / 9), np.cos(x[:, 0] / 11)]) + rng.normal(0, 0.05, 2 * n)
-    xg = np.stack([rng.uniform(-5, 85, m), rng.uniform(-5, 65, m)], 1)
-    ks = E.KernelSpec(kind="df", l_df=5.0)
-    gp = E.fit(ks, x, y, noise=0.0025, variance="ozaki")
-    L = E.N.lib()
-    assert L.gp2d_ozaki_set_crt_side(-1) == 1           # the default
-    ms, vs = (t.cpu().numpy() for t in E.predict(gp, xg, chunk=512))
-    _, _, ma, va = _ahead(ks, x, y, xg, 0.0025, 512)
-    prev = L.gp2d_ozaki_set_crt_side(0)
-    try:
-        assert prev == 1 and L.gp2d_ozaki_set_crt_side(-1) == 0
-        md, vd = (t.cpu().numpy() for t in E.predict(gp, xg, chunk=512))
-        _, _, mad, vad = _ahead(ks, x, y, xg, 0.0025, 512)
-    finally:
-        L.gp2d_ozaki_set_crt_side(1)
-    assert np.array_equal(ms, md) and np.array_equal(vs, vd)
-    assert np.array_equal(ma, mad) and np.array_equal(va, vad)
-    assert np.array_equal(ma, ms) and np.array_equal(va, vs)
-    dev = torch.device("cuda", torch.cuda.current_device())
-    xgd = torch.tensor(xg, device=dev)
-    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
-    s1.wait_stream(torch.cuda.current_stream(dev))
-    s2.wait_stream(torch.cuda.current_stream(dev))
-    with torch.cuda.stream(s1):
-        o1 = E.predict(gp, xgd, chunk=512)
-    with torch.cuda.stream(s2):
-        o2 = E.predict(gp, xgd, chunk=512)
-    torch.cuda.synchronize()
-    for mu, var in (o1, o2):
-        assert np.array_equal(mu.cpu().numpy(), ms) and np.array_equal(var.cpu().numpy(), vs)
-    sub = np.random.default_rng(4).choice(m, 300, replace=False)
-    mo, vo = O.fit_predict(x, y, xg[sub], kind="df", l_df=5.0, noise=0.0025)
-    idx = np.concatenate([sub, m + sub])
-    assert rel(vs[idx], vo) < 1e-10 and rel(ms[idx], mo) < 1e-10
-
-
 def test_zero_slab_skip_far_grid_and_planes():
     """A grid block far from every observation: every K slab is skipped (empty list), so the
     variance is exactly the prior kss and the mean exactly 0; the K*-planes-ahead path (block

@@ -24,7 +24,7 @@ def test_library_exports_every_header_symbol():
     for s in syms:
         assert hasattr(L, s), s
     assert set(syms) == set(_native.EXPORTS)
-    assert L.gp2d_abi_version() == _native.ABI_VERSION == 12
+    assert L.gp2d_abi_version() == _native.ABI_VERSION == 11
     assert L.gp2d_padded_points(1) == 64 and L.gp2d_padded_points(64) == 64 and L.gp2d_padded_points(65) == 128
 
 
