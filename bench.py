@@ -654,7 +654,11 @@ def main():
     barrier(ws)
     ts = time.perf_counter()
     for _ in range(reps):
-        run_jobs(1) if stream is not None else step()
+        if stream is not None:
+            run_jobs(1)
+        else:   # step(): its fit must wait for the previous job's predict (no overlap across reps)
+            cfg["first"] = True
+            step()
     barrier(ws)
     dts = torch.tensor([time.perf_counter() - ts], dtype=torch.float64, device=dev)
     if is_multi(ws):
